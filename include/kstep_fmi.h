@@ -1,0 +1,177 @@
+/*
+ * kstep_fmi.h -- C ABI of the MI355X k-step FM-index backward-search engine
+ * (libkstepfmi.so, built from k-step_fm-index_amd/).
+ *
+ * Section 1 is the reference's own link-time plugin interface
+ * (/root/reference/common/interface.h:27-41) plus the common.h helpers its
+ * driver calls (/root/reference/common/common.h:87-96): a program written
+ * against the reference (common/searchQueries.c) links against this library
+ * instead of common.c + fmIndexCPUBaseline*.c + one fmIndexGPU-*.cu file, and
+ * runs unchanged.  All handles are opaque `void *`; every
+ * size that can exceed 2^32 bytes is 64-bit internally (reference defect B7).
+ *
+ * Section 2 holds the extensions that the reference fixes at compile time
+ * (backend, device, K, d) or does not have (memory-resident handles, status
+ * queries, timing, the GPU index builder).  Plain C types only.
+ *
+ * Error codes are the reference's error_t (common.h:36-62); the index-tag
+ * codes 100/101/200/201 mean "this backend needs an index with that tag".
+ */
+#ifndef KSTEP_FMI_H_
+#define KSTEP_FMI_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* error_t values, common.h:36-62 */
+enum {
+  KFMI_SUCCESS                = 0,
+  KFMI_E_OPENING_INDEX_FILE   = 1,
+  KFMI_E_ALLOCATING_BWT       = 2,
+  KFMI_E_ALLOCATING_FMI       = 3,
+  KFMI_E_READING_BWT          = 4,
+  KFMI_E_READING_FMI          = 5,
+  KFMI_E_SAVING_INDEX_FILE    = 6,
+  KFMI_E_SAVING_BWT_FILE      = 7,
+  KFMI_E_BUILDING_BWT         = 8,
+  KFMI_E_BUILDING_FMI         = 9,
+  KFMI_E_OPENING_REFERENCE_FILE = 10,
+  KFMI_E_ALLOCATING_REFERENCE = 11,
+  KFMI_E_READING_MFASTA_FILE  = 12,
+  KFMI_E_READING_REFERENCE_FILE = 13,
+  KFMI_E_OPENING_MFASTA_FILE  = 14,
+  KFMI_E_ALLOCATING_MFASTA    = 15,
+  KFMI_E_ALLOCATING_RESULTS   = 16,
+  KFMI_E_OPENING_RESULTS_FILE = 17,
+  KFMI_E_READING_RESULTS_FILE = 18,
+  KFMI_E_NOT_IMPLEMENTED      = 19,
+  /* extensions (not in the reference) */
+  KFMI_E_NO_DEVICE            = 30,  /* no HIP device / HIP runtime error      */
+  KFMI_E_DEVICE_ALLOC         = 31,  /* hipMalloc failed                        */
+  KFMI_E_KERNEL               = 32,  /* kernel launch / execution failed        */
+  KFMI_E_BAD_ARGUMENT         = 33,  /* unsupported K, d, query size, backend   */
+  KFMI_E_NOT_ON_DEVICE        = 34,  /* search called before transferCPUtoGPU   */
+  KFMI_INDEX_VER_BASELINE      = 100,
+  KFMI_INDEX_VER_INTERLEAVE    = 101,
+  KFMI_INDEX_VER_BASELINE_AC   = 200,
+  KFMI_INDEX_VER_INTERLEAVE_AC = 201
+};
+
+/* ===================== 1. reference entry points ======================== */
+
+/* interface.h:27 / fmIndexCPUBaseline.c:71-143.  Reads any index tag
+ * (100/101/200/201).  With KFMI_STRICT_TAG=1 in the environment it behaves
+ * exactly like the reference loader of the selected backend: a file with
+ * another tag is rejected and the required tag is returned. */
+int32_t loadIndex(const char *fn, void **index);
+/* interface.h:28 / genFMindex.c:155-181: "<fn>.<n>.<d>fmi<K>steps.fmi" (tag 100),
+ * or the index's own tag/name suffix for transformed indexes. */
+int32_t saveIndex(const char *fn, void *index);
+/* interface.h:29 / common.c:248-260: 2*numresults u32, zeroed. */
+int32_t initResults(uint32_t numresults, void **results);
+/* interface.h:31 / fmIndexGPU-*.cu searchIndexGPU: synchronous search of every
+ * query on the device; results stay on the device until transferGPUtoCPU.
+ * Returns void like the reference; kfmi_last_error() gives the status. */
+void    searchIndexGPU(void *index, void *queries, void *resIntervals);
+/* interface.h:33 / fmIndexCPUBaseline.c:145-155 */
+int32_t freeIndex(void **index);
+/* interface.h:34 / common.c:313-322 */
+int32_t freeReference(void **reference, void **index);
+/* interface.h:35 / genFMindex.c:457-543: tag-100 index of a loadRef() text,
+ * K and d from KFMI_K / KFMI_D (defaults 2 / 64); built on the GPU when one
+ * is present (kfmi_build_index_gpu), else on the host. */
+int32_t buildIndex(void *reference, void **index);
+/* interface.h:36-41 / e.g. fmIndexGPU-Coop-2Step.cu:231-338 */
+int32_t freeQueriesGPU(void **queries);
+int32_t freeResultsGPU(void **results);
+int32_t freeIndexGPU(void **index);
+int32_t transferGPUtoCPU(void *results);
+int32_t transferCPUtoGPU(void *index, void *queries, void *results);
+
+/* common.h:87-96 / common.c */
+double   sampleTime(void);
+uint32_t base2index(uint32_t base);
+int32_t  loadRef(const char *fn, uint32_t refsize, void **reference);
+int32_t  saveRef(const char *fn, void *reference);
+int32_t  loadQueries(const char *fn, uint32_t sizequery, uint32_t numqueries, void **queries);
+int32_t  writeResults(const char *fn, uint32_t *results, uint32_t numqueries);
+int32_t  loadResults(const char *fn, void **results);
+int32_t  freeQueries(void **queries);
+int32_t  freeResults(void **results);
+/* common.c:324-341: "<fn>.res.gpu" */
+int32_t  saveResults(const char *fn, void *results, void *index);
+char    *errorCommon(int32_t e);
+
+/* ========================= 2. extensions ================================= */
+
+/* Backends (the reference selects one per binary at link time,
+ * makefile:177-207).  Names:
+ *   "task"        Task-{1,2}Step   : one thread per query, L and R ends      (tag 101 semantics)
+ *   "coop"        Coop-{1,2}Step   : wave64 cooperative gather into LDS     (tag 101 semantics)
+ *   "task-ac"     Task-2Step-AltCounters                                    (tag 201 semantics)
+ *   "coop-ac"     Coop-2Step-AltCounters                                    (tag 201 semantics)
+ *   "task-packed" task-per-query on the 64-byte-line packed layout          (tag 101 semantics)
+ *   "coop-packed" wave64 cooperative gather on the packed layout            (tag 101 semantics)
+ * The default comes from KFMI_BACKEND, else "task-packed".  An index of any tag
+ * is accepted and re-laid-out on upload; an AC backend applied to a tag-100/101
+ * file first runs the tfmiAC transform, so its results are those of the
+ * AltCounters searcher on that file. */
+int32_t     kfmi_set_backend(const char *name);
+const char *kfmi_get_backend(void);
+/* The HIP device used by the calling thread (reference: compile-time DEVICE).
+ * Default: KFMI_DEVICE, else 0. */
+int32_t     kfmi_set_device(int32_t device);
+int32_t     kfmi_device_count(void);
+/* Status of the last searchIndexGPU() on this thread. */
+int32_t     kfmi_last_error(void);
+/* searchIndexGPU with a status return. */
+int32_t     kfmi_search(void *index, void *queries, void *results);
+/* Device-side timing of the last search, from HIP events on the library's
+ * stream: total (pack + LF), query packing, and the LF kernel alone (ms). */
+int32_t     kfmi_last_timing(double *ms_total, double *ms_pack, double *ms_lf);
+
+/* Strict loader: as the reference, rejects a tag other than `required_tag`
+ * and returns that tag (common.c:304-307 turns it into a hint). */
+int32_t kfmi_load_index_tag(const char *fn, uint32_t required_tag, void **index);
+/* Index from an in-memory file image (header + entries); the bytes are copied. */
+int32_t kfmi_index_from_image(const void *image, uint64_t bytes, void **index);
+/* Serialised file image of an index (header + entries); pointer owned by the index. */
+int32_t kfmi_index_image(void *index, const void **image, uint64_t *bytes);
+/* Header fields: out[0..5] = tag, steps, bwtsize, ncounters, nentries, chunk;
+ * out[6..9] dollarPositionBWT; out[10..13] dollarBaseBWT. */
+int32_t kfmi_index_header(void *index, uint32_t *out14);
+
+/* Layout transforms (transformIndexBitmaps.c:269-295, transformIndexAlternateCounters.c:387-479). */
+int32_t kfmi_transform_interleave(void *index100, void **index101);
+int32_t kfmi_transform_ac(void *index100, void **index200, void **index201);
+
+/* Queries/results handles over caller memory-resident data (the FFI form of
+ * loadQueries/initResults).  `ascii` is num*size bytes, query q at q*size. */
+int32_t   kfmi_queries_from_buffer(const char *ascii, uint64_t num, uint32_t size, void **queries);
+int32_t   kfmi_results_alloc(uint64_t num, void **results);
+uint32_t *kfmi_results_host(void *results);      /* 2*num u32, [L0,R0,L1,R1,...] */
+uint64_t  kfmi_results_num(void *results);
+
+/* Index construction (genFMindex.c:457-543) from an ACGT text of n bases.
+ * _gpu: suffix sort and all layout passes on the device; the tag-100 host
+ * image is produced as well when `want_host_image` != 0 (needed for
+ * saveIndex / md5 pinning / the CPU oracle).  Returns a tag-100 index. */
+int32_t kfmi_build_index_cpu(const char *text, uint64_t n, uint32_t k, uint32_t d, void **index);
+int32_t kfmi_build_index_gpu(const char *text, uint64_t n, uint32_t k, uint32_t d,
+                             int32_t want_host_image, void **index);
+
+/* Dedup-aware algorithmic traffic of the last search: sum over queries and
+ * steps of distinct d-blocks touched (1 if L/d == R/d else 2), SURVEY 8(d). */
+int32_t kfmi_count_blocks(void *index, void *queries, uint64_t *blocks);
+
+/* Bytes of the device-resident index for the current backend. */
+uint64_t kfmi_device_index_bytes(void *index);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* KSTEP_FMI_H_ */

@@ -1,0 +1,176 @@
+/*
+ * kfmi_coop.h -- wave64-cooperative backward search (the reference's
+ * Coop-{1,2}Step and Coop-2Step-AltCounters, fmIndexGPU-Coop-2Step.cu:147-228,
+ * re-designed for CDNA4 instead of translated):
+ *
+ *  - one lane owns one query (both interval ends); a wave serves 64 queries;
+ *  - per K-step every lane posts its L request and, only when R lies in a
+ *    different d-block, an R request.  The R requests are compacted with a
+ *    64-bit ballot + mbcnt (prefix popcount) so a wave issues 64 + popc(ballot)
+ *    requests instead of 128;
+ *  - TPR lanes fetch one request's Occ block (bit planes + the one 16-byte
+ *    counter chunk it needs) with `global_load_lds_dwordx4`, straight from HBM
+ *    into LDS (no VGPR staging); the 64/TPR requests of one round land as one
+ *    contiguous 1 KiB piece;
+ *  - after one vmcnt(0) every lane computes its own LF from its LDS slots.
+ *
+ * Results are identical to task_kernel (same lf math), hence to the CPU oracle.
+ */
+#ifndef KFMI_COOP_H_
+#define KFMI_COOP_H_
+
+#include "kfmi_device.h"
+
+namespace kfmi {
+
+template <class G>
+struct CoopCfg {
+  static constexpr int BC = G::BMW / 4;                 // 16-byte bitmap chunks per block
+  static constexpr int TPR = pow2ceil(BC + 1);          // lanes per request (+1 counter chunk)
+  static constexpr int RPR = 64 / TPR;                  // requests per round
+  static constexpr int SLOT = TPR * 16;                 // LDS bytes per request slot
+  static constexpr int MAXREQ = 128;                    // 64 L + up to 64 R
+  static constexpr int WAVE_LDS = MAXREQ * SLOT + MAXREQ * 4;
+  static constexpr int WPB0 = 65536 / WAVE_LDS;
+  static constexpr int WPB = WPB0 < 1 ? 1 : (WPB0 > 4 ? 4 : WPB0);   // waves per block
+  static constexpr bool OK = (G::BMW % 4 == 0) && (G::EW % 4 == 0) && (G::BOFF % 4 == 0) &&
+                             (G::LAY != LAY_AC || G::HALF >= 4) && TPR <= 64;
+};
+
+// byte address of chunk k of request (b, c)
+template <class G>
+__device__ __forceinline__ const uint8_t* coop_chunk_addr(const IdxArgs& ix, uint32_t b, uint32_t c, int k)
+{
+  using C = CoopCfg<G>;
+  const uint8_t* base = reinterpret_cast<const uint8_t*>(ix.ent);
+  const uint64_t eb = (uint64_t) b * (G::EW * 4);
+  if (k < C::BC) return base + eb + (G::BOFF + 4 * k) * 4;
+  if constexpr (G::LAY == LAY_INTER) {
+    return base + eb + (G::BMW + (c & ~3u)) * 4;
+  } else if constexpr (G::LAY == LAY_AC) {
+    const bool e = ((b & 1u) != 0) == (c < (uint32_t) G::HALF);
+    return base + (uint64_t) (b + (e ? 1u : 0u)) * (G::EW * 4) + ((c & (G::HALF - 1)) & ~3u) * 4;
+  } else {
+    return base + eb + 4 * G::BMW + 2 * (c & ~7u);
+  }
+}
+
+template <class G>
+__device__ __forceinline__ uint32_t coop_lf(const IdxArgs& ix, const uint8_t* slot, uint32_t b, uint32_t X,
+                                            uint32_t c, const uint32_t (&sx)[2 * G::K], uint32_t sbase)
+{
+  using C = CoopCfg<G>;
+  const int o = (int) (X - b * (uint32_t) G::D);
+  bool e = false;
+  if constexpr (G::LAY == LAY_AC) e = ((b & 1u) != 0) == (c < (uint32_t) G::HALF);
+  uint32_t pop = 0;
+#pragma unroll
+  for (int k = 0; k < C::BC; ++k) {
+    const uint4 v = *reinterpret_cast<const uint4*>(slot + 16 * k);
+    const uint32_t pl[4] = {v.x, v.y, v.z, v.w};
+    // K=2: one 32-row word per chunk; K=1: two words per chunk
+#pragma unroll
+    for (int h = 0; h < 4 / G::PW; ++h) {
+      const int w = k * (4 / G::PW) + h;
+      uint32_t m = row_mask(o - 32 * w);
+      if constexpr (G::LAY == LAY_AC) m = e ? ~m : m;
+      pop += __popc(m & select_rows<G::K>(&pl[h * G::PW], sx));
+    }
+  }
+  uint32_t cnt;
+  if constexpr (G::LAY == LAY_PACKED)
+    cnt = sbase + reinterpret_cast<const uint16_t*>(slot + 16 * C::BC)[c & 7u];
+  else
+    cnt = reinterpret_cast<const uint32_t*>(slot + 16 * C::BC)[c & 3u];
+  const int corr = dollar_fix<G::K, G::LAY == LAY_AC>(ix.dl, b, c, X, e);
+  const uint32_t bc = pop - (uint32_t) corr;
+  if constexpr (G::LAY == LAY_AC) return e ? cnt - bc : cnt + bc;
+  return cnt + bc;
+}
+
+template <class G>
+__global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, const uint32_t* __restrict__ qp,
+                                                                    uint64_t num, uint32_t steps, uint32_t nwords,
+                                                                    uint32_t* __restrict__ res)
+{
+  using C = CoopCfg<G>;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  uint8_t* wl = lds + wave * C::WAVE_LDS;
+  uint32_t* tab = reinterpret_cast<uint32_t*>(wl + C::MAXREQ * C::SLOT);
+  const uint64_t q0 = ((uint64_t) blockIdx.x * C::WPB + wave) * 64;
+  if (q0 >= num) return;                       // whole wave idle (wave-uniform)
+  const uint64_t q = q0 + lane;
+  const uint64_t qs = q < num ? q : num - 1;   // tail lanes replay a valid query, never stored
+  const int k = lane % C::TPR;
+  const int g = lane / C::TPR;
+  uint32_t L = 0, R = ix.bwtsize;
+  constexpr int S = sb_shift_for(G::D);
+
+  for (uint32_t w = 0; w < nwords; ++w) {
+    const uint32_t word = qp[(uint64_t) w * num + qs];
+    const uint32_t left = steps - w * G::SPW;
+#pragma unroll 1
+    for (int j = 0; j < G::SPW; ++j) {
+      if ((uint32_t) j >= left) break;
+      const uint32_t c = (word >> (2 * G::K * j)) & (uint32_t) (G::NC - 1);
+      const uint32_t bl = L / (uint32_t) G::D, br = R / (uint32_t) G::D;
+      const bool needR = br != bl;
+      const uint64_t mask = __ballot(needR);
+      const uint32_t nreq = 64u + (uint32_t) __popcll(mask);
+      const uint32_t slotR = 64u + __builtin_amdgcn_mbcnt_hi((uint32_t) (mask >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t) mask, 0u));
+      tab[lane] = bl * (uint32_t) G::NC + c;
+      if (needR) tab[slotR] = br * (uint32_t) G::NC + c;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      uint32_t sbL = 0, sbR = 0;
+      if constexpr (G::LAY == LAY_PACKED) {
+        sbL = ix.sb[(uint64_t) (bl >> S) * G::NC + c];
+        sbR = ix.sb[(uint64_t) (br >> S) * G::NC + c];
+      }
+      const uint32_t rounds = (nreq + C::RPR - 1) / C::RPR;
+      for (uint32_t r = 0; r < rounds; ++r) {
+        const uint32_t s = r * C::RPR + g;
+        if (s < nreq && k <= C::BC) {
+          const uint32_t desc = tab[s];
+          const uint32_t b = desc / (uint32_t) G::NC, cc = desc % (uint32_t) G::NC;
+          const uint8_t* src = coop_chunk_addr<G>(ix, b, cc, k);
+          __builtin_amdgcn_global_load_lds((const void*) src,
+                                           (__attribute__((address_space(3))) void*) (wl + r * 1024), 16, 0, 0);
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      uint32_t sx[2 * G::K];
+      plane_xor<G::K>(c, sx);
+      const uint32_t nL = coop_lf<G>(ix, wl + lane * C::SLOT, bl, L, c, sx, sbL);
+      const uint32_t nR = coop_lf<G>(ix, wl + (needR ? slotR : (uint32_t) lane) * C::SLOT, br, R, c, sx,
+                                     needR ? sbR : sbL);
+      L = nL;
+      R = nR;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+  }
+  if (q < num) *reinterpret_cast<uint2*>(res + 2 * q) = make_uint2(L, R);
+}
+
+template <class G>
+hipError_t coop_launch(hipStream_t st, IdxArgs ix, const uint32_t* qp, uint64_t num, uint32_t steps,
+                       uint32_t nwords, uint32_t* res)
+{
+  using C = CoopCfg<G>;
+  if constexpr (!C::OK) {
+    return hipErrorInvalidValue;
+  } else {
+    const uint64_t waves = (num + 63) / 64;
+    const uint64_t blocks = (waves + C::WPB - 1) / C::WPB;
+    const size_t lds = (size_t) C::WPB * C::WAVE_LDS;
+    hipLaunchKernelGGL((coop_kernel<G>), dim3((uint32_t) blocks), dim3(64 * C::WPB), lds, st, ix, qp, num, steps,
+                       nwords, res);
+    return hipGetLastError();
+  }
+}
+
+}  // namespace kfmi
+
+#endif  // KFMI_COOP_H_

@@ -1,0 +1,248 @@
+/*
+ * kfmi_device.h -- device-side geometry and LF-mapping math for gfx950.
+ *
+ * One LF step of one interval end X with K-mer code c (the reference's
+ * searchIndexCPU inner loop, fmIndexCPUBaseline.c:205-286):
+ *   b = X / d, o = X % d
+ *   X' = cnt_b[c] + popc( first-o-rows-mask & AND_{s<K} sel(plane_{s,0}, c_s.bit0) & sel(plane_{s,1}, c_s.bit1) )
+ *        - #{s : D_s/d == b, c == dollarBase_s, X > D_s}
+ * AltCounters (fmIndexCPUBaseline-AltCounters.c:218-303): when
+ *   e = (b odd & c < NC/2) | (b even & c >= NC/2)
+ * the counter comes from entry b+1 and the popcount runs over the inverted
+ * mask and is subtracted; the $ rule flips to X <= D_s.
+ *
+ * Device layouts (one per backend family; see DESIGN.md "Data layout in HBM"):
+ *   LAY_INTER  : tag-101 entries as in the file, [planes(w,s,t) | cnt[NC]] u32
+ *   LAY_AC     : tag-201 entries as in the file, [cnt_half[NC/2] | planes(w,s,t)]
+ *   LAY_PACKED : one power-of-two line per d-block, [planes(w,s,t) | u16 delta[NC]],
+ *                cnt_b[c] = sb[b >> SB_SHIFT][c] + delta_b[c] (sb: small, cache-resident).
+ *                K=2, d=64 -> exactly one 64-byte line per LF.
+ */
+#ifndef KFMI_DEVICE_H_
+#define KFMI_DEVICE_H_
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace kfmi {
+
+enum Layout : int { LAY_INTER = 0, LAY_AC = 1, LAY_PACKED = 2 };
+
+__host__ __device__ constexpr int pow2ceil(int x) { int p = 1; while (p < x) p <<= 1; return p; }
+
+template <int K_, int NB_, int LAY_>
+struct Geo {
+  static constexpr int K = K_;
+  static constexpr int NB = NB_;                 // 32-row words per block
+  static constexpr int LAY = LAY_;
+  static constexpr int D = 32 * NB;              // rows per block (d)
+  static constexpr int NC = 1 << (2 * K);        // counters (4^K)
+  static constexpr int HALF = NC / 2;
+  static constexpr int PW = 2 * K;               // planes per 32-row word
+  static constexpr int BMW = PW * NB;            // bitmap words per entry
+  // u32 words per entry
+  static constexpr int EW = LAY == LAY_INTER ? BMW + NC
+                          : LAY == LAY_AC    ? HALF + BMW
+                          : pow2ceil(BMW + NC / 2);
+  static constexpr int BOFF = LAY == LAY_AC ? HALF : 0;   // first bitmap word
+  static constexpr int DELTA16 = 2 * BMW;                 // first u16 delta (packed)
+  static constexpr int SPW = 32 / (2 * K);                // K-steps per packed query word
+  static constexpr bool SMALL = BMW <= 16;                // whole bitmap fits in registers
+};
+
+// Superblock shift of the packed layout: the largest S with (2^S - 1) * d <= 65535.
+__host__ __device__ constexpr int sb_shift_for(int d)
+{
+  int s = 0;
+  while (((1 << (s + 1)) - 1) * d <= 65535) ++s;
+  return s;
+}
+
+struct DollarArgs {
+  uint32_t dpos[2];   // dollarPositionBWT[s]
+  uint32_t dbase[2];  // dollarBaseBWT[s]
+  uint32_t dblk[2];   // dollarPositionBWT[s] / d (modposdollarBWT)
+};
+
+struct IdxArgs {
+  const uint32_t* __restrict__ ent;   // entries (layout per backend)
+  const uint32_t* __restrict__ sb;    // packed layout: superblock counters [nsb][NC]
+  uint32_t bwtsize;
+  uint32_t pad_;
+  DollarArgs dl;
+};
+
+// base2index restated on a byte (genFMindex.c:71-84)
+__device__ __forceinline__ uint32_t code_of(uint32_t x)
+{
+  uint32_t b1 = x & 4u, f2 = x & 2u;
+  uint32_t b0 = b1 ? (f2 ^ 2u) : f2;
+  return (b1 | b0) >> 1;
+}
+
+// first-`sh`-rows mask of one 32-row word, MSB = first row; sh clamped to [0,32]
+__device__ __forceinline__ uint32_t row_mask(int sh)
+{
+  sh = sh < 0 ? 0 : (sh > 32 ? 32 : sh);
+  return (uint32_t) ((0xFFFFFFFF00000000ull) >> sh);
+}
+
+// XOR masks selecting the planes of code c: plane p (= 2s+t) is used as is when
+// bit p of c is set, inverted otherwise (fmIndexCPUBaseline.c:239-247).
+template <int K>
+__device__ __forceinline__ void plane_xor(uint32_t c, uint32_t (&sx)[2 * K])
+{
+#pragma unroll
+  for (int p = 0; p < 2 * K; ++p) sx[p] = ((c >> p) & 1u) ? 0u : 0xFFFFFFFFu;
+}
+
+template <int K>
+__device__ __forceinline__ uint32_t select_rows(const uint32_t* pl, const uint32_t (&sx)[2 * K])
+{
+  uint32_t v = ~0u;
+#pragma unroll
+  for (int p = 0; p < 2 * K; ++p) v &= pl[p] ^ sx[p];
+  return v;
+}
+
+// Number of $ rows to discount (fmIndexCPUBaseline.c:252-256; AC :254-263).
+template <int K, bool AC>
+__device__ __forceinline__ int dollar_fix(const DollarArgs& dl, uint32_t b, uint32_t c, uint32_t X, bool e)
+{
+  int corr = 0;
+#pragma unroll
+  for (int s = 0; s < K; ++s) {
+    bool hit = (dl.dblk[s] == b) && (dl.dbase[s] == c);
+    bool cond = (AC && e) ? (X <= dl.dpos[s]) : (X > dl.dpos[s]);
+    corr += (hit && cond) ? 1 : 0;
+  }
+  return corr;
+}
+
+// ---------------------------------------------------------------------------
+// Register-resident block fetch for small blocks (BMW <= 16 words): all bit
+// planes of block b plus the one counter (or delta+superblock) that code c
+// needs.  Loads are 16-byte (dwordx4) when the plane group allows it.
+// ---------------------------------------------------------------------------
+template <class G>
+struct Blk {
+  uint32_t bm[G::BMW];
+  uint32_t cnt;
+  uint32_t b;
+  bool e;
+};
+
+template <class G>
+__device__ __forceinline__ void load_planes(const uint32_t* __restrict__ p, uint32_t (&bm)[G::BMW])
+{
+  if constexpr (G::BMW % 4 == 0 && ((G::BOFF + 0) % 4 == 0) && (G::EW % 4 == 0)) {
+#pragma unroll
+    for (int i = 0; i < G::BMW / 4; ++i) {
+      uint4 v = *reinterpret_cast<const uint4*>(p + 4 * i);
+      bm[4 * i + 0] = v.x; bm[4 * i + 1] = v.y; bm[4 * i + 2] = v.z; bm[4 * i + 3] = v.w;
+    }
+  } else if constexpr (G::BMW % 2 == 0 && (G::BOFF % 2 == 0) && (G::EW % 2 == 0)) {
+#pragma unroll
+    for (int i = 0; i < G::BMW / 2; ++i) {
+      uint2 v = *reinterpret_cast<const uint2*>(p + 2 * i);
+      bm[2 * i + 0] = v.x; bm[2 * i + 1] = v.y;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < G::BMW; ++i) bm[i] = p[i];
+  }
+}
+
+template <class G>
+__device__ __forceinline__ void fetch_block(const IdxArgs& ix, uint32_t b, uint32_t c, Blk<G>& k)
+{
+  k.b = b;
+  const uint32_t* ent = ix.ent + (uint64_t) b * G::EW;
+  if constexpr (G::LAY == LAY_INTER) {
+    k.e = false;
+    load_planes<G>(ent, k.bm);
+    k.cnt = ent[G::BMW + c];
+  } else if constexpr (G::LAY == LAY_AC) {
+    k.e = ((b & 1u) != 0) == (c < (uint32_t) G::HALF);
+    load_planes<G>(ent + G::BOFF, k.bm);
+    k.cnt = ix.ent[(uint64_t) (b + (k.e ? 1u : 0u)) * G::EW + (c & (G::HALF - 1))];
+  } else {
+    k.e = false;
+    load_planes<G>(ent, k.bm);
+    uint32_t delta = reinterpret_cast<const uint16_t*>(ent)[G::DELTA16 + c];
+    constexpr int S = sb_shift_for(G::D);
+    uint32_t base = ix.sb[(uint64_t) (b >> S) * G::NC + c];
+    k.cnt = base + delta;
+  }
+}
+
+template <class G>
+__device__ __forceinline__ uint32_t lf_from_block(const IdxArgs& ix, const Blk<G>& k, uint32_t X, uint32_t c,
+                                                  const uint32_t (&sx)[2 * G::K])
+{
+  const int o = (int) (X - k.b * (uint32_t) G::D);
+  uint32_t pop = 0;
+#pragma unroll
+  for (int w = 0; w < G::NB; ++w) {
+    uint32_t m = row_mask(o - 32 * w);
+    if constexpr (G::LAY == LAY_AC) m = k.e ? ~m : m;
+    pop += __popc(m & select_rows<G::K>(&k.bm[w * G::PW], sx));
+  }
+  const int corr = dollar_fix<G::K, G::LAY == LAY_AC>(ix.dl, k.b, c, X, k.e);
+  const uint32_t bc = pop - (uint32_t) corr;
+  if constexpr (G::LAY == LAY_AC) return k.e ? k.cnt - bc : k.cnt + bc;
+  return k.cnt + bc;
+}
+
+// ---------------------------------------------------------------------------
+// Streaming LF for large blocks (d >= 192 with K=2): planes read word group by
+// word group; only the words that the row mask reaches contribute for
+// forward counting, but all are read (as the reference does) so the result is
+// identical for every layout.
+// ---------------------------------------------------------------------------
+template <class G>
+__device__ __forceinline__ uint32_t lf_stream(const IdxArgs& ix, uint32_t X, uint32_t c,
+                                              const uint32_t (&sx)[2 * G::K])
+{
+  const uint32_t b = X / (uint32_t) G::D;
+  const int o = (int) (X - b * (uint32_t) G::D);
+  const uint32_t* ent = ix.ent + (uint64_t) b * G::EW;
+  bool e = false;
+  uint32_t cnt;
+  if constexpr (G::LAY == LAY_INTER) {
+    cnt = ent[G::BMW + c];
+  } else if constexpr (G::LAY == LAY_AC) {
+    e = ((b & 1u) != 0) == (c < (uint32_t) G::HALF);
+    cnt = ix.ent[(uint64_t) (b + (e ? 1u : 0u)) * G::EW + (c & (G::HALF - 1))];
+  } else {
+    constexpr int S = sb_shift_for(G::D);
+    cnt = ix.sb[(uint64_t) (b >> S) * G::NC + c] + reinterpret_cast<const uint16_t*>(ent)[G::DELTA16 + c];
+  }
+  const uint32_t* pl = ent + G::BOFF;
+  uint32_t pop = 0;
+#pragma unroll 2
+  for (int w = 0; w < G::NB; ++w) {
+    uint32_t v[G::PW];
+    if constexpr (G::PW == 4 && (G::BOFF % 4 == 0) && (G::EW % 4 == 0)) {
+      uint4 q = *reinterpret_cast<const uint4*>(pl + 4 * w);
+      v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+    } else if constexpr (G::PW == 2 && (G::BOFF % 2 == 0) && (G::EW % 2 == 0)) {
+      uint2 q = *reinterpret_cast<const uint2*>(pl + 2 * w);
+      v[0] = q.x; v[1] = q.y;
+    } else {
+#pragma unroll
+      for (int p = 0; p < G::PW; ++p) v[p] = pl[G::PW * w + p];
+    }
+    uint32_t m = row_mask(o - 32 * w);
+    if constexpr (G::LAY == LAY_AC) m = e ? ~m : m;
+    pop += __popc(m & select_rows<G::K>(v, sx));
+  }
+  const int corr = dollar_fix<G::K, G::LAY == LAY_AC>(ix.dl, b, c, X, e);
+  const uint32_t bc = pop - (uint32_t) corr;
+  if constexpr (G::LAY == LAY_AC) return e ? cnt - bc : cnt + bc;
+  return cnt + bc;
+}
+
+}  // namespace kfmi
+
+#endif  // KFMI_DEVICE_H_

@@ -1,0 +1,879 @@
+/*
+ * kfmi_search.hip -- MI355X (gfx950) backward search: query packing, the
+ * task-per-query and wave64-cooperative LF kernels, device index layouts,
+ * and the reference's GPU plugin entry points (common/interface.h:36-41):
+ * transferCPUtoGPU, searchIndexGPU, transferGPUtoCPU, free*GPU.
+ *
+ * Semantics: results are bit-identical to the reference CPU searchers
+ * (fmIndexCPUBaseline.c:157-292 for task/coop/packed, -AltCounters.c:145-310
+ * for the *-ac backends) -- not to the reference .cu files, which carry the
+ * defects B1-B4 of SURVEY.md Appendix B.
+ */
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <mutex>
+#include <vector>
+
+#include "../kfmi_internal.h"
+#include "kfmi_device.h"
+#include "kfmi_coop.h"
+
+using namespace kfmi;
+
+/* ------------------------------------------------------------------------ */
+/* backend registry and per-thread state                                    */
+/* ------------------------------------------------------------------------ */
+
+static const char* kBackendNames[KFMI_BK_COUNT] = {
+    "task", "coop", "task-ac", "coop-ac", "task-packed", "coop-packed"};
+
+static thread_local int t_backend = -1;
+static thread_local int t_device = -1;
+static thread_local int32_t t_last_error = KFMI_SUCCESS;
+static thread_local double t_ms[3] = {0, 0, 0};
+
+static int backend_from_name(const char* n)
+{
+  if (!n) return -1;
+  for (int i = 0; i < KFMI_BK_COUNT; ++i)
+    if (!strcmp(n, kBackendNames[i])) return i;
+  /* reference binary names (makefile:177-207) */
+  if (!strcmp(n, "task-2step") || !strcmp(n, "task-1step")) return KFMI_BK_TASK;
+  if (!strcmp(n, "coop-2step") || !strcmp(n, "coop-1step")) return KFMI_BK_COOP;
+  if (!strcmp(n, "task-2step-ac")) return KFMI_BK_TASK_AC;
+  if (!strcmp(n, "coop-2step-ac")) return KFMI_BK_COOP_AC;
+  if (!strcmp(n, "packed")) return KFMI_BK_TASK_PACKED;
+  return -1;
+}
+
+extern "C" kfmi_backend_t kfmi_backend(void)
+{
+  if (t_backend < 0) {
+    int b = backend_from_name(getenv("KFMI_BACKEND"));
+    t_backend = b >= 0 ? b : KFMI_BK_TASK_PACKED;
+  }
+  return (kfmi_backend_t) t_backend;
+}
+
+extern "C" uint32_t kfmi_backend_tag(kfmi_backend_t b)
+{
+  return (b == KFMI_BK_TASK_AC || b == KFMI_BK_COOP_AC) ? 201u : 101u;
+}
+
+extern "C" int32_t kfmi_set_backend(const char* name)
+{
+  int b = backend_from_name(name);
+  if (b < 0) return KFMI_E_BAD_ARGUMENT;
+  t_backend = b;
+  return KFMI_SUCCESS;
+}
+
+extern "C" const char* kfmi_get_backend(void) { return kBackendNames[kfmi_backend()]; }
+
+extern "C" int32_t kfmi_device_count(void)
+{
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+extern "C" int32_t kfmi_current_device(void)
+{
+  if (t_device < 0) {
+    const char* e = getenv("KFMI_DEVICE");
+    t_device = e ? atoi(e) : 0;
+  }
+  return t_device;
+}
+
+extern "C" int32_t kfmi_set_device(int32_t device)
+{
+  int n = kfmi_device_count();
+  if (device < 0 || device >= n) return KFMI_E_NO_DEVICE;
+  t_device = device;
+  return KFMI_SUCCESS;
+}
+
+extern "C" void kfmi_set_last_error(int32_t e) { t_last_error = e; }
+extern "C" int32_t kfmi_last_error(void) { return t_last_error; }
+
+extern "C" int32_t kfmi_last_timing(double* ms_total, double* ms_pack, double* ms_lf)
+{
+  if (ms_total) *ms_total = t_ms[0];
+  if (ms_pack) *ms_pack = t_ms[1];
+  if (ms_lf) *ms_lf = t_ms[2];
+  return KFMI_SUCCESS;
+}
+
+/* One non-blocking stream and a set of timing events per device. */
+struct DevCtx {
+  bool init = false;
+  hipStream_t st = nullptr;
+  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+};
+static DevCtx g_ctx[64];
+static std::mutex g_ctx_mu;
+
+static int32_t ctx_for(int dev, DevCtx** out)
+{
+  if (dev < 0 || dev >= 64) return KFMI_E_NO_DEVICE;
+  std::lock_guard<std::mutex> lk(g_ctx_mu);
+  DevCtx& c = g_ctx[dev];
+  if (hipSetDevice(dev) != hipSuccess) return KFMI_E_NO_DEVICE;
+  if (!c.init) {
+    if (hipStreamCreateWithFlags(&c.st, hipStreamNonBlocking) != hipSuccess) return KFMI_E_NO_DEVICE;
+    for (int i = 0; i < 3; ++i)
+      if (hipEventCreate(&c.ev[i]) != hipSuccess) return KFMI_E_NO_DEVICE;
+    c.init = true;
+  }
+  *out = &c;
+  return KFMI_SUCCESS;
+}
+
+#define HIP_OK(x)                                                                   \
+  do {                                                                              \
+    hipError_t _e = (x);                                                            \
+    if (_e != hipSuccess) {                                                         \
+      fprintf(stderr, "kstepfmi: %s failed: %s (%s:%d)\n", #x, hipGetErrorString(_e), \
+              __FILE__, __LINE__);                                                  \
+      return KFMI_E_KERNEL;                                                         \
+    }                                                                               \
+  } while (0)
+
+/* ------------------------------------------------------------------------ */
+/* device-side handles                                                      */
+/* ------------------------------------------------------------------------ */
+
+struct kfmi_dev_index {
+  int device = -1;
+  int backend = -1;
+  int layout = -1;
+  uint32_t K = 0, d = 0, nb = 0, bwtsize = 0, nentries = 0;
+  DollarArgs dl{};
+  uint32_t* ent = nullptr;     /* device entries */
+  uint64_t ent_bytes = 0;
+  uint32_t* sb = nullptr;      /* packed: superblock counters */
+  uint64_t sb_bytes = 0;
+};
+
+struct kfmi_dev_queries {
+  int device = -1;
+  uint8_t* ascii = nullptr;    /* num*size bytes, plain layout */
+  uint32_t* packed = nullptr;  /* nwords x num u32 codes */
+  uint64_t num = 0;
+  uint32_t size = 0, K = 0, steps = 0, nwords = 0;
+};
+
+/* ------------------------------------------------------------------------ */
+/* query packing: ASCII [num][m] -> codes [nwords][num], step t of query q in */
+/* word t/SPW, bits 2K*(t%SPW)..; step t consumes chars m-1-K*t-i (i<K), the  */
+/* order of fmIndexCPUBaseline.c:200-226.                                   */
+/* ------------------------------------------------------------------------ */
+
+template <int K>
+__global__ __launch_bounds__(256) void pack_queries_kernel(const uint8_t* __restrict__ q, uint64_t num,
+                                                           uint32_t m, uint32_t steps, uint32_t nwords,
+                                                           uint32_t tq, uint32_t* __restrict__ out)
+{
+  extern __shared__ __attribute__((aligned(16))) uint8_t tile[];
+  constexpr int SPW = 32 / (2 * K);
+  const uint64_t q0 = (uint64_t) blockIdx.x * tq;
+  const uint64_t nq = (num - q0) < tq ? (num - q0) : tq;
+  const uint64_t bytes = nq * m;
+  const uint8_t* src = q + q0 * m;   /* q0*m is a multiple of 64*m: 16-byte aligned when m%... */
+  if ((((uintptr_t) src) & 15u) == 0) {
+    const uint64_t n16 = bytes / 16;
+    for (uint64_t i = threadIdx.x; i < n16; i += blockDim.x)
+      reinterpret_cast<uint4*>(tile)[i] = reinterpret_cast<const uint4*>(src)[i];
+    for (uint64_t i = n16 * 16 + threadIdx.x; i < bytes; i += blockDim.x) tile[i] = src[i];
+  } else {
+    for (uint64_t i = threadIdx.x; i < bytes; i += blockDim.x) tile[i] = src[i];
+  }
+  __syncthreads();
+  for (uint32_t t = threadIdx.x; t < nq; t += blockDim.x) {
+    const uint8_t* p = tile + (uint64_t) t * m;
+    for (uint32_t w = 0; w < nwords; ++w) {
+      uint32_t word = 0;
+#pragma unroll
+      for (int j = 0; j < SPW; ++j) {
+        const uint32_t st = w * SPW + j;
+        if (st < steps) {
+          const int pos = (int) m - 1 - (int) (K * st);
+          uint32_t c = 0;
+#pragma unroll
+          for (int i = 0; i < K; ++i) c |= code_of(p[pos - i]) << (2 * i);
+          word |= c << (2 * K * j);
+        }
+      }
+      out[(uint64_t) w * num + q0 + t] = word;
+    }
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* task-per-query kernel: one thread owns QPT queries (both ends each)       */
+/* ------------------------------------------------------------------------ */
+
+template <class G, int QPT>
+__global__ __launch_bounds__(256) void task_kernel(IdxArgs ix, const uint32_t* __restrict__ qp, uint64_t num,
+                                                   uint32_t steps, uint32_t nwords, uint32_t* __restrict__ res)
+{
+  constexpr int SPW = G::SPW;
+  const uint64_t base = (uint64_t) blockIdx.x * (256 * QPT) + threadIdx.x;
+  if (base >= num) return;
+  uint64_t q[QPT];
+  uint32_t L[QPT], R[QPT];
+#pragma unroll
+  for (int i = 0; i < QPT; ++i) {
+    q[i] = base + (uint64_t) i * 256;
+    if (q[i] >= num) q[i] = base;   /* duplicate work for the tail, never stored twice */
+    L[i] = 0;
+    R[i] = ix.bwtsize;
+  }
+  for (uint32_t w = 0; w < nwords; ++w) {
+    uint32_t word[QPT];
+#pragma unroll
+    for (int i = 0; i < QPT; ++i) word[i] = qp[(uint64_t) w * num + q[i]];
+    const uint32_t left = steps - w * SPW;
+#pragma unroll
+    for (int j = 0; j < SPW; ++j) {
+      if ((uint32_t) j >= left) continue;   /* only the last word is partial (wave-uniform) */
+      uint32_t c[QPT];
+#pragma unroll
+      for (int i = 0; i < QPT; ++i) c[i] = (word[i] >> (2 * G::K * j)) & (uint32_t) (G::NC - 1);
+      if constexpr (G::SMALL) {
+        Blk<G> kl[QPT], kr[QPT];
+#pragma unroll
+        for (int i = 0; i < QPT; ++i) fetch_block<G>(ix, L[i] / (uint32_t) G::D, c[i], kl[i]);
+#pragma unroll
+        for (int i = 0; i < QPT; ++i) {
+          const uint32_t br = R[i] / (uint32_t) G::D;
+          if (br != kl[i].b) fetch_block<G>(ix, br, c[i], kr[i]);
+          else kr[i] = kl[i];
+        }
+#pragma unroll
+        for (int i = 0; i < QPT; ++i) {
+          uint32_t sx[2 * G::K];
+          plane_xor<G::K>(c[i], sx);
+          L[i] = lf_from_block<G>(ix, kl[i], L[i], c[i], sx);
+          R[i] = lf_from_block<G>(ix, kr[i], R[i], c[i], sx);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < QPT; ++i) {
+          uint32_t sx[2 * G::K];
+          plane_xor<G::K>(c[i], sx);
+          L[i] = lf_stream<G>(ix, L[i], c[i], sx);
+          R[i] = lf_stream<G>(ix, R[i], c[i], sx);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < QPT; ++i) {
+    const uint64_t qi = base + (uint64_t) i * 256;
+    if (qi < num) *reinterpret_cast<uint2*>(res + 2 * qi) = make_uint2(L[i], R[i]);
+  }
+}
+
+/* distinct d-blocks touched per step (1 if L/d == R/d else 2): the
+ * dedup-aware algorithmic traffic of SURVEY 8(d).  Same LF math as the
+ * task kernel; a separate launch so the timed kernels carry no counters. */
+template <class G>
+__global__ __launch_bounds__(256) void count_blocks_kernel(IdxArgs ix, const uint32_t* __restrict__ qp, uint64_t num,
+                                                           uint32_t steps, uint32_t nwords,
+                                                           unsigned long long* __restrict__ total)
+{
+  const uint64_t q = (uint64_t) blockIdx.x * 256 + threadIdx.x;
+  uint32_t cnt = 0;
+  if (q < num) {
+    uint32_t L = 0, R = ix.bwtsize;
+    for (uint32_t t = 0; t < steps; ++t) {
+      const uint32_t word = qp[(uint64_t) (t / G::SPW) * num + q];
+      const uint32_t c = (word >> (2 * G::K * (t % G::SPW))) & (uint32_t) (G::NC - 1);
+      uint32_t sx[2 * G::K];
+      plane_xor<G::K>(c, sx);
+      cnt += (L / (uint32_t) G::D == R / (uint32_t) G::D) ? 1u : 2u;
+      L = lf_stream<G>(ix, L, c, sx);
+      R = lf_stream<G>(ix, R, c, sx);
+    }
+  }
+  /* wave reduction, one atomic per wave */
+  for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+  if ((threadIdx.x & 63) == 0) atomicAdd(total, (unsigned long long) cnt);
+}
+
+/* ------------------------------------------------------------------------ */
+/* packed layout construction from tag-101 entries (on the device)          */
+/* ------------------------------------------------------------------------ */
+
+template <int K, int NB>
+__global__ __launch_bounds__(256) void build_packed_kernel(const uint32_t* __restrict__ inter, uint32_t nentries,
+                                                           uint32_t* __restrict__ packed, uint32_t* __restrict__ sb,
+                                                           uint32_t* __restrict__ overflow)
+{
+  using GI = Geo<K, NB, LAY_INTER>;
+  using GP = Geo<K, NB, LAY_PACKED>;
+  constexpr int S = sb_shift_for(GI::D);
+  const uint64_t b = (uint64_t) blockIdx.x * 256 + threadIdx.x;
+  if (b >= nentries) return;
+  const uint32_t* src = inter + b * GI::EW;
+  const uint32_t* sup = inter + ((b >> S) << S) * GI::EW;
+  uint32_t* dst = packed + b * GP::EW;
+  for (int i = 0; i < GI::BMW; ++i) dst[i] = src[i];
+  uint16_t* d16 = reinterpret_cast<uint16_t*>(dst);
+  for (int c = 0; c < GI::NC; ++c) {
+    const uint32_t delta = src[GI::BMW + c] - sup[GI::BMW + c];
+    if (delta > 0xFFFFu) atomicAdd(overflow, 1u);
+    d16[GP::DELTA16 + c] = (uint16_t) delta;
+  }
+  for (int i = GI::BMW + GI::NC / 2; i < GP::EW; ++i) dst[i] = 0;
+  if ((b & ((1u << S) - 1)) == 0)
+    for (int c = 0; c < GI::NC; ++c) sb[(b >> S) * GI::NC + c] = src[GI::BMW + c];
+}
+
+/* ------------------------------------------------------------------------ */
+/* dispatch tables                                                          */
+/* ------------------------------------------------------------------------ */
+
+struct SearchLaunch {
+  const DevCtx* ctx;
+  IdxArgs ix;
+  const uint32_t* qp;
+  uint64_t num;
+  uint32_t steps, nwords;
+  uint32_t* res;
+};
+
+static int task_qpt(void)
+{
+  const char* e = getenv("KFMI_QPT");
+  int v = e ? atoi(e) : 1;
+  return v == 2 ? 2 : 1;
+}
+
+template <class G>
+static hipError_t launch_task(const SearchLaunch& a)
+{
+  if (task_qpt() == 2) {
+    const uint64_t blocks = (a.num + 511) / 512;
+    hipLaunchKernelGGL((task_kernel<G, 2>), dim3((uint32_t) blocks), dim3(256), 0, a.ctx->st, a.ix, a.qp, a.num,
+                       a.steps, a.nwords, a.res);
+  } else {
+    const uint64_t blocks = (a.num + 255) / 256;
+    hipLaunchKernelGGL((task_kernel<G, 1>), dim3((uint32_t) blocks), dim3(256), 0, a.ctx->st, a.ix, a.qp, a.num,
+                       a.steps, a.nwords, a.res);
+  }
+  return hipGetLastError();
+}
+
+template <class G>
+static hipError_t launch_coop(const SearchLaunch& a)
+{
+  return coop_launch<G>(a.ctx->st, a.ix, a.qp, a.num, a.steps, a.nwords, a.res);
+}
+
+template <class G>
+static hipError_t launch_count(const SearchLaunch& a, unsigned long long* d_total)
+{
+  const uint64_t blocks = (a.num + 255) / 256;
+  hipLaunchKernelGGL((count_blocks_kernel<G>), dim3((uint32_t) blocks), dim3(256), 0, a.ctx->st, a.ix, a.qp, a.num,
+                     a.steps, a.nwords, d_total);
+  return hipGetLastError();
+}
+
+/* K in {1,2}; d in {32,64,128,192,256,448,960} */
+#define KFMI_FOR_NB(X, K, LAY) \
+  X(K, 1, LAY) X(K, 2, LAY) X(K, 4, LAY) X(K, 6, LAY) X(K, 8, LAY) X(K, 14, LAY) X(K, 30, LAY)
+
+static bool nb_supported(uint32_t nb)
+{
+  return nb == 1 || nb == 2 || nb == 4 || nb == 6 || nb == 8 || nb == 14 || nb == 30;
+}
+
+enum class Op { Task, Coop, Count };
+
+template <int K, int NB, int LAY>
+static hipError_t dispatch_one(Op op, const SearchLaunch& a, unsigned long long* d_total)
+{
+  using G = Geo<K, NB, LAY>;
+  switch (op) {
+    case Op::Task: return launch_task<G>(a);
+    case Op::Coop: return launch_coop<G>(a);
+    default: return launch_count<G>(a, d_total);
+  }
+}
+
+static hipError_t dispatch(Op op, uint32_t K, uint32_t nb, int lay, const SearchLaunch& a,
+                           unsigned long long* d_total = nullptr)
+{
+#define KFMI_CASE(KK, NBV, LAYV)                                   \
+  if (K == KK && nb == NBV && lay == LAYV) return dispatch_one<KK, NBV, LAYV>(op, a, d_total);
+  KFMI_FOR_NB(KFMI_CASE, 1, LAY_INTER)
+  KFMI_FOR_NB(KFMI_CASE, 2, LAY_INTER)
+  KFMI_FOR_NB(KFMI_CASE, 1, LAY_AC)
+  KFMI_FOR_NB(KFMI_CASE, 2, LAY_AC)
+  KFMI_FOR_NB(KFMI_CASE, 1, LAY_PACKED)
+  KFMI_FOR_NB(KFMI_CASE, 2, LAY_PACKED)
+#undef KFMI_CASE
+  return hipErrorInvalidValue;
+}
+
+static hipError_t dispatch_build_packed(uint32_t K, uint32_t nb, const uint32_t* inter, uint32_t nentries,
+                                        uint32_t* packed, uint32_t* sb, uint32_t* overflow, hipStream_t st)
+{
+  const uint32_t blocks = (nentries + 255) / 256;
+#define KFMI_BP(KK, NBV, LAYV)                                                                  \
+  if (K == KK && nb == NBV) {                                                                   \
+    hipLaunchKernelGGL((build_packed_kernel<KK, NBV>), dim3(blocks), dim3(256), 0, st, inter, nentries, \
+                       packed, sb, overflow);                                                   \
+    return hipGetLastError();                                                                   \
+  }
+  KFMI_FOR_NB(KFMI_BP, 1, 0)
+  KFMI_FOR_NB(KFMI_BP, 2, 0)
+#undef KFMI_BP
+  return hipErrorInvalidValue;
+}
+
+static int layout_of(int backend)
+{
+  switch (backend) {
+    case KFMI_BK_TASK: case KFMI_BK_COOP: return LAY_INTER;
+    case KFMI_BK_TASK_AC: case KFMI_BK_COOP_AC: return LAY_AC;
+    default: return LAY_PACKED;
+  }
+}
+
+static bool is_coop(int backend)
+{
+  return backend == KFMI_BK_COOP || backend == KFMI_BK_COOP_AC || backend == KFMI_BK_COOP_PACKED;
+}
+
+/* ------------------------------------------------------------------------ */
+/* host helpers for the device layouts                                      */
+/* ------------------------------------------------------------------------ */
+
+/* Counters at row n+1 (one past the last row) from a tag-100/101 index:
+ * cnt_{E-1} + rows of each code in the last block, $ rows excluded.  Used for
+ * the padding entry that keeps R/d == nentries in bounds when (n+1) % d == 0
+ * (reference defect B5: it reads past the end there). */
+static void end_counters(const kfmi_fmi_t* f, uint32_t* out)
+{
+  const uint32_t nc = 1u << (2 * f->steps), nb = f->nbitmaps;
+  const uint32_t last = f->nentries - 1;
+  const uint32_t* e = f->h_index + (uint64_t) last * f->entry_words;
+  const uint32_t o = f->bwtsize - last * f->chunk;  /* rows of the last block, in (0, d] */
+  for (uint32_t c = 0; c < nc; ++c) {
+    uint32_t pop = 0;
+    for (uint32_t w = 0; w < nb; ++w) {
+      int sh = (int) o - 32 * (int) w;
+      sh = sh < 0 ? 0 : (sh > 32 ? 32 : sh);
+      uint32_t m = (uint32_t) (0xFFFFFFFF00000000ull >> sh);
+      for (uint32_t s = 0; s < f->steps; ++s)
+        for (uint32_t t = 0; t < 2; ++t) {
+          uint32_t p = e[kfmi_plane_index(f->tag, f->steps, nb, s, t, w)];
+          m &= ((c >> (2 * s + t)) & 1u) ? p : ~p;
+        }
+      pop += (uint32_t) __builtin_popcount(m);
+    }
+    for (uint32_t s = 0; s < f->steps; ++s)
+      if (f->modposdollarBWT[s] == last && f->dollarBaseBWT[s] == c && f->bwtsize > f->dollarPositionBWT[s]) pop--;
+    out[c] = e[2 * nb * f->steps + c] + pop;
+  }
+}
+
+/* Host image of the entries for a layout, converting tags as needed.
+ * INTER/PACKED need plain counters (tag 100/101); AC needs tag 201 (a
+ * tag-100/101 input goes through the tfmiAC transform first). */
+static int32_t host_entries_for(const kfmi_fmi_t* f, int lay, kfmi_fmi_t** owned, const kfmi_fmi_t** use)
+{
+  *owned = nullptr;
+  *use = f;
+  if (lay == LAY_INTER || lay == LAY_PACKED) {
+    if (f->tag == 101) return KFMI_SUCCESS;
+    if (f->tag == 100) {
+      int32_t e = kfmi_transform_interleave((void*) f, (void**) owned);
+      if (e) return e;
+      *use = *owned;
+      return KFMI_SUCCESS;
+    }
+    return KFMI_INDEX_VER_INTERLEAVE;   /* an AC file cannot feed a plain-counter backend */
+  }
+  /* AC */
+  if (f->tag == 201) return KFMI_SUCCESS;
+  kfmi_fmi_t* t100 = nullptr;
+  const kfmi_fmi_t* src100 = f;
+  if (f->tag == 101) {
+    /* de-interleave to tag 100 first */
+    int32_t e = kfmi_index_alloc(100, f->steps, f->bwtsize, f->nentries, f->chunk, f->dollarPositionBWT,
+                                 f->dollarBaseBWT, &t100);
+    if (e) return e;
+    const uint32_t nb = f->nbitmaps, K = f->steps, nbw = 2 * nb * K;
+    for (uint64_t i = 0; i < f->nentries; ++i) {
+      const uint32_t* s = f->h_index + i * f->entry_words;
+      uint32_t* d = t100->h_index + i * t100->entry_words;
+      for (uint32_t w = 0; w < nb; ++w)
+        for (uint32_t st = 0; st < K; ++st)
+          for (uint32_t t = 0; t < 2; ++t)
+            d[kfmi_plane_index(100, K, nb, st, t, w)] = s[kfmi_plane_index(101, K, nb, st, t, w)];
+      for (uint32_t c = 0; c < f->ncounters; ++c) d[nbw + c] = s[nbw + c];
+    }
+    src100 = t100;
+  } else if (f->tag == 200) {
+    /* permute the bit planes of every entry into tag-201 order */
+    int32_t e = kfmi_index_alloc(201, f->steps, f->bwtsize, f->nentries, f->chunk, f->dollarPositionBWT,
+                                 f->dollarBaseBWT, owned);
+    if (e) return e;
+    const uint32_t nb = f->nbitmaps, K = f->steps, half = f->ncounters;
+    for (uint64_t i = 0; i < f->nentries; ++i) {
+      const uint32_t* s = f->h_index + i * f->entry_words;
+      uint32_t* d = (*owned)->h_index + i * (*owned)->entry_words;
+      for (uint32_t c = 0; c < half; ++c) d[c] = s[c];
+      for (uint32_t w = 0; w < nb; ++w)
+        for (uint32_t st = 0; st < K; ++st)
+          for (uint32_t t = 0; t < 2; ++t)
+            d[half + kfmi_plane_index(201, K, nb, st, t, w)] = s[half + kfmi_plane_index(200, K, nb, st, t, w)];
+    }
+    *use = *owned;
+    return KFMI_SUCCESS;
+  }
+  int32_t e = kfmi_transform_ac((void*) src100, nullptr, (void**) owned);
+  if (t100) freeIndex((void**) &t100);
+  if (e) return e;
+  *use = *owned;
+  return KFMI_SUCCESS;
+}
+
+static void free_dev_index(kfmi_dev_index* di)
+{
+  if (!di) return;
+  if (di->device >= 0) (void) hipSetDevice(di->device);
+  if (di->ent) (void) hipFree(di->ent);
+  if (di->sb) (void) hipFree(di->sb);
+  delete di;
+}
+
+static int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx)
+{
+  if (f->steps < 1 || f->steps > 2) return KFMI_E_BAD_ARGUMENT;   /* GPU kernels: K in {1,2} */
+  if (!nb_supported(f->nbitmaps)) return KFMI_E_BAD_ARGUMENT;
+  const int lay = layout_of(backend);
+  kfmi_fmi_t* owned = nullptr;
+  const kfmi_fmi_t* src = nullptr;
+  int32_t err = host_entries_for(f, lay, &owned, &src);
+  if (err) return err;
+
+  kfmi_dev_index* di = new kfmi_dev_index();
+  di->device = dev;
+  di->backend = backend;
+  di->layout = lay;
+  di->K = f->steps;
+  di->d = f->chunk;
+  di->nb = f->nbitmaps;
+  di->bwtsize = f->bwtsize;
+  di->nentries = src->nentries;
+  for (uint32_t s = 0; s < 2; ++s) {
+    di->dl.dpos[s] = s < f->steps ? f->dollarPositionBWT[s] : 0xFFFFFFFFu;
+    di->dl.dbase[s] = s < f->steps ? f->dollarBaseBWT[s] : 0xFFFFFFFFu;
+    di->dl.dblk[s] = s < f->steps ? f->dollarPositionBWT[s] / f->chunk : 0xFFFFFFFFu;
+  }
+  const uint64_t ew = src->entry_words;
+  const uint64_t body = 4ull * ew * src->nentries;
+  const uint32_t nc = 1u << (2 * f->steps);
+  std::vector<uint32_t> pad(ew * 2, 0);
+
+  auto fail = [&](int32_t code) {
+    if (owned) freeIndex((void**) &owned);
+    free_dev_index(di);
+    return code;
+  };
+
+  if (lay == LAY_INTER || lay == LAY_AC) {
+    /* entries + 2 padding entries (B5 guard; AC may look at b+1 of the sentinel) */
+    di->ent_bytes = body + 4ull * ew * 2;
+    if (hipMalloc((void**) &di->ent, di->ent_bytes) != hipSuccess) return fail(KFMI_E_DEVICE_ALLOC);
+    if (lay == LAY_INTER) end_counters(src, pad.data() + 2 * f->nbitmaps * f->steps);
+    if (hipMemcpyAsync(di->ent, src->h_index, body, hipMemcpyHostToDevice, ctx->st) != hipSuccess ||
+        hipMemcpyAsync((uint8_t*) di->ent + body, pad.data(), 4ull * ew * 2, hipMemcpyHostToDevice, ctx->st) !=
+            hipSuccess ||
+        hipStreamSynchronize(ctx->st) != hipSuccess)
+      return fail(KFMI_E_KERNEL);
+  } else {
+    /* packed: build on the device from tag-101 entries (+ the padding entry) */
+    const uint32_t ne = src->nentries + 1;
+    uint32_t* tmp = nullptr;
+    uint32_t* d_over = nullptr;
+    const uint32_t pw = (uint32_t) pow2ceil((int) (2 * f->nbitmaps * f->steps + nc / 2));
+    const int S = sb_shift_for((int) f->chunk);
+    const uint64_t nsb = ((uint64_t) ne + (1u << S) - 1) >> S;
+    end_counters(src, pad.data() + 2 * f->nbitmaps * f->steps);
+    di->ent_bytes = 4ull * pw * (ne + 1);
+    di->sb_bytes = 4ull * nc * nsb;
+    if (hipMalloc((void**) &tmp, 4ull * ew * ne) != hipSuccess) return fail(KFMI_E_DEVICE_ALLOC);
+    if (hipMalloc((void**) &di->ent, di->ent_bytes) != hipSuccess ||
+        hipMalloc((void**) &di->sb, di->sb_bytes) != hipSuccess || hipMalloc((void**) &d_over, 4) != hipSuccess) {
+      (void) hipFree(tmp);
+      if (d_over) (void) hipFree(d_over);
+      return fail(KFMI_E_DEVICE_ALLOC);
+    }
+    uint32_t over = 0;
+    bool ok = hipMemcpyAsync(tmp, src->h_index, body, hipMemcpyHostToDevice, ctx->st) == hipSuccess &&
+              hipMemcpyAsync((uint8_t*) tmp + body, pad.data(), 4ull * ew, hipMemcpyHostToDevice, ctx->st) ==
+                  hipSuccess &&
+              hipMemsetAsync(d_over, 0, 4, ctx->st) == hipSuccess &&
+              hipMemsetAsync(di->ent, 0, di->ent_bytes, ctx->st) == hipSuccess &&
+              dispatch_build_packed(f->steps, f->nbitmaps, tmp, ne, di->ent, di->sb, d_over, ctx->st) ==
+                  hipSuccess &&
+              hipMemcpyAsync(&over, d_over, 4, hipMemcpyDeviceToHost, ctx->st) == hipSuccess &&
+              hipStreamSynchronize(ctx->st) == hipSuccess;
+    (void) hipFree(tmp);
+    (void) hipFree(d_over);
+    if (!ok) return fail(KFMI_E_KERNEL);
+    if (over) {
+      fprintf(stderr, "kstepfmi: packed layout delta overflow (%u) -- corrupt counters\n", over);
+      return fail(KFMI_E_READING_FMI);
+    }
+  }
+  if (owned) freeIndex((void**) &owned);
+  if (f->dev) free_dev_index(f->dev);
+  f->dev = di;
+  return KFMI_SUCCESS;
+}
+
+static IdxArgs idx_args(const kfmi_dev_index* di)
+{
+  IdxArgs ix;
+  ix.ent = di->ent;
+  ix.sb = di->sb;
+  ix.bwtsize = di->bwtsize;
+  ix.pad_ = 0;
+  ix.dl = di->dl;
+  return ix;
+}
+
+static void free_dev_queries(kfmi_dev_queries* dq)
+{
+  if (!dq) return;
+  if (dq->device >= 0) (void) hipSetDevice(dq->device);
+  if (dq->ascii) (void) hipFree(dq->ascii);
+  if (dq->packed) (void) hipFree(dq->packed);
+  delete dq;
+}
+
+static int32_t upload_queries(kfmi_qrys_t* q, uint32_t K, int dev, DevCtx* ctx)
+{
+  if (q->size == 0 || (q->size % K) != 0) return KFMI_E_BAD_ARGUMENT;   /* B6 */
+  if (64ull * q->size > 160ull * 1024) return KFMI_E_BAD_ARGUMENT;       /* pack tile must fit LDS */
+  kfmi_dev_queries* dq = new kfmi_dev_queries();
+  dq->device = dev;
+  dq->num = q->num;
+  dq->size = q->size;
+  dq->K = K;
+  dq->steps = q->size / K;
+  const uint32_t spw = 32 / (2 * K);
+  dq->nwords = (dq->steps + spw - 1) / spw;
+  const uint64_t abytes = q->num * (uint64_t) q->size;
+  if (hipMalloc((void**) &dq->ascii, abytes + 16) != hipSuccess ||
+      hipMalloc((void**) &dq->packed, 4ull * dq->nwords * (q->num ? q->num : 1)) != hipSuccess) {
+    free_dev_queries(dq);
+    return KFMI_E_DEVICE_ALLOC;
+  }
+  if (abytes && (hipMemcpyAsync(dq->ascii, q->h_queries, abytes, hipMemcpyHostToDevice, ctx->st) != hipSuccess ||
+                 hipStreamSynchronize(ctx->st) != hipSuccess)) {
+    free_dev_queries(dq);
+    return KFMI_E_KERNEL;
+  }
+  if (q->dev) free_dev_queries(q->dev);
+  q->dev = dq;
+  return KFMI_SUCCESS;
+}
+
+static hipError_t launch_pack(const kfmi_dev_queries* dq, hipStream_t st)
+{
+  if (dq->num == 0) return hipSuccess;
+  uint32_t tq = 256;
+  while ((uint64_t) tq * dq->size > 64 * 1024 && tq > 64) tq >>= 1;
+  const uint64_t blocks = (dq->num + tq - 1) / tq;
+  const size_t lds = (size_t) tq * dq->size + 16;
+  if (dq->K == 1)
+    hipLaunchKernelGGL((pack_queries_kernel<1>), dim3((uint32_t) blocks), dim3(256), lds, st, dq->ascii, dq->num,
+                       dq->size, dq->steps, dq->nwords, tq, dq->packed);
+  else
+    hipLaunchKernelGGL((pack_queries_kernel<2>), dim3((uint32_t) blocks), dim3(256), lds, st, dq->ascii, dq->num,
+                       dq->size, dq->steps, dq->nwords, tq, dq->packed);
+  return hipGetLastError();
+}
+
+/* ------------------------------------------------------------------------ */
+/* C ABI: the reference's GPU plugin entry points                           */
+/* ------------------------------------------------------------------------ */
+
+/* interface.h:40, e.g. fmIndexGPU-Coop-2Step.cu:250-285 (index, $ arrays,
+ * queries and zeroed results to the device; the index is re-laid-out for the
+ * selected backend). */
+extern "C" int32_t transferCPUtoGPU(void* index, void* queries, void* results)
+{
+  kfmi_fmi_t* f = (kfmi_fmi_t*) index;
+  kfmi_qrys_t* q = (kfmi_qrys_t*) queries;
+  kfmi_res_t* r = (kfmi_res_t*) results;
+  const int dev = kfmi_current_device();
+  DevCtx* ctx = nullptr;
+  int32_t err = ctx_for(dev, &ctx);
+  if (err) return err;
+  const int backend = kfmi_backend();
+  if (f && (!f->dev || f->dev->backend != backend || f->dev->device != dev)) {
+    err = upload_index(f, backend, dev, ctx);
+    if (err) return err;
+  }
+  if (q) {
+    if (!f) return KFMI_E_BAD_ARGUMENT;
+    err = upload_queries(q, f->steps, dev, ctx);
+    if (err) return err;
+  }
+  if (r) {
+    if (r->d_results) { (void) hipFree(r->d_results); r->d_results = nullptr; }
+    if (hipMalloc((void**) &r->d_results, 8ull * (r->num ? r->num : 1)) != hipSuccess) return KFMI_E_DEVICE_ALLOC;
+    if (hipMemsetAsync(r->d_results, 0, 8ull * r->num, ctx->st) != hipSuccess ||
+        hipStreamSynchronize(ctx->st) != hipSuccess)
+      return KFMI_E_KERNEL;
+  }
+  return KFMI_SUCCESS;
+}
+
+extern "C" int32_t kfmi_search(void* index, void* queries, void* results)
+{
+  kfmi_fmi_t* f = (kfmi_fmi_t*) index;
+  kfmi_qrys_t* q = (kfmi_qrys_t*) queries;
+  kfmi_res_t* r = (kfmi_res_t*) results;
+  if (!f || !q || !r) return KFMI_E_BAD_ARGUMENT;
+  if (!f->dev || !q->dev || !r->d_results) return KFMI_E_NOT_ON_DEVICE;
+  if (q->num != r->num) return KFMI_E_BAD_ARGUMENT;
+  kfmi_dev_index* di = f->dev;
+  kfmi_dev_queries* dq = q->dev;
+  if (dq->device != di->device || dq->K != di->K) return KFMI_E_BAD_ARGUMENT;
+  DevCtx* ctx = nullptr;
+  int32_t err = ctx_for(di->device, &ctx);
+  if (err) return err;
+
+  SearchLaunch a;
+  a.ctx = ctx;
+  a.ix = idx_args(di);
+  a.qp = dq->packed;
+  a.num = dq->num;
+  a.steps = dq->steps;
+  a.nwords = dq->nwords;
+  a.res = r->d_results;
+
+  HIP_OK(hipEventRecord(ctx->ev[0], ctx->st));
+  HIP_OK(launch_pack(dq, ctx->st));
+  HIP_OK(hipEventRecord(ctx->ev[1], ctx->st));
+  if (dq->num) {
+    const Op op = is_coop(di->backend) ? Op::Coop : Op::Task;
+    HIP_OK(dispatch(op, di->K, di->nb, di->layout, a));
+  }
+  HIP_OK(hipEventRecord(ctx->ev[2], ctx->st));
+  HIP_OK(hipStreamSynchronize(ctx->st));
+  float ms01 = 0, ms12 = 0;
+  HIP_OK(hipEventElapsedTime(&ms01, ctx->ev[0], ctx->ev[1]));
+  HIP_OK(hipEventElapsedTime(&ms12, ctx->ev[1], ctx->ev[2]));
+  t_ms[0] = ms01 + ms12;
+  t_ms[1] = ms01;
+  t_ms[2] = ms12;
+  return KFMI_SUCCESS;
+}
+
+/* interface.h:31: synchronous like the reference (cudaThreadSynchronize,
+ * Task-2Step.cu:209) but its status is kept (kfmi_last_error) instead of
+ * being dropped. */
+extern "C" void searchIndexGPU(void* index, void* queries, void* resIntervals)
+{
+  int32_t e = kfmi_search(index, queries, resIntervals);
+  t_last_error = e;
+  if (e) fprintf(stderr, "kstepfmi: searchIndexGPU failed: %s\n", errorCommon(e));
+}
+
+extern "C" int32_t kfmi_count_blocks(void* index, void* queries, uint64_t* blocks)
+{
+  kfmi_fmi_t* f = (kfmi_fmi_t*) index;
+  kfmi_qrys_t* q = (kfmi_qrys_t*) queries;
+  if (!f || !q || !blocks) return KFMI_E_BAD_ARGUMENT;
+  if (!f->dev || !q->dev) return KFMI_E_NOT_ON_DEVICE;
+  kfmi_dev_index* di = f->dev;
+  kfmi_dev_queries* dq = q->dev;
+  DevCtx* ctx = nullptr;
+  int32_t err = ctx_for(di->device, &ctx);
+  if (err) return err;
+  unsigned long long* d_total = nullptr;
+  HIP_OK(hipMalloc((void**) &d_total, sizeof(unsigned long long)));
+  SearchLaunch a;
+  a.ctx = ctx;
+  a.ix = idx_args(di);
+  a.qp = dq->packed;
+  a.num = dq->num;
+  a.steps = dq->steps;
+  a.nwords = dq->nwords;
+  a.res = nullptr;
+  unsigned long long total = 0;
+  bool ok = hipMemsetAsync(d_total, 0, sizeof(total), ctx->st) == hipSuccess &&
+            launch_pack(dq, ctx->st) == hipSuccess &&
+            (dq->num == 0 || dispatch(Op::Count, di->K, di->nb, di->layout, a, d_total) == hipSuccess) &&
+            hipMemcpyAsync(&total, d_total, sizeof(total), hipMemcpyDeviceToHost, ctx->st) == hipSuccess &&
+            hipStreamSynchronize(ctx->st) == hipSuccess;
+  (void) hipFree(d_total);
+  if (!ok) return KFMI_E_KERNEL;
+  *blocks = total;
+  return KFMI_SUCCESS;
+}
+
+/* interface.h:39, Coop-2Step.cu:287-293 */
+extern "C" int32_t transferGPUtoCPU(void* results)
+{
+  kfmi_res_t* r = (kfmi_res_t*) results;
+  if (!r || !r->d_results) return KFMI_E_NOT_ON_DEVICE;
+  DevCtx* ctx = nullptr;
+  int32_t err = ctx_for(kfmi_current_device(), &ctx);
+  if (err) return err;
+  HIP_OK(hipMemcpyAsync(r->h_results, r->d_results, 8ull * r->num, hipMemcpyDeviceToHost, ctx->st));
+  HIP_OK(hipStreamSynchronize(ctx->st));
+  return KFMI_SUCCESS;
+}
+
+/* interface.h:38, Task-1Step.cu:236-256: releases and NULLs the device copy */
+extern "C" int32_t freeIndexGPU(void** index)
+{
+  kfmi_fmi_t* f = index ? (kfmi_fmi_t*) *index : nullptr;
+  if (f && f->dev) {
+    free_dev_index(f->dev);
+    f->dev = nullptr;
+  }
+  return KFMI_SUCCESS;
+}
+
+extern "C" int32_t freeQueriesGPU(void** queries)
+{
+  kfmi_qrys_t* q = queries ? (kfmi_qrys_t*) *queries : nullptr;
+  if (q && q->dev) {
+    free_dev_queries(q->dev);
+    q->dev = nullptr;
+  }
+  return KFMI_SUCCESS;
+}
+
+extern "C" int32_t freeResultsGPU(void** results)
+{
+  kfmi_res_t* r = results ? (kfmi_res_t*) *results : nullptr;
+  if (r && r->d_results) {
+    (void) hipFree(r->d_results);
+    r->d_results = nullptr;
+  }
+  return KFMI_SUCCESS;
+}
+
+extern "C" uint64_t kfmi_device_index_bytes(void* index)
+{
+  kfmi_fmi_t* f = (kfmi_fmi_t*) index;
+  if (!f || !f->dev) return 0;
+  return f->dev->ent_bytes + f->dev->sb_bytes;
+}

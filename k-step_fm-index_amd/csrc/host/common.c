@@ -1,0 +1,319 @@
+/*
+ * common.c -- host I/O and helpers of the k-step FM-index engine.
+ *
+ * Behavioural restatement of /root/reference/common/common.c (queries,
+ * results, reference text, error strings, timer) with 64-bit sizes (B7),
+ * no fixed line buffers, and no 32-query interleave: the device packs
+ * queries itself (csrc/hip/kfmi_search.hip, pack kernel), so queries stay in
+ * the plain layout `q*size` (common.c:163-173 without -DINTERLEAVING_QUERIES).
+ */
+#define _GNU_SOURCE
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#include "../kfmi_internal.h"
+
+/* common.c:28-33 (monotonic instead of CLOCK_REALTIME) */
+double sampleTime(void)
+{
+  struct timespec tv;
+  clock_gettime(CLOCK_MONOTONIC, &tv);
+  return (double) tv.tv_sec + (double) tv.tv_nsec / 1e9;
+}
+
+/* genFMindex.c:71-84: A/a=0 C/c=1 G/g=2 T/t=3, N->2, by ASCII bits 1..2 */
+uint32_t base2index(uint32_t base)
+{
+  uint32_t f2 = base & 0x02u, b1 = base & 0x04u;
+  uint32_t b0 = b1 ? (f2 ^ 0x02u) : f2;
+  return (b1 | b0) >> 1;
+}
+
+/* ----------------------------------------------------------------------- */
+/* reference text (common.c:42-130)                                        */
+/* ----------------------------------------------------------------------- */
+
+/* Reads the first `refsize` sequence characters of a (multi-)FASTA file; the
+ * first line must be a '>' header (common.c:59-62); later lines are
+ * concatenated with their line terminator removed. */
+static int32_t read_ref(const char *fn, uint64_t refsize, char **out, uint64_t *got)
+{
+  FILE *fp = fopen(fn, "rb");
+  char *ref, *line = NULL;
+  size_t cap = 0;
+  ssize_t len;
+  uint64_t pos = 0;
+  if (!fp) return KFMI_E_OPENING_REFERENCE_FILE;
+  ref = (char *) malloc(refsize ? refsize : 1);
+  if (!ref) { fclose(fp); return KFMI_E_ALLOCATING_REFERENCE; }
+  len = getline(&line, &cap, fp);
+  if (len <= 0) { free(ref); free(line); fclose(fp); return KFMI_E_READING_REFERENCE_FILE; }
+  if (line[0] != '>') { free(ref); free(line); fclose(fp); return KFMI_E_READING_MFASTA_FILE; }
+  while (pos < refsize && (len = getline(&line, &cap, fp)) > 0) {
+    while (len > 0 && (line[len - 1] == '\n' || line[len - 1] == '\r')) len--;
+    if (len > 0 && line[0] == '>') continue;
+    if ((uint64_t) len > refsize - pos) len = (ssize_t) (refsize - pos);
+    memcpy(ref + pos, line, (size_t) len);
+    pos += (uint64_t) len;
+  }
+  free(line);
+  fclose(fp);
+  *out = ref;
+  *got = pos;
+  return KFMI_SUCCESS;
+}
+
+int32_t loadRef(const char *fn, uint32_t refsize, void **reference)
+{
+  kfmi_ref_t *ref = (kfmi_ref_t *) calloc(1, sizeof(*ref));
+  uint64_t got = 0;
+  int32_t err;
+  if (!ref) return KFMI_E_ALLOCATING_REFERENCE;
+  err = read_ref(fn, refsize, &ref->h_reference, &got);
+  if (err) { free(ref); return err; }
+  if (got != refsize) { free(ref->h_reference); free(ref); return KFMI_E_READING_REFERENCE_FILE; }
+  ref->size = got;
+  *reference = ref;
+  return KFMI_SUCCESS;
+}
+
+/* common.c:88-130: "<fn>.<size>.fa", header "> <size>", 70-column lines */
+int32_t saveRef(const char *fn, void *reference)
+{
+  kfmi_ref_t *ref = (kfmi_ref_t *) reference;
+  char name[1024];
+  FILE *fp;
+  uint64_t i;
+  snprintf(name, sizeof(name), "%s.%llu.fa", fn, (unsigned long long) ref->size);
+  fp = fopen(name, "wb");
+  if (!fp) return KFMI_E_OPENING_REFERENCE_FILE;
+  fprintf(fp, "> %llu", (unsigned long long) ref->size);
+  for (i = 0; i < ref->size; i += 70) {
+    uint64_t l = ref->size - i < 70 ? ref->size - i : 70;
+    fputc('\n', fp);
+    fwrite(ref->h_reference + i, 1, l, fp);
+  }
+  fputc('\n', fp);
+  fclose(fp);
+  return KFMI_SUCCESS;
+}
+
+/* common.c:313-322 */
+int32_t freeReference(void **reference, void **index)
+{
+  kfmi_ref_t *ref = reference ? (kfmi_ref_t *) *reference : NULL;
+  (void) index;
+  if (ref && ref->h_reference) { free(ref->h_reference); ref->h_reference = NULL; }
+  return KFMI_SUCCESS;
+}
+
+/* ----------------------------------------------------------------------- */
+/* queries (common.c:132-199)                                              */
+/* ----------------------------------------------------------------------- */
+
+/* Multi-FASTA reads: '>' lines are skipped, every other line is one read of
+ * exactly `sizequery` characters (common.c:167-173 copies strlen-1 bytes per
+ * line; a line of another length is an error here instead of silently
+ * shifting every following read).  Reads beyond `numqueries` are ignored;
+ * fewer reads than `numqueries` is an error. */
+int32_t loadQueries(const char *fn, uint32_t sizequery, uint32_t numqueries, void **queries)
+{
+  kfmi_qrys_t *q;
+  FILE *fp;
+  char *line = NULL;
+  size_t cap = 0;
+  ssize_t len;
+  uint64_t i = 0;
+  if (sizequery == 0) return KFMI_E_BAD_ARGUMENT;
+  fp = fopen(fn, "rb");
+  if (!fp) return KFMI_E_OPENING_MFASTA_FILE;
+  q = (kfmi_qrys_t *) calloc(1, sizeof(*q));
+  if (!q) { fclose(fp); return KFMI_E_ALLOCATING_MFASTA; }
+  q->num = numqueries;
+  q->size = sizequery;
+  q->h_queries = (char *) malloc((size_t) numqueries * sizequery + 1);
+  if (!q->h_queries) { free(q); fclose(fp); return KFMI_E_ALLOCATING_MFASTA; }
+  while (i < numqueries && (len = getline(&line, &cap, fp)) > 0) {
+    if (line[0] == '>') continue;
+    while (len > 0 && (line[len - 1] == '\n' || line[len - 1] == '\r')) len--;
+    if ((uint64_t) len != sizequery) {
+      free(line); free(q->h_queries); free(q); fclose(fp);
+      return KFMI_E_READING_MFASTA_FILE;
+    }
+    memcpy(q->h_queries + i * sizequery, line, sizequery);
+    i++;
+  }
+  free(line);
+  fclose(fp);
+  if (i != numqueries) { free(q->h_queries); free(q); return KFMI_E_READING_MFASTA_FILE; }
+  *queries = q;
+  return KFMI_SUCCESS;
+}
+
+int32_t kfmi_queries_from_buffer(const char *ascii, uint64_t num, uint32_t size, void **queries)
+{
+  kfmi_qrys_t *q;
+  if (size == 0 || (!ascii && num)) return KFMI_E_BAD_ARGUMENT;
+  q = (kfmi_qrys_t *) calloc(1, sizeof(*q));
+  if (!q) return KFMI_E_ALLOCATING_MFASTA;
+  q->num = num;
+  q->size = size;
+  q->h_queries = (char *) malloc(num * size + 1);
+  if (!q->h_queries) { free(q); return KFMI_E_ALLOCATING_MFASTA; }
+  if (num) memcpy(q->h_queries, ascii, num * size);
+  *queries = q;
+  return KFMI_SUCCESS;
+}
+
+/* common.c:262-270 (also releases the handle) */
+int32_t freeQueries(void **queries)
+{
+  kfmi_qrys_t *q = queries ? (kfmi_qrys_t *) *queries : NULL;
+  if (!q) return KFMI_SUCCESS;
+  if (q->dev) freeQueriesGPU(queries);
+  free(q->h_queries);
+  free(q);
+  *queries = NULL;
+  return KFMI_SUCCESS;
+}
+
+/* ----------------------------------------------------------------------- */
+/* results (common.c:201-260, 324-341)                                     */
+/* ----------------------------------------------------------------------- */
+
+int32_t kfmi_results_alloc(uint64_t num, void **results)
+{
+  kfmi_res_t *r = (kfmi_res_t *) calloc(1, sizeof(*r));
+  if (!r) return KFMI_E_ALLOCATING_RESULTS;
+  r->num = num;
+  r->h_results = (uint32_t *) calloc(2 * num + 1, sizeof(uint32_t));
+  if (!r->h_results) { free(r); return KFMI_E_ALLOCATING_RESULTS; }
+  *results = r;
+  return KFMI_SUCCESS;
+}
+
+int32_t initResults(uint32_t numresults, void **results)
+{
+  return kfmi_results_alloc(numresults, results);
+}
+
+uint32_t *kfmi_results_host(void *results) { return results ? ((kfmi_res_t *) results)->h_results : NULL; }
+uint64_t  kfmi_results_num(void *results)  { return results ? ((kfmi_res_t *) results)->num : 0; }
+
+int32_t freeResults(void **results)
+{
+  kfmi_res_t *r = results ? (kfmi_res_t *) *results : NULL;
+  if (!r) return KFMI_SUCCESS;
+  if (r->d_results) freeResultsGPU(results);
+  free(r->h_results);
+  free(r);
+  *results = NULL;
+  return KFMI_SUCCESS;
+}
+
+static char *put_u32(char *p, uint32_t v)
+{
+  char tmp[12];
+  int n = 0;
+  do { tmp[n++] = (char) ('0' + v % 10); v /= 10; } while (v);
+  while (n) *p++ = tmp[--n];
+  return p;
+}
+
+static int32_t write_results64(const char *fn, const uint32_t *res, uint64_t num)
+{
+  FILE *fp = fopen(fn, "wb");
+  char *buf, *p;
+  const size_t chunk = 1u << 20;
+  uint64_t i;
+  if (!fp) return KFMI_E_OPENING_RESULTS_FILE;
+  buf = (char *) malloc(chunk * 24 + 32);
+  if (!buf) { fclose(fp); return KFMI_E_ALLOCATING_RESULTS; }
+  p = buf;
+  p += sprintf(p, "%llu\n", (unsigned long long) num);
+  for (i = 0; i < num; i++) {
+    p = put_u32(p, res[2 * i]); *p++ = ' ';
+    p = put_u32(p, res[2 * i + 1]); *p++ = '\n';
+    if ((size_t) (p - buf) >= chunk * 22) { fwrite(buf, 1, (size_t) (p - buf), fp); p = buf; }
+  }
+  fwrite(buf, 1, (size_t) (p - buf), fp);
+  free(buf);
+  fclose(fp);
+  return KFMI_SUCCESS;
+}
+
+/* common.c:201-220: "N\n" then "L R\n" per query */
+int32_t writeResults(const char *fn, uint32_t *results, uint32_t numqueries)
+{
+  return write_results64(fn, results, numqueries);
+}
+
+/* common.c:222-246 */
+int32_t loadResults(const char *fn, void **results)
+{
+  FILE *fp = fopen(fn, "rb");
+  unsigned long long n;
+  uint64_t i;
+  kfmi_res_t *r;
+  int32_t err;
+  if (!fp) return KFMI_E_OPENING_RESULTS_FILE;
+  if (fscanf(fp, "%llu", &n) != 1) { fclose(fp); return KFMI_E_READING_RESULTS_FILE; }
+  err = kfmi_results_alloc(n, (void **) &r);
+  if (err) { fclose(fp); return err; }
+  for (i = 0; i < n; i++) {
+    if (fscanf(fp, "%u %u", &r->h_results[2 * i], &r->h_results[2 * i + 1]) != 2) {
+      fclose(fp); freeResults((void **) &r); return KFMI_E_READING_RESULTS_FILE;
+    }
+  }
+  fclose(fp);
+  *results = r;
+  return KFMI_SUCCESS;
+}
+
+/* common.c:324-341 (GPU build: "<fn>.res.gpu") */
+int32_t saveResults(const char *fn, void *results, void *index)
+{
+  kfmi_res_t *r = (kfmi_res_t *) results;
+  char name[1024];
+  (void) index;
+  snprintf(name, sizeof(name), "%s.res.gpu", fn);
+  return write_results64(name, r->h_results, r->num);
+}
+
+/* common.c:282-310 */
+char *errorCommon(int32_t e)
+{
+  switch (e) {
+    case KFMI_SUCCESS:                  return "No error";
+    case KFMI_E_OPENING_INDEX_FILE:     return "Cannot open index file";
+    case KFMI_E_ALLOCATING_BWT:         return "Cannot allocate memory for bwt";
+    case KFMI_E_ALLOCATING_FMI:         return "Cannot allocate memory for counters";
+    case KFMI_E_READING_BWT:            return "Error reading index bwt";
+    case KFMI_E_READING_FMI:            return "Error reading index counters";
+    case KFMI_E_SAVING_INDEX_FILE:      return "Cannot open index file for save";
+    case KFMI_E_SAVING_BWT_FILE:        return "Cannot open bwt file for save";
+    case KFMI_E_BUILDING_BWT:           return "Error building bwt";
+    case KFMI_E_BUILDING_FMI:           return "Error building FMI, cannot allocate memory for bwt";
+    case KFMI_E_OPENING_REFERENCE_FILE: return "Cannot open reference file";
+    case KFMI_E_ALLOCATING_REFERENCE:   return "Cannot allocate reference";
+    case KFMI_E_READING_MFASTA_FILE:    return "Reference file isn't MFASTA format";
+    case KFMI_E_READING_REFERENCE_FILE: return "Error reading reference file";
+    case KFMI_E_OPENING_MFASTA_FILE:    return "Cannot open MFASTS queries file";
+    case KFMI_E_ALLOCATING_MFASTA:      return "Cannot allocate MFASTA queries";
+    case KFMI_E_ALLOCATING_RESULTS:     return "Cannot allocate results";
+    case KFMI_E_OPENING_RESULTS_FILE:   return "Cannot open results file for load intervals";
+    case KFMI_E_READING_RESULTS_FILE:   return "Error reading results";
+    case KFMI_E_NOT_IMPLEMENTED:        return "Not implemented";
+    case KFMI_E_NO_DEVICE:              return "No usable HIP device (HIP runtime error)";
+    case KFMI_E_DEVICE_ALLOC:           return "Cannot allocate device memory";
+    case KFMI_E_KERNEL:                 return "HIP kernel launch or execution failed";
+    case KFMI_E_BAD_ARGUMENT:           return "Unsupported argument (K, d, query size or backend)";
+    case KFMI_E_NOT_ON_DEVICE:          return "Index/queries/results not transferred to the device";
+    case KFMI_INDEX_VER_BASELINE:       return "Error in the index type, use gfmiBaseLine_*Bases_*Step to generate an index_name.fmi type";
+    case KFMI_INDEX_VER_INTERLEAVE:     return "Error in the index type, use tfmiBMP_*Bases_*Step to generate an index_name.fmi.interleaving type";
+    case KFMI_INDEX_VER_BASELINE_AC:    return "Error in the index type, use tfmiAC_*Bases_*Step to generate an index_name.fmi.ac type";
+    case KFMI_INDEX_VER_INTERLEAVE_AC:  return "Error in the index type, use tfmiAC_*Bases_*Step to generate an index_name.fmi.interleaving.ac type";
+    default:                            return "Unknown error";
+  }
+}

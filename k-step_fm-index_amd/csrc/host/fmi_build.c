@@ -1,0 +1,290 @@
+/*
+ * fmi_build.c -- host index builder (the reference's genFMindex.c:457-543,
+ * restated on a suffix array instead of libdivsufsort + an LF walk).
+ *
+ * Construction (bit-exact with genFMindex.c output, pinned by md5 in tests):
+ *   SA       : suffix array of T$ ('$' lowest), own SA-IS below
+ *   BWT_s[r] : (T$)[(SA[r] - 1 - s) mod (n+1)]          (generateOthersBWTs :327-400)
+ *   D_s      : the row with SA[r] == s                  (dollarPositionBWT)
+ *   '$' is stored as A in every BWT_s                    (:505-509)
+ *   c(r)     : sum_s code(BWT_s[r]) << 2s
+ *   cnt_b[c] : C'[c] + #{r < b*d : r not in D, c(r) == c}  (precalculateBasesKSteps :184-260)
+ *   C'[c]    : sum_{c'<c} total(c') + #{s : (c(D_s) & (~0 << 2s)) <= c}
+ *   planes   : bit 31-p of plane (s,t,w) of entry b = bit t of code(BWT_s[b*d+32w+p]),
+ *              rows >= n+1 are 0 (bwt2bin :402-455)
+ *   dollarBaseBWT[s] = c(D_s)
+ * The text must be A/C/G/T only: the reference builder's LF walk only counts
+ * those four letters (precalculateBasesPreviousBWT :283-309) and produces a
+ * broken index for anything else, so other letters are rejected here.
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include "../kfmi_internal.h"
+
+#define EMPTY 0xFFFFFFFFu
+
+/* ----------------------------------------------------------------------- */
+/* SA-IS (Nong, Zhang & Chan 2009) over 32-bit indexes.                    */
+/* T has n symbols in [0, alpha) and T[n-1] == 0 is a unique sentinel.     */
+/* ----------------------------------------------------------------------- */
+
+typedef struct {
+  const void *t;
+  int wide;            /* 0: uint8_t symbols, 1: uint32_t symbols */
+} sym_t;
+
+static inline uint32_t SYM(const sym_t *s, uint32_t i)
+{
+  return s->wide ? ((const uint32_t *) s->t)[i] : ((const uint8_t *) s->t)[i];
+}
+
+#define TGET(tb, i) (((tb)[(i) >> 3] >> ((i) & 7)) & 1u)
+#define TSET(tb, i, v) ((tb)[(i) >> 3] = (uint8_t) (((tb)[(i) >> 3] & ~(1u << ((i) & 7))) | ((v) << ((i) & 7))))
+#define IS_LMS(tb, i) ((i) > 0 && TGET(tb, i) && !TGET(tb, (i) - 1))
+
+static void buckets(const sym_t *s, uint32_t n, uint32_t *bkt, uint32_t alpha, int ends)
+{
+  uint32_t i, sum = 0;
+  memset(bkt, 0, sizeof(uint32_t) * (alpha + 1));
+  for (i = 0; i < n; i++) bkt[SYM(s, i)]++;
+  for (i = 0; i < alpha; i++) {
+    sum += bkt[i];
+    bkt[i] = ends ? sum : sum - bkt[i];
+  }
+}
+
+static void induce(const sym_t *s, const uint8_t *tb, uint32_t *sa, uint32_t n, uint32_t *bkt, uint32_t alpha)
+{
+  uint32_t i, j;
+  buckets(s, n, bkt, alpha, 0);
+  for (i = 0; i < n; i++) {
+    j = sa[i];
+    if (j != EMPTY && j > 0 && !TGET(tb, j - 1)) sa[bkt[SYM(s, j - 1)]++] = j - 1;
+  }
+  buckets(s, n, bkt, alpha, 1);
+  for (i = n; i-- > 0;) {
+    j = sa[i];
+    if (j != EMPTY && j > 0 && TGET(tb, j - 1)) sa[--bkt[SYM(s, j - 1)]] = j - 1;
+  }
+}
+
+static int sais_rec(const sym_t *s, uint32_t *sa, uint32_t n, uint32_t alpha)
+{
+  uint8_t *tb;
+  uint32_t *bkt;
+  uint32_t i, j, n1, name, prev;
+  if (n == 1) { sa[0] = 0; return 0; }
+  tb = (uint8_t *) calloc(n / 8 + 1, 1);
+  bkt = (uint32_t *) malloc(sizeof(uint32_t) * (alpha + 1));
+  if (!tb || !bkt) { free(tb); free(bkt); return -1; }
+
+  /* S/L types: T[n-1] is S; T[i] is S iff T[i] < T[i+1] or equal and T[i+1] is S */
+  TSET(tb, n - 1, 1u);
+  for (i = n - 1; i-- > 0;) {
+    uint32_t a = SYM(s, i), b = SYM(s, i + 1);
+    TSET(tb, i, (a < b || (a == b && TGET(tb, i + 1))) ? 1u : 0u);
+  }
+
+  /* stage 1: sort the LMS substrings by induction */
+  buckets(s, n, bkt, alpha, 1);
+  for (i = 0; i < n; i++) sa[i] = EMPTY;
+  for (i = 1; i < n; i++)
+    if (IS_LMS(tb, i)) sa[--bkt[SYM(s, i)]] = i;
+  induce(s, tb, sa, n, bkt, alpha);
+
+  /* compact the sorted LMS positions into sa[0..n1) */
+  n1 = 0;
+  for (i = 0; i < n; i++)
+    if (IS_LMS(tb, sa[i])) sa[n1++] = sa[i];
+
+  /* name the LMS substrings (equal substrings get equal names) */
+  for (i = n1; i < n; i++) sa[i] = EMPTY;
+  name = 0;
+  prev = EMPTY;
+  for (i = 0; i < n1; i++) {
+    uint32_t pos = sa[i], d;
+    int diff = 0;
+    for (d = 0;; d++) {
+      if (prev == EMPTY || pos + d >= n || prev + d >= n || SYM(s, pos + d) != SYM(s, prev + d) ||
+          TGET(tb, pos + d) != TGET(tb, prev + d)) {
+        diff = 1;
+        break;
+      }
+      if (d > 0 && (IS_LMS(tb, pos + d) || IS_LMS(tb, prev + d))) break;
+    }
+    if (diff) { name++; prev = pos; }
+    sa[n1 + pos / 2] = name - 1;
+  }
+  for (i = n, j = n; i-- > n1;)
+    if (sa[i] != EMPTY) sa[--j] = sa[i];
+
+  /* stage 2: sort the reduced string (recursively if names repeat) */
+  {
+    uint32_t *s1 = sa + n - n1;
+    if (name < n1) {
+      sym_t r = {s1, 1};
+      if (sais_rec(&r, sa, n1, name)) { free(tb); free(bkt); return -1; }
+    } else {
+      for (i = 0; i < n1; i++) sa[s1[i]] = i;
+    }
+    /* stage 3: induce the full SA from the sorted LMS suffixes */
+    for (i = 1, j = 0; i < n; i++)
+      if (IS_LMS(tb, i)) s1[j++] = i;
+    for (i = 0; i < n1; i++) sa[i] = s1[sa[i]];
+    for (i = n1; i < n; i++) sa[i] = EMPTY;
+    buckets(s, n, bkt, alpha, 1);
+    for (i = n1; i-- > 0;) {
+      j = sa[i];
+      sa[i] = EMPTY;
+      sa[--bkt[SYM(s, j)]] = j;
+    }
+  }
+  induce(s, tb, sa, n, bkt, alpha);
+  free(tb);
+  free(bkt);
+  return 0;
+}
+
+/* SA of text_codes[0..n) where text_codes[n-1] == 0 is the unique sentinel. */
+int32_t kfmi_sais(const uint8_t *text_codes, uint32_t *sa, uint32_t n, uint32_t alpha)
+{
+  sym_t s = {text_codes, 0};
+  if (n == 0) return KFMI_SUCCESS;
+  return sais_rec(&s, sa, n, alpha) ? KFMI_E_BUILDING_BWT : KFMI_SUCCESS;
+}
+
+/* ----------------------------------------------------------------------- */
+/* tag-100 index from the suffix array of T$                               */
+/* ----------------------------------------------------------------------- */
+
+/* codes: T as 2-bit codes (0..3), n symbols; sa: n+1 rows of T$ (sa[0] == n) */
+int32_t kfmi_index_from_sa(const uint8_t *codes, const uint32_t *sa, uint64_t n, uint32_t k, uint32_t d,
+                           kfmi_fmi_t **out)
+{
+  const uint64_t rows = n + 1;
+  const uint32_t nc = 1u << (2 * k), nb = d / 32;
+  uint32_t nentries, s, c, dpos[KFMI_MAX_STEPS], dbase[KFMI_MAX_STEPS];
+  uint64_t *total, r;
+  uint32_t *cprime;
+  kfmi_fmi_t *f;
+  int32_t err;
+  if (k < 1 || k > KFMI_MAX_STEPS || d == 0 || d % 32 || rows > 0xFFFFFFFFull) return KFMI_E_BAD_ARGUMENT;
+  nentries = (uint32_t) ((rows + d - 1) / d);
+  for (s = 0; s < k; s++) { dpos[s] = 0; dbase[s] = 0; }
+  err = kfmi_index_alloc(100, k, (uint32_t) rows, nentries, d, NULL, NULL, &f);
+  if (err) return err;
+  total = (uint64_t *) calloc(nc, sizeof(uint64_t));
+  cprime = (uint32_t *) calloc(nc, sizeof(uint32_t));
+  if (!total || !cprime) { free(total); free(cprime); freeIndex((void **) &f); return KFMI_E_ALLOCATING_FMI; }
+
+  /* D_s first (rows whose suffix starts at s): needed to exclude them while counting */
+  for (r = 0; r < rows; r++)
+    if (sa[r] < k) dpos[sa[r]] = (uint32_t) r;
+
+  {
+    uint32_t *run = (uint32_t *) calloc(nc, sizeof(uint32_t));
+    const uint32_t ew = f->entry_words, nbw = 2 * nb * k;
+    if (!run) { free(total); free(cprime); freeIndex((void **) &f); return KFMI_E_ALLOCATING_FMI; }
+    for (r = 0; r < rows; r++) {
+      const uint64_t b = r / d;
+      const uint32_t off = (uint32_t) (r % d), w = off / 32, p = off % 32;
+      uint32_t *ent = f->h_index + b * ew;
+      uint32_t code = 0, isd = 0;
+      if (off == 0) memcpy(ent + nbw, run, sizeof(uint32_t) * nc);   /* Occ before block b */
+      for (s = 0; s < k; s++) {
+        /* BWT_s[r] = (T$)[(SA[r]-1-s) mod (n+1)], '$' -> A */
+        int64_t pos = (int64_t) sa[r] - 1 - (int64_t) s;
+        uint32_t cs;
+        if (pos < 0) pos += (int64_t) rows;
+        cs = ((uint64_t) pos == n) ? 0u : codes[pos];
+        code |= cs << (2 * s);
+        if (cs & 1u) ent[kfmi_plane_index(100, k, nb, s, 0, w)] |= 1u << (31 - p);
+        if (cs & 2u) ent[kfmi_plane_index(100, k, nb, s, 1, w)] |= 1u << (31 - p);
+      }
+      for (s = 0; s < k; s++) if (dpos[s] == r) { isd = 1; dbase[s] = code; }
+      if (!isd) { run[code]++; total[code]++; }
+    }
+    free(run);
+  }
+  /* C'[c] = sum_{c'<c} total(c') + #{s : (c(D_s) & (~0 << 2s)) <= c} */
+  {
+    uint64_t acc = 0;
+    for (c = 0; c < nc; c++) { cprime[c] = (uint32_t) acc; acc += total[c]; }
+    for (s = 0; s < k; s++) {
+      uint32_t masked = dbase[s] & (0xFFFFFFFFu << (2 * s));
+      for (c = masked; c < nc; c++) cprime[c]++;
+    }
+  }
+  {
+    const uint32_t ew = f->entry_words, nbw = 2 * nb * k;
+    uint64_t b;
+    for (b = 0; b < nentries; b++) {
+      uint32_t *cnt = f->h_index + b * ew + nbw;
+      for (c = 0; c < nc; c++) cnt[c] += cprime[c];
+    }
+  }
+  for (s = 0; s < k; s++) {
+    f->dollarPositionBWT[s] = dpos[s];
+    f->dollarBaseBWT[s] = dbase[s];
+    f->modposdollarBWT[s] = dpos[s] / d;
+  }
+  {
+    const void *img; uint64_t bytes;
+    kfmi_index_image(f, &img, &bytes);   /* refresh header words */
+  }
+  free(total);
+  free(cprime);
+  *out = f;
+  return KFMI_SUCCESS;
+}
+
+static int text_to_codes(const char *text, uint64_t n, uint8_t *codes)
+{
+  uint64_t i;
+  for (i = 0; i < n; i++) {
+    switch (text[i]) {
+      case 'A': codes[i] = 0; break;
+      case 'C': codes[i] = 1; break;
+      case 'G': codes[i] = 2; break;
+      case 'T': codes[i] = 3; break;
+      default: return -1;
+    }
+  }
+  return 0;
+}
+
+int32_t kfmi_build_index_cpu(const char *text, uint64_t n, uint32_t k, uint32_t d, void **index)
+{
+  uint8_t *codes, *sym;
+  uint32_t *sa;
+  uint64_t i;
+  int32_t err;
+  if (n == 0 || n + 1 > 0xFFFFFFFEull) return KFMI_E_BAD_ARGUMENT;
+  if (k < 1 || k > KFMI_MAX_STEPS || d == 0 || d % 32) return KFMI_E_BAD_ARGUMENT;
+  codes = (uint8_t *) malloc(n);
+  sym = (uint8_t *) malloc(n + 1);
+  sa = (uint32_t *) malloc(sizeof(uint32_t) * (n + 1));
+  if (!codes || !sym || !sa) { free(codes); free(sym); free(sa); return KFMI_E_ALLOCATING_BWT; }
+  if (text_to_codes(text, n, codes)) { free(codes); free(sym); free(sa); return KFMI_E_BUILDING_BWT; }
+  for (i = 0; i < n; i++) sym[i] = (uint8_t) (codes[i] + 1);   /* '$' = 0 < A..T = 1..4 */
+  sym[n] = 0;
+  err = kfmi_sais(sym, sa, (uint32_t) (n + 1), 5);
+  free(sym);
+  if (!err) err = kfmi_index_from_sa(codes, sa, n, k, d, (kfmi_fmi_t **) index);
+  free(codes);
+  free(sa);
+  return err;
+}
+
+/* interface.h:35: K, d from KFMI_K / KFMI_D (the reference: -DK_STEPS, -DNUM_CHUNK). */
+int32_t buildIndex(void *reference, void **index)
+{
+  kfmi_ref_t *ref = (kfmi_ref_t *) reference;
+  const char *ek = getenv("KFMI_K"), *ed = getenv("KFMI_D"), *eg = getenv("KFMI_BUILD_GPU");
+  uint32_t k = ek ? (uint32_t) atoi(ek) : 2, d = ed ? (uint32_t) atoi(ed) : 64;
+  int use_gpu = eg ? atoi(eg) : (kfmi_device_count() > 0);
+  if (!ref) return KFMI_E_BAD_ARGUMENT;
+  if (use_gpu) return kfmi_build_index_gpu(ref->h_reference, ref->size, k, d, 1, index);
+  return kfmi_build_index_cpu(ref->h_reference, ref->size, k, d, index);
+}

@@ -1,0 +1,86 @@
+/*
+ * kfmi_internal.h -- host structures shared by the C host layer (csrc/host)
+ * and the HIP layer (csrc/hip).  Not part of the public ABI: callers only
+ * see opaque `void *` handles (include/kstep_fmi.h).
+ *
+ * Field meanings follow the reference handles (fmIndexCPUBaseline.c:54-69,
+ * common.h:64-81) with 64-bit sizes where the reference overflows (B7).
+ */
+#ifndef KFMI_INTERNAL_H_
+#define KFMI_INTERNAL_H_
+
+#include <stdint.h>
+#include <stddef.h>
+#include "../../include/kstep_fmi.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KFMI_MAX_STEPS 4
+
+struct kfmi_dev_index;   /* device-resident layouts, defined in csrc/hip */
+struct kfmi_dev_queries;
+
+typedef struct {
+  /* header, genFMindex.c:167-178 */
+  uint32_t tag, steps, bwtsize, ncounters, nentries, chunk;
+  uint32_t dollarPositionBWT[KFMI_MAX_STEPS];
+  uint32_t dollarBaseBWT[KFMI_MAX_STEPS];
+  uint32_t modposdollarBWT[KFMI_MAX_STEPS];   /* = dollarPositionBWT / chunk */
+  uint32_t nbitmaps;       /* 32-bit words per bit-plane row = chunk / 32 */
+  uint32_t entry_words;    /* u32 words per entry for this tag */
+  /* file image: header followed by nentries entries, one allocation */
+  uint8_t  *image;
+  uint64_t  image_bytes;
+  uint32_t  header_bytes;
+  uint32_t *h_index;       /* = (uint32_t *)(image + header_bytes), may be unaligned to 16 */
+  struct kfmi_dev_index *dev;
+  char      src_name[512]; /* file the index came from (for saveIndex/saveResults naming) */
+} kfmi_fmi_t;
+
+typedef struct {
+  uint64_t num;
+  uint32_t size;
+  char    *h_queries;      /* num*size ASCII, query q at q*size (plain layout) */
+  struct kfmi_dev_queries *dev;
+} kfmi_qrys_t;
+
+typedef struct {
+  uint64_t  num;
+  uint32_t *h_results;     /* 2*num: [L0,R0,L1,R1,...] */
+  uint32_t *d_results;     /* device copy (hipMalloc), NULL until transfer */
+} kfmi_res_t;
+
+typedef struct {
+  uint64_t size;
+  char    *h_reference;
+} kfmi_ref_t;
+
+/* fmi_index.c */
+int32_t kfmi_index_alloc(uint32_t tag, uint32_t steps, uint32_t bwtsize, uint32_t nentries,
+                         uint32_t chunk, const uint32_t *dpos, const uint32_t *dbase,
+                         kfmi_fmi_t **out);
+uint32_t kfmi_entry_words(uint32_t tag, uint32_t steps, uint32_t chunk);
+uint32_t kfmi_plane_index(uint32_t tag, uint32_t steps, uint32_t nb, uint32_t s, uint32_t t, uint32_t w);
+
+/* backend registry, fmi_backend.c */
+typedef enum {
+  KFMI_BK_TASK = 0, KFMI_BK_COOP, KFMI_BK_TASK_AC, KFMI_BK_COOP_AC,
+  KFMI_BK_TASK_PACKED, KFMI_BK_COOP_PACKED, KFMI_BK_COUNT
+} kfmi_backend_t;
+kfmi_backend_t kfmi_backend(void);
+uint32_t       kfmi_backend_tag(kfmi_backend_t b);   /* 101 or 201 */
+int32_t        kfmi_current_device(void);
+void           kfmi_set_last_error(int32_t e);
+
+/* suffix array construction, fmi_build.c */
+int32_t kfmi_sais(const uint8_t *text_codes, uint32_t *sa, uint32_t n, uint32_t alpha);
+int32_t kfmi_index_from_sa(const uint8_t *codes, const uint32_t *sa, uint64_t n,
+                           uint32_t k, uint32_t d, kfmi_fmi_t **out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* KFMI_INTERNAL_H_ */

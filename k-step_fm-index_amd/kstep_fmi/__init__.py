@@ -1,0 +1,313 @@
+"""kstep_fmi -- Python host binding of libkstepfmi.so (include/kstep_fmi.h).
+
+This is the ctypes form of the reference's link-time plugin interface
+(/root/reference/common/interface.h:27-41): the same entry points, argument
+meaning and error codes, over opaque handles.  It is plumbing for the test
+suite, bench.py and multi-GPU runs; the engine itself is the C ABI library
+(HIP kernels for gfx950 + C host code) and there is no Python or CPU fallback
+for the search: if the library or a GPU is missing, calls fail loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+PKG_DIR = Path(__file__).resolve().parent.parent          # k-step_fm-index_amd/
+LIB_PATH = PKG_DIR / "lib" / "libkstepfmi.so"
+BIN_DIR = PKG_DIR / "bin"
+
+BACKENDS = ("task", "coop", "task-ac", "coop-ac", "task-packed", "coop-packed")
+BACKEND_TAG = {"task": 101, "coop": 101, "task-ac": 201, "coop-ac": 201,
+               "task-packed": 101, "coop-packed": 101}
+
+_lib = None
+
+
+class KfmiError(RuntimeError):
+    def __init__(self, code: int, what: str = ""):
+        self.code = code
+        msg = _lib.errorCommon(code).decode() if _lib is not None else f"error {code}"
+        super().__init__(f"{what}: {msg} (code {code})" if what else f"{msg} (code {code})")
+
+
+def build(jobs: int = 8) -> None:
+    """Compile the HIP + C library and tools in-tree (hipcc --offload-arch=gfx950)."""
+    subprocess.run(["make", "-C", str(PKG_DIR), f"-j{jobs}"], check=True)
+
+
+def load() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise FileNotFoundError(f"{LIB_PATH} not built -- run kstep_fmi.build() / make -C {PKG_DIR}")
+    L = ctypes.CDLL(str(LIB_PATH), mode=ctypes.RTLD_GLOBAL)
+    vp, u32, u64, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int32
+    pvp = ctypes.POINTER(ctypes.c_void_p)
+    sig = {
+        "loadIndex": (i32, [ctypes.c_char_p, pvp]),
+        "saveIndex": (i32, [ctypes.c_char_p, vp]),
+        "initResults": (i32, [u32, pvp]),
+        "searchIndexGPU": (None, [vp, vp, vp]),
+        "freeIndex": (i32, [pvp]),
+        "freeReference": (i32, [pvp, pvp]),
+        "buildIndex": (i32, [vp, pvp]),
+        "freeQueriesGPU": (i32, [pvp]),
+        "freeResultsGPU": (i32, [pvp]),
+        "freeIndexGPU": (i32, [pvp]),
+        "transferGPUtoCPU": (i32, [vp]),
+        "transferCPUtoGPU": (i32, [vp, vp, vp]),
+        "sampleTime": (ctypes.c_double, []),
+        "base2index": (u32, [u32]),
+        "loadRef": (i32, [ctypes.c_char_p, u32, pvp]),
+        "saveRef": (i32, [ctypes.c_char_p, vp]),
+        "loadQueries": (i32, [ctypes.c_char_p, u32, u32, pvp]),
+        "writeResults": (i32, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint32), u32]),
+        "loadResults": (i32, [ctypes.c_char_p, pvp]),
+        "freeQueries": (i32, [pvp]),
+        "freeResults": (i32, [pvp]),
+        "saveResults": (i32, [ctypes.c_char_p, vp, vp]),
+        "errorCommon": (ctypes.c_char_p, [i32]),
+        "kfmi_set_backend": (i32, [ctypes.c_char_p]),
+        "kfmi_get_backend": (ctypes.c_char_p, []),
+        "kfmi_set_device": (i32, [i32]),
+        "kfmi_device_count": (i32, []),
+        "kfmi_last_error": (i32, []),
+        "kfmi_search": (i32, [vp, vp, vp]),
+        "kfmi_last_timing": (i32, [ctypes.POINTER(ctypes.c_double)] * 3),
+        "kfmi_load_index_tag": (i32, [ctypes.c_char_p, u32, pvp]),
+        "kfmi_index_from_image": (i32, [vp, u64, pvp]),
+        "kfmi_index_image": (i32, [vp, pvp, ctypes.POINTER(ctypes.c_uint64)]),
+        "kfmi_index_header": (i32, [vp, vp]),
+        "kfmi_transform_interleave": (i32, [vp, pvp]),
+        "kfmi_transform_ac": (i32, [vp, pvp, pvp]),
+        "kfmi_queries_from_buffer": (i32, [vp, u64, u32, pvp]),
+        "kfmi_results_alloc": (i32, [u64, pvp]),
+        "kfmi_results_host": (ctypes.POINTER(ctypes.c_uint32), [vp]),
+        "kfmi_results_num": (u64, [vp]),
+        "kfmi_build_index_cpu": (i32, [vp, u64, u32, u32, pvp]),
+        "kfmi_build_index_gpu": (i32, [vp, u64, u32, u32, i32, pvp]),
+        "kfmi_count_blocks": (i32, [vp, vp, ctypes.POINTER(ctypes.c_uint64)]),
+        "kfmi_device_index_bytes": (u64, [vp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def exported_symbols():
+    """Names every C-ABI entry point the header declares (for the load test)."""
+    load()
+    return [n for n in _lib.__dict__ if not n.startswith("_")]
+
+
+def _check(code: int, what: str) -> None:
+    if code:
+        raise KfmiError(code, what)
+
+
+def set_backend(name: str) -> None:
+    _check(load().kfmi_set_backend(name.encode()), f"set_backend({name})")
+
+
+def get_backend() -> str:
+    return load().kfmi_get_backend().decode()
+
+
+def set_device(dev: int) -> None:
+    _check(load().kfmi_set_device(int(dev)), f"set_device({dev})")
+
+
+def device_count() -> int:
+    return int(load().kfmi_device_count())
+
+
+def last_timing():
+    t = [ctypes.c_double() for _ in range(3)]
+    load().kfmi_last_timing(*[ctypes.byref(x) for x in t])
+    return {"total_ms": t[0].value, "pack_ms": t[1].value, "lf_ms": t[2].value}
+
+
+class _Handle:
+    _free = ""
+
+    def __init__(self, ptr):
+        self._p = ctypes.c_void_p(ptr)
+
+    @property
+    def ptr(self):
+        return self._p
+
+    def close(self):
+        if self._p and self._p.value:
+            getattr(load(), self._free)(ctypes.byref(self._p))
+            self._p = ctypes.c_void_p(None)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Index(_Handle):
+    """An FM-index (any tag) -- the `fmi_t` handle of fmIndexCPUBaseline.c:54-69."""
+    _free = "freeIndex"
+
+    @classmethod
+    def load(cls, path, required_tag: int = 0) -> "Index":
+        L = load()
+        p = ctypes.c_void_p()
+        if required_tag:
+            _check(L.kfmi_load_index_tag(str(path).encode(), required_tag, ctypes.byref(p)), f"load {path}")
+        else:
+            _check(L.loadIndex(str(path).encode(), ctypes.byref(p)), f"load {path}")
+        return cls(p.value)
+
+    @classmethod
+    def from_image(cls, image) -> "Index":
+        buf = np.ascontiguousarray(np.frombuffer(image, dtype=np.uint8) if isinstance(image, (bytes, bytearray))
+                                   else image).view(np.uint8)
+        p = ctypes.c_void_p()
+        _check(load().kfmi_index_from_image(buf.ctypes.data, buf.nbytes, ctypes.byref(p)), "index_from_image")
+        return cls(p.value)
+
+    @classmethod
+    def build(cls, text: bytes, k: int = 2, d: int = 64, gpu: bool = False, host_image: bool = True) -> "Index":
+        L = load()
+        buf = np.frombuffer(text, dtype=np.uint8)
+        p = ctypes.c_void_p()
+        if gpu:
+            err = L.kfmi_build_index_gpu(buf.ctypes.data, buf.size, k, d, int(host_image), ctypes.byref(p))
+        else:
+            err = L.kfmi_build_index_cpu(buf.ctypes.data, buf.size, k, d, ctypes.byref(p))
+        _check(err, "build_index")
+        return cls(p.value)
+
+    def header(self) -> dict:
+        out = np.zeros(14, dtype=np.uint32)
+        _check(load().kfmi_index_header(self._p, out.ctypes.data), "header")
+        k = int(out[1])
+        return dict(tag=int(out[0]), steps=k, bwtsize=int(out[2]), ncounters=int(out[3]),
+                    nentries=int(out[4]), chunk=int(out[5]),
+                    dollar_pos=[int(x) for x in out[6:6 + k]],
+                    dollar_base=[int(x) for x in out[10:10 + k]])
+
+    def image(self) -> np.ndarray:
+        """Zero-copy view of the serialised file image (header + entries)."""
+        p = ctypes.c_void_p()
+        n = ctypes.c_uint64()
+        _check(load().kfmi_index_image(self._p, ctypes.byref(p), ctypes.byref(n)), "image")
+        return np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint8)), shape=(n.value,))
+
+    def save(self, fn) -> None:
+        _check(load().saveIndex(str(fn).encode(), self._p), f"saveIndex {fn}")
+
+    def interleave(self) -> "Index":
+        p = ctypes.c_void_p()
+        _check(load().kfmi_transform_interleave(self._p, ctypes.byref(p)), "transform_interleave")
+        return Index(p.value)
+
+    def alt_counters(self):
+        a, b = ctypes.c_void_p(), ctypes.c_void_p()
+        _check(load().kfmi_transform_ac(self._p, ctypes.byref(a), ctypes.byref(b)), "transform_ac")
+        return Index(a.value), Index(b.value)
+
+    def device_bytes(self) -> int:
+        return int(load().kfmi_device_index_bytes(self._p))
+
+    def free_gpu(self) -> None:
+        load().freeIndexGPU(ctypes.byref(self._p))
+
+
+class Queries(_Handle):
+    """`qrys_t` (common.h:64-69): num reads of `size` ASCII bases, plain layout."""
+    _free = "freeQueries"
+
+    @classmethod
+    def from_array(cls, q: np.ndarray) -> "Queries":
+        q = np.ascontiguousarray(q, dtype=np.uint8)
+        n, m = q.shape
+        p = ctypes.c_void_p()
+        _check(load().kfmi_queries_from_buffer(q.ctypes.data, n, m, ctypes.byref(p)), "queries_from_buffer")
+        return cls(p.value)
+
+    @classmethod
+    def load(cls, path, size: int, num: int) -> "Queries":
+        p = ctypes.c_void_p()
+        _check(load().loadQueries(str(path).encode(), size, num, ctypes.byref(p)), f"loadQueries {path}")
+        return cls(p.value)
+
+    def free_gpu(self) -> None:
+        load().freeQueriesGPU(ctypes.byref(self._p))
+
+
+class Results(_Handle):
+    """`res_t` (common.h:77-81): 2*num u32 [L0,R0,L1,R1,...]."""
+    _free = "freeResults"
+
+    @classmethod
+    def alloc(cls, num: int) -> "Results":
+        p = ctypes.c_void_p()
+        _check(load().kfmi_results_alloc(num, ctypes.byref(p)), "results_alloc")
+        return cls(p.value)
+
+    def array(self) -> np.ndarray:
+        L = load()
+        n = int(L.kfmi_results_num(self._p))
+        ptr = L.kfmi_results_host(self._p)
+        return np.ctypeslib.as_array(ptr, shape=(2 * n,)) if n else np.zeros(0, dtype=np.uint32)
+
+    def save(self, fn) -> None:
+        _check(load().saveResults(str(fn).encode(), self._p, None), f"saveResults {fn}")
+
+    def free_gpu(self) -> None:
+        load().freeResultsGPU(ctypes.byref(self._p))
+
+
+def transfer_to_gpu(index: Index | None, queries: Queries | None, results: Results | None) -> None:
+    _check(load().transferCPUtoGPU(index.ptr if index else None, queries.ptr if queries else None,
+                                   results.ptr if results else None), "transferCPUtoGPU")
+
+
+def search(index: Index, queries: Queries, results: Results) -> None:
+    _check(load().kfmi_search(index.ptr, queries.ptr, results.ptr), "searchIndexGPU")
+
+
+def transfer_to_cpu(results: Results) -> None:
+    _check(load().transferGPUtoCPU(results.ptr), "transferGPUtoCPU")
+
+
+def count_blocks(index: Index, queries: Queries) -> int:
+    n = ctypes.c_uint64()
+    _check(load().kfmi_count_blocks(index.ptr, queries.ptr, ctypes.byref(n)), "count_blocks")
+    return int(n.value)
+
+
+def search_array(index: Index, queries: np.ndarray, backend: str | None = None) -> np.ndarray:
+    """One-shot GPU search of uint8 [N, m] reads; returns uint32[2N]."""
+    if backend:
+        set_backend(backend)
+    q = Queries.from_array(queries)
+    r = Results.alloc(queries.shape[0])
+    transfer_to_gpu(index, q, r)
+    search(index, q, r)
+    transfer_to_cpu(r)
+    out = r.array().copy()
+    q.close()
+    r.close()
+    return out
+
+
+def env_int(name: str, default: int) -> int:
+    try:
+        return int(os.environ.get(name, default))
+    except ValueError:
+        return default

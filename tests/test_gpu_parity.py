@@ -1,0 +1,180 @@
+"""GPU parity: every backend through the C ABI vs the reference's own result
+files (tests/golden) and vs the CPU oracle (oracle/fmi_oracle.c) on seeded
+inputs.  Bit-exact: the path is integer rank arithmetic.
+
+Run on the GPU box:  python -m pytest tests -m gpu -x -q
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+import util
+from util import GOLDEN, manifest, read_qry
+
+pytestmark = pytest.mark.gpu
+
+PLAIN = ("task", "coop", "task-packed", "coop-packed")
+ALT = ("task-ac", "coop-ac")
+
+
+def coop_supported(backend, k, d):
+    """Geometries the LDS-staged cooperative kernel accepts (16-byte chunks)."""
+    if not backend.startswith("coop"):
+        return True
+    nb = d // 32
+    bmw = 2 * nb * k
+    if backend == "coop-ac":
+        return k == 2 and bmw % 4 == 0
+    if backend == "coop":
+        return bmw % 4 == 0 and (bmw + 4 ** k) % 4 == 0
+    return bmw % 4 == 0
+
+
+@pytest.fixture(scope="module")
+def gpu(kfmi_mod):
+    if kfmi_mod.device_count() < 1:
+        pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
+    kfmi_mod.set_device(0)
+    return kfmi_mod
+
+
+def _cases():
+    for case, c in sorted(manifest().items()):
+        for key, ent in sorted(c["indexes"].items()):
+            yield case, key
+
+
+@pytest.mark.parametrize("backend", PLAIN + ALT)
+@pytest.mark.parametrize("case,key", list(_cases()), ids=[f"{a}-{b}" for a, b in _cases()])
+def test_backend_matches_reference_results(gpu, oracle_mod, backend, case, key):
+    c = manifest()[case]
+    ent = c["indexes"][key]
+    k, d = ent["k"], ent["d"]
+    ac = backend in ALT
+    tags = (200, 201, 100) if ac else (100, 101)
+    checked = 0
+    for tag in tags:
+        idx = gpu.Index.load(GOLDEN / case / ent["files"][str(tag)]["file"])
+        for m, qd in sorted(c["queries"].items()):
+            m = int(m)
+            if m % k:
+                continue
+            q = read_qry(GOLDEN / case / qd["file"], m)
+            want = oracle_mod.read_results_file(
+                GOLDEN / case / ent["results"][f"{m}.{200 if ac else 100}"]["file"])
+            if not coop_supported(backend, k, d):
+                with pytest.raises(gpu.KfmiError):
+                    gpu.search_array(idx, q, backend)
+                return
+            got = gpu.search_array(idx, q, backend)
+            assert np.array_equal(got, want), (backend, case, key, tag, m,
+                                               int(np.flatnonzero(got != want)[0]))
+            checked += 1
+        idx.close()
+    assert checked
+
+
+@pytest.fixture(scope="module")
+def random_index(kfmi_mod):
+    rng = np.random.default_rng(2026)
+    text = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), size=3_000_001).tobytes()
+    return text, {(k, d): kfmi_mod.Index.build(text, k=k, d=d) for k, d in
+                  [(2, 64), (1, 64), (2, 192), (2, 448), (2, 960), (1, 32), (2, 128), (2, 256)]}
+
+
+def _reads(text, n, m, seed):
+    rng = np.random.default_rng(seed)
+    t = np.frombuffer(text, dtype=np.uint8)
+    st = rng.integers(0, len(text) - m, size=n)
+    samp = t[st[:, None] + np.arange(m)[None, :]]
+    rnd = rng.choice(np.frombuffer(b"ACGTNacgt", dtype=np.uint8), size=(n // 4, m))
+    return np.concatenate([samp, rnd])
+
+
+@pytest.mark.parametrize("backend", PLAIN + ALT)
+@pytest.mark.parametrize("kd", [(2, 64), (1, 64), (2, 192), (2, 448), (2, 960), (1, 32), (2, 128), (2, 256)],
+                         ids=lambda kd: f"k{kd[0]}d{kd[1]}")
+def test_backend_matches_oracle_random(gpu, oracle_mod, random_index, backend, kd):
+    text, idxs = random_index
+    k, d = kd
+    idx = idxs[kd]
+    for m, n in ((100, 20000), (150, 4000), (2 * k, 4000)):
+        q = _reads(text, n, m, seed=m * 7 + k)
+        if backend in ALT:
+            i200, _ = idx.alt_counters()
+            want, _ = oracle_mod.search(i200.image(), q)
+        else:
+            want, _ = oracle_mod.search(idx.image(), q)
+        if not coop_supported(backend, k, d):
+            with pytest.raises(gpu.KfmiError):
+                gpu.search_array(idx, q, backend)
+            return
+        got = gpu.search_array(idx, q, backend)
+        assert np.array_equal(got, want), (backend, kd, m)
+
+
+def test_block_count_matches_oracle(gpu, oracle_mod, random_index):
+    text, idxs = random_index
+    idx = idxs[(2, 64)]
+    q = _reads(text, 20000, 100, seed=3)
+    _, want = oracle_mod.search(idx.image(), q)
+    gpu.set_backend("task-packed")
+    qq = gpu.Queries.from_array(q)
+    r = gpu.Results.alloc(q.shape[0])
+    gpu.transfer_to_gpu(idx, qq, r)
+    assert gpu.count_blocks(idx, qq) == want
+
+
+def test_edge_cases(gpu, oracle_mod, random_index):
+    text, idxs = random_index
+    idx = idxs[(2, 64)]
+    # empty batch
+    for b in PLAIN + ALT:
+        out = gpu.search_array(idx, np.zeros((0, 100), dtype=np.uint8), b)
+        assert out.size == 0
+    # batches that are not multiples of the wave / block size
+    for n in (1, 63, 65, 257, 1023):
+        q = _reads(text, n, 100, seed=n)[:n]
+        want, _ = oracle_mod.search(idx.image(), q)
+        for b in PLAIN:
+            assert np.array_equal(gpu.search_array(idx, q, b), want), (b, n)
+    # m % K != 0 is rejected (reference reads query[-1])
+    with pytest.raises(gpu.KfmiError):
+        gpu.search_array(idx, np.zeros((4, 5), dtype=np.uint8) + 65, "task")
+    # search before transfer
+    q = gpu.Queries.from_array(np.zeros((4, 8), dtype=np.uint8) + 65)
+    r = gpu.Results.alloc(4)
+    fresh = gpu.Index.from_image(idx.image())
+    with pytest.raises(gpu.KfmiError) as e:
+        gpu.search(fresh, q, r)
+    assert e.value.code == 34
+
+
+def test_strict_tag_like_reference(gpu, monkeypatch):
+    c = manifest()["textA"]["indexes"]["k2_d64"]["files"]
+    monkeypatch.setenv("KFMI_STRICT_TAG", "1")
+    gpu.set_backend("task")
+    with pytest.raises(gpu.KfmiError) as e:
+        gpu.Index.load(GOLDEN / "textA" / c["100"]["file"])
+    assert e.value.code == 101
+    gpu.Index.load(GOLDEN / "textA" / c["101"]["file"]).close()
+    gpu.set_backend("task-ac")
+    with pytest.raises(gpu.KfmiError) as e:
+        gpu.Index.load(GOLDEN / "textA" / c["101"]["file"])
+    assert e.value.code == 201
+
+
+def test_config1_64mbase_md5_pinned(gpu):
+    """BASELINE config #1 end to end: recipe text (md5), host builder (md5 of
+    the reference-built .fmi), 2^20 reads (md5), GPU search on every backend
+    -> md5 of the results file the reference CPU searcher wrote."""
+    from kstep_fmi import synth
+    text, rng = synth.text_64m()
+    assert synth.fasta_md5(text, b">synthetic_64M\n") == synth.MD5["ref64.fa"]
+    idx = gpu.Index.build(text, k=2, d=64)
+    assert hashlib.md5(idx.image().tobytes()).hexdigest() == synth.MD5["ref64.k2d64.fmi"]
+    q = synth.reads_64m(text, rng)
+    for b in PLAIN + ALT:
+        res = gpu.search_array(idx, q, b)
+        assert synth.results_md5(res) == synth.MD5["res64"], b
