@@ -1,0 +1,292 @@
+#!/usr/bin/env python3
+"""bench.py -- BASELINE.json metric: Mqueries/s of batched k-step FM-index
+backward search (3 Gbase synthetic reference, 10M x 100 bp reads, K=2, d=64)
+on N MI355X, one process per GPU, plus the achieved HBM fraction of the LF
+kernel and the CPU oracle timed on the host cores.
+
+  python bench.py --gpus 1 --steps 10 --warmup 3
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
+      --master-port P bench.py --gpus N
+
+A step = one searchIndexGPU() over the rank's whole batch (query packing +
+LF kernel, inputs resident in HBM).  Each rank builds its own replica of the
+index on its GPU (no collective on the data path) and searches its own 10M
+reads (weak scaling).  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "k-step_fm-index_amd"))
+
+import kstep_fmi as K  # noqa: E402
+from kstep_fmi import synth  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def log(*a):
+    print(f"[bench {time.strftime('%H:%M:%S')}]", *a, file=sys.stderr, flush=True)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--backend", default="task-packed")
+    p.add_argument("--ref-size", type=int, default=3_000_000_000)
+    p.add_argument("--queries", type=int, default=10_000_000)
+    p.add_argument("--qlen", type=int, default=100)
+    p.add_argument("--k", type=int, default=2)
+    p.add_argument("--d", type=int, default=64)
+    p.add_argument("--cpu-sample", type=int, default=2_000_000,
+                   help="queries of the CPU-oracle baseline sample (0 = skip)")
+    p.add_argument("--cpu-threads", type=int, default=0)
+    p.add_argument("--variants", default="task,coop,task-ac,coop-ac,coop-packed",
+                   help="other backends timed on rank 0 at N=1 (empty = none)")
+    p.add_argument("--variant-steps", type=int, default=3)
+    p.add_argument("--no-md5", action="store_true")
+    p.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic.json"))
+    return p.parse_args()
+
+
+class Dist:
+    def __init__(self, gpus: int):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.pg = None
+        if self.world > 1:
+            import torch.distributed as dist
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo")    # control plane only: barrier + timing max
+            self.pg = dist
+
+    def barrier(self):
+        if self.pg:
+            self.pg.barrier()
+
+    def max(self, x: float) -> float:
+        if not self.pg:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self.pg.all_reduce(t, op=self.pg.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, x: float) -> float:
+        if not self.pg:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self.pg.all_reduce(t, op=self.pg.ReduceOp.SUM)
+        return float(t.item())
+
+    def close(self):
+        if self.pg:
+            self.pg.destroy_process_group()
+
+
+def cuda_sync(dev: int):
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.synchronize(dev)
+    except Exception:
+        pass
+
+
+def make_text(n: int) -> bytes:
+    if n == 3_000_000_000:
+        return synth.text_3g(n)
+    import random
+    rng = random.Random(n)
+    return rng.randbytes(n).translate(synth.TBL)
+
+
+def time_backend(idx, q, r, backend, steps, warmup):
+    K.set_backend(backend)
+    K.transfer_to_gpu(idx, q, r)
+    for _ in range(warmup):
+        K.search(idx, q, r)
+    lf, tot = [], []
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        K.search(idx, q, r)
+        t = K.last_timing()
+        lf.append(t["lf_ms"])
+        tot.append(t["total_ms"])
+    wall = time.perf_counter() - t0
+    K.transfer_to_cpu(r)
+    return wall, float(np.mean(lf)), float(np.mean(tot))
+
+
+def main():
+    a = parse()
+    D = Dist(a.gpus)
+    K.load()
+    ndev = K.device_count()
+    if ndev < 1:
+        raise SystemExit("bench.py: no HIP device visible")
+    dev = D.local % ndev
+    K.set_device(dev)
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.set_device(dev)
+    except Exception:
+        pass
+
+    # ---- inputs: reference text, index replica, this rank's reads ----------
+    t = time.perf_counter()
+    text = make_text(a.ref_size)
+    log(f"rank {D.rank}: text {len(text)} bases in {time.perf_counter() - t:.1f}s")
+    t = time.perf_counter()
+    idx = K.Index.build(text, k=a.k, d=a.d, gpu=True)
+    build_s = time.perf_counter() - t
+    log(f"rank {D.rank}: GPU index build {build_s:.1f}s")
+    pinned = (a.ref_size == 3_000_000_000 and a.k == 2 and a.d == 64)
+    index_md5_ok = None
+    if pinned and D.rank == 0 and not a.no_md5:
+        h = hashlib.md5(idx.image().tobytes()).hexdigest()
+        index_md5_ok = h == synth.MD5["ref3g.k2d64.fmi"]
+        log(f"index md5 {h} pinned-ok={index_md5_ok}")
+    t = time.perf_counter()
+    starts = synth.read_starts(len(text), a.queries, a.qlen, seed=10 + D.rank)
+    reads = synth.gather_reads(text, starts, a.qlen)
+    del starts
+    log(f"rank {D.rank}: {reads.shape[0]} reads in {time.perf_counter() - t:.1f}s")
+
+    q = K.Queries.from_array(reads)
+    r = K.Results.alloc(reads.shape[0])
+    K.set_backend(a.backend)
+    t = time.perf_counter()
+    K.transfer_to_gpu(idx, q, r)
+    upload_s = time.perf_counter() - t
+    dev_index_bytes = idx.device_bytes()
+
+    # ---- timed region --------------------------------------------------------
+    for _ in range(a.warmup):
+        K.search(idx, q, r)
+    cuda_sync(dev)
+    D.barrier()
+    lf_ms, tot_ms, pack_ms = [], [], []
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        K.search(idx, q, r)
+        tm = K.last_timing()
+        lf_ms.append(tm["lf_ms"])
+        tot_ms.append(tm["total_ms"])
+        pack_ms.append(tm["pack_ms"])
+    cuda_sync(dev)
+    D.barrier()
+    elapsed = time.perf_counter() - t0
+    elapsed_max = D.max(elapsed)
+    total_queries = D.sum(float(reads.shape[0]))
+    ms_per_step = elapsed_max / a.steps * 1e3
+    value = total_queries * a.steps / elapsed_max / 1e6      # Mqueries/s, whole job
+
+    # ---- correctness of the timed results -----------------------------------
+    t = time.perf_counter()
+    K.transfer_to_cpu(r)
+    d2h_s = time.perf_counter() - t
+    res = r.array().copy()
+    results_md5_ok = None
+    if pinned and a.qlen == 100 and a.queries == 10_000_000 and D.rank == 0 and not a.no_md5:
+        results_md5_ok = synth.results_md5(res) == synth.MD5["res3g.q10M"]
+        log(f"results md5 pinned-ok={results_md5_ok}")
+
+    # ---- roofline: algorithmic bytes of the LF kernel ------------------------
+    blocks = K.count_blocks(idx, q)
+    b_lf = a.k * a.d // 4 + 4                               # bit planes of one block + one counter
+    bytes_alg = blocks * b_lf
+    lf_avg_ms = float(np.mean(lf_ms))
+    achieved = bytes_alg / (lf_avg_ms / 1e3) / 1e9
+    traffic = None
+    tj = Path(a.traffic_json)
+    if tj.exists():
+        try:
+            tr = json.loads(tj.read_text())
+            if tr.get("backend") == a.backend and tr.get("queries") == a.queries and tr.get("ref_size") == a.ref_size:
+                traffic = tr.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    extra = {}
+    cpu = None
+    if D.rank == 0 and D.world == 1:
+        # ---- other backends (same index, same reads) ------------------------
+        for b in [x for x in a.variants.split(",") if x and x != a.backend]:
+            try:
+                wall, lf, tot = time_backend(idx, q, r, b, a.variant_steps, 1)
+                ok = bool(np.array_equal(r.array(), res))
+                extra[b] = {"mqps": round(reads.shape[0] * a.variant_steps / wall / 1e6, 2),
+                            "lf_ms": round(lf, 3), "step_ms": round(tot, 3), "results_equal": ok,
+                            "device_index_bytes": idx.device_bytes()}
+                log(f"variant {b}: {extra[b]}")
+            except K.KfmiError as e:
+                extra[b] = {"error": str(e)}
+            idx.free_gpu()
+        # ---- CPU baseline: the oracle restatement on the host cores ---------
+        if a.cpu_sample > 0:
+            from oracle import oracle
+            thr = a.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+            ns = min(a.cpu_sample, reads.shape[0])
+            img = idx.image()
+            t = time.perf_counter()
+            cres, _ = oracle.search(img, reads[:ns], nthreads=thr)
+            cpu_s = time.perf_counter() - t
+            cpu = {"value": round(ns / cpu_s / 1e6, 4), "unit": "Mqueries/s", "cores": thr, "kind": "port",
+                   "sample": f"first {ns} of the same 10M reads, 1 pass, oracle/fmi_oracle.c "
+                             f"(restatement of fmIndexCPUBaseline.c), OMP threads={thr}, {cpu_s:.2f}s",
+                   "parity_with_gpu": bool(np.array_equal(cres, res[:2 * ns]))}
+            log(f"cpu baseline {cpu}")
+
+    if D.rank == 0:
+        line = {
+            "metric": "Mqueries/s (100 bp reads, 3 Gbase index)",
+            "value": round(value, 3),
+            "unit": "Mqueries/s",
+            "n_gpus": D.world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic: seeded uniform-ACGT reference + exact-substring reads (SURVEY App. C recipe, md5-pinned)",
+            "config": {"workload": f"{'Task' if a.backend.startswith('task') else 'Coop'}-{a.k}Step backward search, "
+                                   f"{a.ref_size / 1e9:g} Gbase index, {a.queries // 1_000_000}M x {a.qlen} bp reads per GPU",
+                       "backend": a.backend, "k": a.k, "d": a.d, "ref_size": a.ref_size,
+                       "queries_per_gpu": a.queries, "qlen": a.qlen,
+                       "parallelism": f"query-sharded dp{D.world}, index replicated per GPU, no collective"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel": "LF kernel (task/coop search), HIP-event average over the timed steps",
+                         "bytes_per_launch": bytes_alg, "distinct_blocks": blocks, "bytes_per_block": b_lf,
+                         "lf_ms": round(lf_avg_ms, 4), "pack_ms": round(float(np.mean(pack_ms)), 4),
+                         "naive_bytes_per_launch": 2 * (a.qlen // a.k) * b_lf * a.queries},
+            "cpu_baseline": cpu,
+            "parity": {"index_md5_pinned": index_md5_ok, "results_md5_pinned": results_md5_ok},
+            "setup_s": {"gpu_index_build": round(build_s, 2), "h2d": round(upload_s, 2), "d2h": round(d2h_s, 3)},
+            "device_index_bytes": dev_index_bytes,
+            "variants": extra,
+        }
+        print(json.dumps(line), flush=True)
+    D.close()
+
+
+if __name__ == "__main__":
+    main()
