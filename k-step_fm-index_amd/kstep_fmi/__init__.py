@@ -135,6 +135,13 @@ def last_timing():
     return {"total_ms": t[0].value, "pack_ms": t[1].value, "lf_ms": t[2].value}
 
 
+def _owned_view(addr: int, nbytes: int, dtype, owner) -> np.ndarray:
+    """numpy view of library-owned memory that keeps `owner` (the handle) alive."""
+    buf = (ctypes.c_uint8 * nbytes).from_address(addr)
+    buf._kfmi_owner = owner
+    return np.frombuffer(buf, dtype=dtype)
+
+
 class _Handle:
     _free = ""
 
@@ -205,7 +212,7 @@ class Index(_Handle):
         p = ctypes.c_void_p()
         n = ctypes.c_uint64()
         _check(load().kfmi_index_image(self._p, ctypes.byref(p), ctypes.byref(n)), "image")
-        return np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint8)), shape=(n.value,))
+        return _owned_view(p.value, n.value, np.uint8, self)
 
     def save(self, fn) -> None:
         _check(load().saveIndex(str(fn).encode(), self._p), f"saveIndex {fn}")
@@ -263,7 +270,9 @@ class Results(_Handle):
         L = load()
         n = int(L.kfmi_results_num(self._p))
         ptr = L.kfmi_results_host(self._p)
-        return np.ctypeslib.as_array(ptr, shape=(2 * n,)) if n else np.zeros(0, dtype=np.uint32)
+        if not n:
+            return np.zeros(0, dtype=np.uint32)
+        return _owned_view(ctypes.cast(ptr, ctypes.c_void_p).value, 8 * n, np.uint32, self)
 
     def save(self, fn) -> None:
         _check(load().saveResults(str(fn).encode(), self._p, None), f"saveResults {fn}")
