@@ -1,0 +1,95 @@
+#!/usr/bin/env python3
+"""Kernel-variant sweep on one index build (dev tool; not the bench contract).
+
+Builds the 3 Gbase (or --ref-size) index once on the GPU, then times each
+backend x tuning knob and prints one JSON line per variant to stdout:
+  python scripts/sweep.py --backends task-packed,task,coop --qpt 1,2 --steps 5
+Every variant's results are compared with the first variant's (bit-exact).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "k-step_fm-index_amd"))
+import kstep_fmi as K  # noqa: E402
+from kstep_fmi import synth  # noqa: E402
+
+
+def log(*a):
+    print(f"[sweep {time.strftime('%H:%M:%S')}]", *a, file=sys.stderr, flush=True)
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--ref-size", type=int, default=3_000_000_000)
+    p.add_argument("--queries", type=int, default=10_000_000)
+    p.add_argument("--qlen", type=int, default=100)
+    p.add_argument("--k", type=int, default=2)
+    p.add_argument("--d", type=int, default=64)
+    p.add_argument("--backends", default="task-packed,task,task-ac,coop,coop-ac,coop-packed")
+    p.add_argument("--env", default="", help="semicolon list of VAR=v1,v2 knobs swept for every backend")
+    p.add_argument("--steps", type=int, default=5)
+    a = p.parse_args()
+
+    K.load()
+    K.set_device(0)
+    t = time.perf_counter()
+    text = synth.text_3g(a.ref_size) if a.ref_size == 3_000_000_000 else \
+        np.random.default_rng(1).choice(np.frombuffer(b"ACGT", dtype=np.uint8), size=a.ref_size).tobytes()
+    log(f"text {time.perf_counter() - t:.1f}s")
+    t = time.perf_counter()
+    idx = K.Index.build(text, k=a.k, d=a.d, gpu=True)
+    log(f"build {time.perf_counter() - t:.1f}s")
+    reads = synth.gather_reads(text, synth.read_starts(len(text), a.queries, a.qlen, 10), a.qlen)
+    log("reads ready")
+    q = K.Queries.from_array(reads)
+    r = K.Results.alloc(reads.shape[0])
+    knobs = [{}]
+    for spec in [s for s in a.env.split(";") if s]:
+        var, vals = spec.split("=")
+        knobs = [dict(k, **{var: v}) for k in knobs for v in vals.split(",")]
+    ref = None
+    for b in a.backends.split(","):
+        for kn in knobs:
+            for var, v in kn.items():
+                os.environ[var] = v
+            try:
+                K.set_backend(b)
+                K.transfer_to_gpu(idx, q, r)
+                K.search(idx, q, r)
+                lf, tot = [], []
+                t0 = time.perf_counter()
+                for _ in range(a.steps):
+                    K.search(idx, q, r)
+                    tm = K.last_timing()
+                    lf.append(tm["lf_ms"])
+                    tot.append(tm["total_ms"])
+                wall = (time.perf_counter() - t0) / a.steps
+                K.transfer_to_cpu(r)
+                res = r.array().copy()
+                if ref is None:
+                    ref = res
+                out = {"backend": b, "knobs": kn, "lf_ms": round(float(np.median(lf)), 3),
+                       "lf_ms_min": round(float(np.min(lf)), 3), "step_ms": round(float(np.median(tot)), 3),
+                       "wall_ms": round(wall * 1e3, 3), "mqps": round(reads.shape[0] / wall / 1e6, 1),
+                       "equal": bool(np.array_equal(res, ref)), "dev_bytes": idx.device_bytes()}
+            except K.KfmiError as e:
+                out = {"backend": b, "knobs": kn, "error": str(e)}
+            print(json.dumps(out), flush=True)
+            log(out)
+            for var in kn:
+                os.environ.pop(var, None)
+        idx.free_gpu()
+
+
+if __name__ == "__main__":
+    main()
