@@ -207,7 +207,10 @@ struct SuffixLess {
 
 int32_t build_gpu(const char* text, uint64_t n, uint32_t k, uint32_t d, int dev, kfmi_fmi_t** out)
 {
-  if (n == 0 || n + 1 > 0xFFFFFFFEull || k < 1 || k > 4 || d == 0 || d % 32) return KFMI_E_BAD_ARGUMENT;
+  /* n + 1 >= k: every D_s (s < k) exists -- SA = s is a suffix of T for s < n and
+   * the '$' row 0 for s == n -- and (SA - 1 - s) wraps at most once. */
+  if (n == 0 || n + 1 < k || n + 1 > 0xFFFFFFFEull || k < 1 || k > 4 || d == 0 || d % 32)
+    return KFMI_E_BAD_ARGUMENT;
   BHIP(hipSetDevice(dev));
   hipStream_t st;
   BHIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
@@ -291,6 +294,7 @@ int32_t build_gpu(const char* text, uint64_t n, uint32_t k, uint32_t d, int dev,
 
   /* 5. '$' rows and blocks */
   uint32_t drow[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+  if (n < 4) drow[n] = 0;   /* SA[0] = n: the '$' row */
   {
     DevBuf dd;
     BHIP(dd.alloc(16));

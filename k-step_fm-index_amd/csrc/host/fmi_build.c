@@ -169,7 +169,9 @@ int32_t kfmi_index_from_sa(const uint8_t *codes, const uint32_t *sa, uint64_t n,
   uint32_t *cprime;
   kfmi_fmi_t *f;
   int32_t err;
-  if (k < 1 || k > KFMI_MAX_STEPS || d == 0 || d % 32 || rows > 0xFFFFFFFFull) return KFMI_E_BAD_ARGUMENT;
+  /* n + 1 >= k: every D_s exists and (SA - 1 - s) wraps at most once */
+  if (k < 1 || k > KFMI_MAX_STEPS || d == 0 || d % 32 || rows > 0xFFFFFFFFull || rows < k)
+    return KFMI_E_BAD_ARGUMENT;
   nentries = (uint32_t) ((rows + d - 1) / d);
   for (s = 0; s < k; s++) { dpos[s] = 0; dbase[s] = 0; }
   err = kfmi_index_alloc(100, k, (uint32_t) rows, nentries, d, NULL, NULL, &f);
@@ -260,7 +262,7 @@ int32_t kfmi_build_index_cpu(const char *text, uint64_t n, uint32_t k, uint32_t 
   uint32_t *sa;
   uint64_t i;
   int32_t err;
-  if (n == 0 || n + 1 > 0xFFFFFFFEull) return KFMI_E_BAD_ARGUMENT;
+  if (n == 0 || n + 1 < k || n + 1 > 0xFFFFFFFEull) return KFMI_E_BAD_ARGUMENT;
   if (k < 1 || k > KFMI_MAX_STEPS || d == 0 || d % 32) return KFMI_E_BAD_ARGUMENT;
   codes = (uint8_t *) malloc(n);
   sym = (uint8_t *) malloc(n + 1);

@@ -33,6 +33,11 @@ def test_gpu_builder_equals_host_builder(gpu, k, d):
     rng = np.random.default_rng(k * 1000 + d)
     for n in (1, 5, 63, 64, 65, 1000, 250_000):
         text = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), size=n).tobytes()
+        if n + 1 < k:      # a D_s would not exist: both builders refuse
+            for g in (True, False):
+                with pytest.raises(gpu.KfmiError):
+                    gpu.Index.build(text, k=k, d=d, gpu=g)
+            continue
         a = gpu.Index.build(text, k=k, d=d, gpu=True).image().tobytes()
         b = gpu.Index.build(text, k=k, d=d, gpu=False).image().tobytes()
         assert a == b, (k, d, n)
