@@ -1,0 +1,172 @@
+/*
+ * gather_probe -- random-line gather ceiling of the MI355X memory system for
+ * the LF access pattern (dev tool, not part of the engine).
+ *
+ *   gather_probe [table_GB=3] [lines_M=512]
+ *
+ * For line sizes of 32/64/128 B it reads `lines` uniformly random, line-aligned
+ * lines of a `table_GB` table and reports lines/s and GB/s for:
+ *   indep  : every lane issues independent line reads (4 in flight per lane),
+ *            one lane per line (dwordx4 loads)
+ *   coop   : TPR lanes read one line cooperatively, 16 B each
+ *   chain  : dependent chains (next address = f(loaded data)), 1 or 2 chains
+ *            per lane -- the LF kernel's shape
+ * Addresses come from a per-lane xorshift generator (no index array traffic).
+ */
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <stdint.h>
+
+#define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
+
+__device__ __forceinline__ uint64_t xs(uint64_t& s)
+{
+  s ^= s << 13; s ^= s >> 7; s ^= s << 17;
+  return s;
+}
+
+/* uniform line index in [0, n) without a 64-bit modulo (n < 2^32) */
+__device__ __forceinline__ uint64_t pick(uint64_t x, uint64_t n) { return ((x >> 32) * n) >> 32; }
+
+template <int LB>   // line bytes
+__global__ __launch_bounds__(256) void k_indep(const uint4* __restrict__ t, uint64_t nlines, uint64_t per_thread,
+                                               uint32_t* __restrict__ sink)
+{
+  constexpr int V = LB / 16;
+  uint64_t s = 0x9E3779B97F4A7C15ull ^ ((uint64_t) blockIdx.x * 256 + threadIdx.x) * 0xBF58476D1CE4E5B9ull;
+  uint32_t acc = 0;
+  for (uint64_t i = 0; i < per_thread; i += 4) {
+    uint4 v[4][V];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint64_t l = pick(xs(s), nlines);
+#pragma unroll
+      for (int k = 0; k < V; ++k) v[j][k] = t[l * V + k];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int k = 0; k < V; ++k) acc ^= v[j][k].x ^ v[j][k].w;
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
+template <int LB>
+__global__ __launch_bounds__(256) void k_coop(const uint4* __restrict__ t, uint64_t nlines, uint64_t per_group,
+                                              uint32_t* __restrict__ sink)
+{
+  constexpr int TPR = LB / 16;
+  const int lane = threadIdx.x & 63, k = lane % TPR;
+  /* lanes of one group share the generator state: same address */
+  uint64_t s = 0x9E3779B97F4A7C15ull ^ (((uint64_t) blockIdx.x * 256 + threadIdx.x) / TPR) * 0xBF58476D1CE4E5B9ull;
+  uint32_t acc = 0;
+  for (uint64_t i = 0; i < per_group; i += 4) {
+    uint4 v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = t[(pick(xs(s), nlines)) * TPR + k];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc ^= v[j].x ^ v[j].w;
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
+template <int LB, int CH>
+__global__ __launch_bounds__(256) void k_chain(const uint4* __restrict__ t, uint64_t nlines, uint32_t steps,
+                                               uint32_t* __restrict__ sink)
+{
+  constexpr int V = LB / 16;
+  uint64_t s[CH];
+  uint64_t l[CH];
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    s[c] = 0x9E3779B97F4A7C15ull ^ (((uint64_t) blockIdx.x * 256 + threadIdx.x) * CH + c) * 0xBF58476D1CE4E5B9ull;
+    l[c] = pick(xs(s[c]), nlines);
+  }
+  uint32_t acc = 0;
+  for (uint32_t i = 0; i < steps; ++i) {
+    uint4 v[CH][V];
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+#pragma unroll
+      for (int k = 0; k < V; ++k) v[c][k] = t[l[c] * V + k];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      uint32_t x = 0;
+#pragma unroll
+      for (int k = 0; k < V; ++k) x ^= v[c][k].x ^ v[c][k].y;
+      acc ^= x;
+      l[c] = pick(xs(s[c]) ^ ((uint64_t) x << 32), nlines);     /* next address depends on the loaded data */
+    }
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
+static float timed(hipEvent_t a, hipEvent_t b)
+{
+  float ms;
+  CHECK(hipEventSynchronize(b));
+  CHECK(hipEventElapsedTime(&ms, a, b));
+  return ms;
+}
+
+int main(int argc, char** argv)
+{
+  const double gb = argc > 1 ? atof(argv[1]) : 3.0;
+  const uint64_t lines_target = (uint64_t) ((argc > 2 ? atof(argv[2]) : 512.0) * 1e6);
+  const uint64_t bytes = (uint64_t) (gb * 1e9) & ~(uint64_t) 127;
+  uint4* t;
+  uint32_t* sink;
+  CHECK(hipMalloc(&t, bytes));
+  CHECK(hipMalloc(&sink, 4));
+  CHECK(hipMemset(t, 0x5a, bytes));
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  const uint32_t threads = 256 * 256 * 8;   /* 8 blocks of 256 per CU */
+  const dim3 grid(threads / 256), blk(256);
+  printf("{\"probe\": \"gather\", \"table_bytes\": %llu}\n", (unsigned long long) bytes);
+
+  auto run = [&](const char* name, int lb, auto launch, double nlines) {
+    launch();
+    CHECK(hipDeviceSynchronize());
+    CHECK(hipEventRecord(e0));
+    launch();
+    CHECK(hipEventRecord(e1));
+    const float ms = timed(e0, e1);
+    printf("{\"kind\": \"%s\", \"line_B\": %d, \"ms\": %.3f, \"Glines_s\": %.2f, \"GB_s\": %.1f}\n", name, lb,
+           ms, nlines / ms / 1e6, nlines * lb / ms / 1e6);
+    fflush(stdout);
+  };
+  {
+    const uint64_t pt = (lines_target / threads + 3) & ~3ull;
+    run("indep", 32, [&] { hipLaunchKernelGGL((k_indep<32>), grid, blk, 0, 0, t, bytes / 32, pt, sink); }, (double) pt * threads);
+    run("indep", 64, [&] { hipLaunchKernelGGL((k_indep<64>), grid, blk, 0, 0, t, bytes / 64, pt, sink); }, (double) pt * threads);
+    run("indep", 128, [&] { hipLaunchKernelGGL((k_indep<128>), grid, blk, 0, 0, t, bytes / 128, pt, sink); }, (double) pt * threads);
+  }
+  {
+    const uint64_t pg32 = (lines_target / (threads / 2) + 3) & ~3ull;
+    const uint64_t pg64 = (lines_target / (threads / 4) + 3) & ~3ull;
+    const uint64_t pg128 = (lines_target / (threads / 8) + 3) & ~3ull;
+    run("coop", 32, [&] { hipLaunchKernelGGL((k_coop<32>), grid, blk, 0, 0, t, bytes / 32, pg32, sink); }, (double) pg32 * (threads / 2));
+    run("coop", 64, [&] { hipLaunchKernelGGL((k_coop<64>), grid, blk, 0, 0, t, bytes / 64, pg64, sink); }, (double) pg64 * (threads / 4));
+    run("coop", 128, [&] { hipLaunchKernelGGL((k_coop<128>), grid, blk, 0, 0, t, bytes / 128, pg128, sink); }, (double) pg128 * (threads / 8));
+  }
+  {
+    const uint32_t st = (uint32_t) (lines_target / threads);
+    run("chain1", 32, [&] { hipLaunchKernelGGL((k_chain<32, 1>), grid, blk, 0, 0, t, bytes / 32, st, sink); }, (double) st * threads);
+    run("chain1", 64, [&] { hipLaunchKernelGGL((k_chain<64, 1>), grid, blk, 0, 0, t, bytes / 64, st, sink); }, (double) st * threads);
+    run("chain1", 128, [&] { hipLaunchKernelGGL((k_chain<128, 1>), grid, blk, 0, 0, t, bytes / 128, st, sink); }, (double) st * threads);
+    const uint32_t st2 = st / 2;
+    run("chain2", 64, [&] { hipLaunchKernelGGL((k_chain<64, 2>), grid, blk, 0, 0, t, bytes / 64, st2, sink); }, (double) st2 * threads * 2);
+  }
+  /* smaller tables: L2 / MALL resident */
+  for (double sub : {0.004, 0.2}) {
+    const uint64_t sb = (uint64_t) (sub * 1e9) & ~(uint64_t) 127;
+    const uint64_t pt = (lines_target / threads + 3) & ~3ull;
+    printf("{\"table_bytes\": %llu}\n", (unsigned long long) sb);
+    run("indep", 64, [&] { hipLaunchKernelGGL((k_indep<64>), grid, blk, 0, 0, t, sb / 64, pt, sink); }, (double) pt * threads);
+  }
+  CHECK(hipFree(t));
+  return 0;
+}
