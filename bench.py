@@ -53,7 +53,7 @@ def parse():
     p.add_argument("--cpu-sample", type=int, default=2_000_000,
                    help="queries of the CPU-oracle baseline sample (0 = skip)")
     p.add_argument("--cpu-threads", type=int, default=0)
-    p.add_argument("--variants", default="task,coop,task-ac,coop-ac,coop-packed",
+    p.add_argument("--variants", default="task,coop,task-ac,coop-ac,task-packed,coop-packed,task-mid,coop-mid",
                    help="other backends timed on rank 0 at N=1 (empty = none)")
     p.add_argument("--variant-steps", type=int, default=3)
     p.add_argument("--no-md5", action="store_true")

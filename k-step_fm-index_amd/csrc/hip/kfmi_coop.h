@@ -34,7 +34,8 @@ struct CoopCfg {
   static constexpr int WPB0 = 65536 / WAVE_LDS;
   static constexpr int WPB = WPB0 < 1 ? 1 : (WPB0 > 4 ? 4 : WPB0);   // waves per block
   static constexpr bool OK = (G::BMW % 4 == 0) && (G::EW % 4 == 0) && (G::BOFF % 4 == 0) &&
-                             (G::LAY != LAY_AC || G::HALF >= 4) && TPR <= 64;
+                             (G::LAY != LAY_AC || G::HALF >= 4) && (G::LAY != LAY_MID || G::NC >= 4) &&
+                             TPR <= 64;
 };
 
 // byte address of chunk k of request (b, c)
@@ -44,6 +45,11 @@ __device__ __forceinline__ const uint8_t* coop_chunk_addr(const IdxArgs& ix, uin
   using C = CoopCfg<G>;
   const uint8_t* base = reinterpret_cast<const uint8_t*>(ix.ent);
   const uint64_t eb = (uint64_t) b * (G::EW * 4);
+  if constexpr (G::LAY == LAY_MID) {
+    const uint64_t lb = (uint64_t) (b >> 1) * (G::EW * 4);
+    if (k < C::BC) return base + lb + ((b & 1u) * G::BMW + 4 * k) * 4;
+    return base + lb + (G::MIDCNT + (c & ~3u)) * 4;
+  }
   if (k < C::BC) return base + eb + (G::BOFF + 4 * k) * 4;
   if constexpr (G::LAY == LAY_INTER) {
     return base + eb + (G::BMW + (c & ~3u)) * 4;
@@ -63,6 +69,7 @@ __device__ __forceinline__ uint32_t coop_lf(const IdxArgs& ix, const uint8_t* sl
   const int o = (int) (X - b * (uint32_t) G::D);
   bool e = false;
   if constexpr (G::LAY == LAY_AC) e = ((b & 1u) != 0) == (c < (uint32_t) G::HALF);
+  if constexpr (G::LAY == LAY_MID) e = (b & 1u) == 0;
   uint32_t pop = 0;
 #pragma unroll
   for (int k = 0; k < C::BC; ++k) {
@@ -73,7 +80,7 @@ __device__ __forceinline__ uint32_t coop_lf(const IdxArgs& ix, const uint8_t* sl
     for (int h = 0; h < 4 / G::PW; ++h) {
       const int w = k * (4 / G::PW) + h;
       uint32_t m = row_mask(o - 32 * w);
-      if constexpr (G::LAY == LAY_AC) m = e ? ~m : m;
+      if constexpr (G::TWO_SIDED) m = e ? ~m : m;
       pop += __popc(m & select_rows<G::K>(&pl[h * G::PW], sx));
     }
   }
@@ -82,10 +89,7 @@ __device__ __forceinline__ uint32_t coop_lf(const IdxArgs& ix, const uint8_t* sl
     cnt = sbase + reinterpret_cast<const uint16_t*>(slot + 16 * C::BC)[c & 7u];
   else
     cnt = reinterpret_cast<const uint32_t*>(slot + 16 * C::BC)[c & 3u];
-  const int corr = dollar_fix<G::K, G::LAY == LAY_AC>(ix.dl, b, c, X, e);
-  const uint32_t bc = pop - (uint32_t) corr;
-  if constexpr (G::LAY == LAY_AC) return e ? cnt - bc : cnt + bc;
-  return cnt + bc;
+  return finish<G>(ix, cnt, pop, b, c, X, e);
 }
 
 template <class G>

@@ -6,17 +6,22 @@
  *   b = X / d, o = X % d
  *   X' = cnt_b[c] + popc( first-o-rows-mask & AND_{s<K} sel(plane_{s,0}, c_s.bit0) & sel(plane_{s,1}, c_s.bit1) )
  *        - #{s : D_s/d == b, c == dollarBase_s, X > D_s}
- * AltCounters (fmIndexCPUBaseline-AltCounters.c:218-303): when
- *   e = (b odd & c < NC/2) | (b even & c >= NC/2)
- * the counter comes from entry b+1 and the popcount runs over the inverted
- * mask and is subtracted; the $ rule flips to X <= D_s.
+ * Two-sided form (AltCounters, fmIndexCPUBaseline-AltCounters.c:218-303): when
+ * the counter sampled at the END of block b is used ("backward", e = 1),
+ *   X' = cnt_{b+1}[c] - (popc(rows [o, d) of code c) - #{s : D_s/d == b, c == dollarBase_s, X <= D_s}).
  *
  * Device layouts (one per backend family; see DESIGN.md "Data layout in HBM"):
  *   LAY_INTER  : tag-101 entries as in the file, [planes(w,s,t) | cnt[NC]] u32
- *   LAY_AC     : tag-201 entries as in the file, [cnt_half[NC/2] | planes(w,s,t)]
+ *   LAY_AC     : tag-201 entries as in the file, [cnt_half[NC/2] | planes(w,s,t)];
+ *                e = (b odd & c < NC/2) | (b even & c >= NC/2)
  *   LAY_PACKED : one power-of-two line per d-block, [planes(w,s,t) | u16 delta[NC]],
- *                cnt_b[c] = sb[b >> SB_SHIFT][c] + delta_b[c] (sb: small, cache-resident).
- *                K=2, d=64 -> exactly one 64-byte line per LF.
+ *                cnt_b[c] = sb[b >> SB_SHIFT][c] + delta_b[c] (sb: small, cache-resident)
+ *   LAY_MID    : one power-of-two line per PAIR of d-blocks (2d rows),
+ *                [planes of block 2p | planes of block 2p+1 | cnt_{2p+1}[NC]]:
+ *                every counter sits at the pair's midpoint, so an even block is
+ *                searched backward (e = 1) and an odd block forward from the SAME
+ *                line.  K=2, d=64: one 128-byte line per LF and nothing else --
+ *                the AltCounters idea packed into one 128-B HBM request.
  */
 #ifndef KFMI_DEVICE_H_
 #define KFMI_DEVICE_H_
@@ -26,7 +31,7 @@
 
 namespace kfmi {
 
-enum Layout : int { LAY_INTER = 0, LAY_AC = 1, LAY_PACKED = 2 };
+enum Layout : int { LAY_INTER = 0, LAY_AC = 1, LAY_PACKED = 2, LAY_MID = 3 };
 
 __host__ __device__ constexpr int pow2ceil(int x) { int p = 1; while (p < x) p <<= 1; return p; }
 
@@ -39,15 +44,18 @@ struct Geo {
   static constexpr int NC = 1 << (2 * K);        // counters (4^K)
   static constexpr int HALF = NC / 2;
   static constexpr int PW = 2 * K;               // planes per 32-row word
-  static constexpr int BMW = PW * NB;            // bitmap words per entry
-  // u32 words per entry
+  static constexpr int BMW = PW * NB;            // bitmap words per block
+  // u32 words per entry (per line for LAY_MID)
   static constexpr int EW = LAY == LAY_INTER ? BMW + NC
                           : LAY == LAY_AC    ? HALF + BMW
-                          : pow2ceil(BMW + NC / 2);
+                          : LAY == LAY_PACKED ? pow2ceil(BMW + NC / 2)
+                          : pow2ceil(2 * BMW + NC);
   static constexpr int BOFF = LAY == LAY_AC ? HALF : 0;   // first bitmap word
   static constexpr int DELTA16 = 2 * BMW;                 // first u16 delta (packed)
+  static constexpr int MIDCNT = 2 * BMW;                  // first mid counter (mid)
   static constexpr int SPW = 32 / (2 * K);                // K-steps per packed query word
   static constexpr bool SMALL = BMW <= 16;                // whole bitmap fits in registers
+  static constexpr bool TWO_SIDED = LAY == LAY_AC || LAY == LAY_MID;
 };
 
 // Superblock shift of the packed layout: the largest S with (2^S - 1) * d <= 65535.
@@ -65,7 +73,7 @@ struct DollarArgs {
 };
 
 struct IdxArgs {
-  const uint32_t* __restrict__ ent;   // entries (layout per backend)
+  const uint32_t* __restrict__ ent;   // entries / lines (layout per backend)
   const uint32_t* __restrict__ sb;    // packed layout: superblock counters [nsb][NC]
   uint32_t bwtsize;
   uint32_t pad_;
@@ -106,23 +114,81 @@ __device__ __forceinline__ uint32_t select_rows(const uint32_t* pl, const uint32
 }
 
 // Number of $ rows to discount (fmIndexCPUBaseline.c:252-256; AC :254-263).
-template <int K, bool AC>
+template <int K, bool TWO>
 __device__ __forceinline__ int dollar_fix(const DollarArgs& dl, uint32_t b, uint32_t c, uint32_t X, bool e)
 {
   int corr = 0;
 #pragma unroll
   for (int s = 0; s < K; ++s) {
     bool hit = (dl.dblk[s] == b) && (dl.dbase[s] == c);
-    bool cond = (AC && e) ? (X <= dl.dpos[s]) : (X > dl.dpos[s]);
+    bool cond = (TWO && e) ? (X <= dl.dpos[s]) : (X > dl.dpos[s]);
     corr += (hit && cond) ? 1 : 0;
   }
   return corr;
 }
 
+// Direction and planes/counter addresses of block b for code c.
+template <class G>
+struct Where {
+  const uint32_t* planes;
+  const uint32_t* cnt;      // counter word (unused for packed: see delta/sb)
+  bool e;                   // backward (two-sided layouts)
+};
+
+template <class G>
+__device__ __forceinline__ Where<G> locate(const IdxArgs& ix, uint32_t b, uint32_t c)
+{
+  Where<G> w;
+  if constexpr (G::LAY == LAY_INTER) {
+    const uint32_t* ent = ix.ent + (uint64_t) b * G::EW;
+    w.planes = ent;
+    w.cnt = ent + G::BMW + c;
+    w.e = false;
+  } else if constexpr (G::LAY == LAY_AC) {
+    const uint32_t* ent = ix.ent + (uint64_t) b * G::EW;
+    w.e = ((b & 1u) != 0) == (c < (uint32_t) G::HALF);
+    w.planes = ent + G::BOFF;
+    w.cnt = ix.ent + (uint64_t) (b + (w.e ? 1u : 0u)) * G::EW + (c & (G::HALF - 1));
+  } else if constexpr (G::LAY == LAY_PACKED) {
+    const uint32_t* ent = ix.ent + (uint64_t) b * G::EW;
+    w.planes = ent;
+    w.cnt = nullptr;
+    w.e = false;
+  } else {
+    const uint32_t* line = ix.ent + (uint64_t) (b >> 1) * G::EW;
+    w.e = (b & 1u) == 0;                          // even block: backward from the midpoint
+    w.planes = line + (b & 1u) * G::BMW;
+    w.cnt = line + G::MIDCNT + c;
+  }
+  return w;
+}
+
+template <class G>
+__device__ __forceinline__ uint32_t load_counter(const IdxArgs& ix, const Where<G>& w, uint32_t b, uint32_t c)
+{
+  if constexpr (G::LAY == LAY_PACKED) {
+    constexpr int S = sb_shift_for(G::D);
+    const uint32_t* ent = ix.ent + (uint64_t) b * G::EW;
+    return ix.sb[(uint64_t) (b >> S) * G::NC + c] + reinterpret_cast<const uint16_t*>(ent)[G::DELTA16 + c];
+  } else {
+    return *w.cnt;
+  }
+}
+
+template <class G>
+__device__ __forceinline__ uint32_t finish(const IdxArgs& ix, uint32_t cnt, uint32_t pop, uint32_t b, uint32_t c,
+                                          uint32_t X, bool e)
+{
+  const int corr = dollar_fix<G::K, G::TWO_SIDED>(ix.dl, b, c, X, e);
+  const uint32_t bc = pop - (uint32_t) corr;
+  if constexpr (G::TWO_SIDED) return e ? cnt - bc : cnt + bc;
+  return cnt + bc;
+}
+
 // ---------------------------------------------------------------------------
 // Register-resident block fetch for small blocks (BMW <= 16 words): all bit
-// planes of block b plus the one counter (or delta+superblock) that code c
-// needs.  Loads are 16-byte (dwordx4) when the plane group allows it.
+// planes of block b plus the one counter that code c needs.  Loads are
+// 16-byte (dwordx4) when the plane group allows it.
 // ---------------------------------------------------------------------------
 template <class G>
 struct Blk {
@@ -156,24 +222,11 @@ __device__ __forceinline__ void load_planes(const uint32_t* __restrict__ p, uint
 template <class G>
 __device__ __forceinline__ void fetch_block(const IdxArgs& ix, uint32_t b, uint32_t c, Blk<G>& k)
 {
+  const Where<G> w = locate<G>(ix, b, c);
   k.b = b;
-  const uint32_t* ent = ix.ent + (uint64_t) b * G::EW;
-  if constexpr (G::LAY == LAY_INTER) {
-    k.e = false;
-    load_planes<G>(ent, k.bm);
-    k.cnt = ent[G::BMW + c];
-  } else if constexpr (G::LAY == LAY_AC) {
-    k.e = ((b & 1u) != 0) == (c < (uint32_t) G::HALF);
-    load_planes<G>(ent + G::BOFF, k.bm);
-    k.cnt = ix.ent[(uint64_t) (b + (k.e ? 1u : 0u)) * G::EW + (c & (G::HALF - 1))];
-  } else {
-    k.e = false;
-    load_planes<G>(ent, k.bm);
-    uint32_t delta = reinterpret_cast<const uint16_t*>(ent)[G::DELTA16 + c];
-    constexpr int S = sb_shift_for(G::D);
-    uint32_t base = ix.sb[(uint64_t) (b >> S) * G::NC + c];
-    k.cnt = base + delta;
-  }
+  k.e = w.e;
+  load_planes<G>(w.planes, k.bm);
+  k.cnt = load_counter<G>(ix, w, b, c);
 }
 
 template <class G>
@@ -185,20 +238,15 @@ __device__ __forceinline__ uint32_t lf_from_block(const IdxArgs& ix, const Blk<G
 #pragma unroll
   for (int w = 0; w < G::NB; ++w) {
     uint32_t m = row_mask(o - 32 * w);
-    if constexpr (G::LAY == LAY_AC) m = k.e ? ~m : m;
+    if constexpr (G::TWO_SIDED) m = k.e ? ~m : m;
     pop += __popc(m & select_rows<G::K>(&k.bm[w * G::PW], sx));
   }
-  const int corr = dollar_fix<G::K, G::LAY == LAY_AC>(ix.dl, k.b, c, X, k.e);
-  const uint32_t bc = pop - (uint32_t) corr;
-  if constexpr (G::LAY == LAY_AC) return k.e ? k.cnt - bc : k.cnt + bc;
-  return k.cnt + bc;
+  return finish<G>(ix, k.cnt, pop, k.b, c, X, k.e);
 }
 
 // ---------------------------------------------------------------------------
 // Streaming LF for large blocks (d >= 192 with K=2): planes read word group by
-// word group; only the words that the row mask reaches contribute for
-// forward counting, but all are read (as the reference does) so the result is
-// identical for every layout.
+// word group; all words are read (as the reference does).
 // ---------------------------------------------------------------------------
 template <class G>
 __device__ __forceinline__ uint32_t lf_stream(const IdxArgs& ix, uint32_t X, uint32_t c,
@@ -206,19 +254,9 @@ __device__ __forceinline__ uint32_t lf_stream(const IdxArgs& ix, uint32_t X, uin
 {
   const uint32_t b = X / (uint32_t) G::D;
   const int o = (int) (X - b * (uint32_t) G::D);
-  const uint32_t* ent = ix.ent + (uint64_t) b * G::EW;
-  bool e = false;
-  uint32_t cnt;
-  if constexpr (G::LAY == LAY_INTER) {
-    cnt = ent[G::BMW + c];
-  } else if constexpr (G::LAY == LAY_AC) {
-    e = ((b & 1u) != 0) == (c < (uint32_t) G::HALF);
-    cnt = ix.ent[(uint64_t) (b + (e ? 1u : 0u)) * G::EW + (c & (G::HALF - 1))];
-  } else {
-    constexpr int S = sb_shift_for(G::D);
-    cnt = ix.sb[(uint64_t) (b >> S) * G::NC + c] + reinterpret_cast<const uint16_t*>(ent)[G::DELTA16 + c];
-  }
-  const uint32_t* pl = ent + G::BOFF;
+  const Where<G> wh = locate<G>(ix, b, c);
+  const uint32_t cnt = load_counter<G>(ix, wh, b, c);
+  const uint32_t* pl = wh.planes;
   uint32_t pop = 0;
 #pragma unroll 2
   for (int w = 0; w < G::NB; ++w) {
@@ -234,13 +272,10 @@ __device__ __forceinline__ uint32_t lf_stream(const IdxArgs& ix, uint32_t X, uin
       for (int p = 0; p < G::PW; ++p) v[p] = pl[G::PW * w + p];
     }
     uint32_t m = row_mask(o - 32 * w);
-    if constexpr (G::LAY == LAY_AC) m = e ? ~m : m;
+    if constexpr (G::TWO_SIDED) m = wh.e ? ~m : m;
     pop += __popc(m & select_rows<G::K>(v, sx));
   }
-  const int corr = dollar_fix<G::K, G::LAY == LAY_AC>(ix.dl, b, c, X, e);
-  const uint32_t bc = pop - (uint32_t) corr;
-  if constexpr (G::LAY == LAY_AC) return e ? cnt - bc : cnt + bc;
-  return cnt + bc;
+  return finish<G>(ix, cnt, pop, b, c, X, wh.e);
 }
 
 }  // namespace kfmi

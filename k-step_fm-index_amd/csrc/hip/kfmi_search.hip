@@ -27,7 +27,7 @@ using namespace kfmi;
 /* ------------------------------------------------------------------------ */
 
 static const char* kBackendNames[KFMI_BK_COUNT] = {
-    "task", "coop", "task-ac", "coop-ac", "task-packed", "coop-packed"};
+    "task", "coop", "task-ac", "coop-ac", "task-packed", "coop-packed", "task-mid", "coop-mid"};
 
 static thread_local int t_backend = -1;
 static thread_local int t_device = -1;
@@ -334,6 +334,35 @@ __global__ __launch_bounds__(256) void build_packed_kernel(const uint32_t* __res
     for (int c = 0; c < GI::NC; ++c) sb[(b >> S) * GI::NC + c] = src[GI::BMW + c];
 }
 
+/* MID layout construction from tag-101 entries: line p holds the planes of
+ * blocks 2p and 2p+1 and the counters sampled at its midpoint (= cnt_{2p+1}).
+ * The last odd-count line and one padding line take host-computed counters
+ * (rows past n+1 read as code 0, see mid_ext_counters). */
+template <int K, int NB>
+__global__ __launch_bounds__(256) void build_mid_kernel(const uint32_t* __restrict__ inter, uint32_t nentries,
+                                                        uint32_t nlines, uint32_t* __restrict__ lines,
+                                                        const uint32_t* __restrict__ ext_last,
+                                                        const uint32_t* __restrict__ ext_pad)
+{
+  using GI = Geo<K, NB, LAY_INTER>;
+  using GM = Geo<K, NB, LAY_MID>;
+  const uint64_t p = (uint64_t) blockIdx.x * 256 + threadIdx.x;
+  if (p >= nlines) return;
+  uint32_t* dst = lines + p * GM::EW;
+  for (int h = 0; h < 2; ++h) {
+    const uint64_t b = 2 * p + h;
+    for (int i = 0; i < GI::BMW; ++i) dst[h * GI::BMW + i] = b < nentries ? inter[b * GI::EW + i] : 0u;
+  }
+  for (int c = 0; c < GI::NC; ++c) {
+    uint32_t v;
+    if (2 * p + 1 < nentries) v = inter[(2 * p + 1) * GI::EW + GI::BMW + c];
+    else if (2 * p < nentries) v = ext_last[c];
+    else v = ext_pad[c];
+    dst[GM::MIDCNT + c] = v;
+  }
+  for (int i = GM::MIDCNT + GI::NC; i < GM::EW; ++i) dst[i] = 0;
+}
+
 /* ------------------------------------------------------------------------ */
 /* dispatch tables                                                          */
 /* ------------------------------------------------------------------------ */
@@ -417,6 +446,8 @@ static hipError_t dispatch(Op op, uint32_t K, uint32_t nb, int lay, const Search
   KFMI_FOR_NB(KFMI_CASE, 2, LAY_AC)
   KFMI_FOR_NB(KFMI_CASE, 1, LAY_PACKED)
   KFMI_FOR_NB(KFMI_CASE, 2, LAY_PACKED)
+  KFMI_FOR_NB(KFMI_CASE, 1, LAY_MID)
+  KFMI_FOR_NB(KFMI_CASE, 2, LAY_MID)
 #undef KFMI_CASE
   return hipErrorInvalidValue;
 }
@@ -437,18 +468,37 @@ static hipError_t dispatch_build_packed(uint32_t K, uint32_t nb, const uint32_t*
   return hipErrorInvalidValue;
 }
 
+static hipError_t dispatch_build_mid(uint32_t K, uint32_t nb, const uint32_t* inter, uint32_t nentries,
+                                     uint32_t nlines, uint32_t* lines, const uint32_t* ext_last,
+                                     const uint32_t* ext_pad, hipStream_t st)
+{
+  const uint32_t blocks = (nlines + 255) / 256;
+#define KFMI_BM(KK, NBV, LAYV)                                                                         \
+  if (K == KK && nb == NBV) {                                                                          \
+    hipLaunchKernelGGL((build_mid_kernel<KK, NBV>), dim3(blocks), dim3(256), 0, st, inter, nentries, nlines, \
+                       lines, ext_last, ext_pad);                                                      \
+    return hipGetLastError();                                                                          \
+  }
+  KFMI_FOR_NB(KFMI_BM, 1, 0)
+  KFMI_FOR_NB(KFMI_BM, 2, 0)
+#undef KFMI_BM
+  return hipErrorInvalidValue;
+}
+
 static int layout_of(int backend)
 {
   switch (backend) {
     case KFMI_BK_TASK: case KFMI_BK_COOP: return LAY_INTER;
     case KFMI_BK_TASK_AC: case KFMI_BK_COOP_AC: return LAY_AC;
+    case KFMI_BK_TASK_MID: case KFMI_BK_COOP_MID: return LAY_MID;
     default: return LAY_PACKED;
   }
 }
 
 static bool is_coop(int backend)
 {
-  return backend == KFMI_BK_COOP || backend == KFMI_BK_COOP_AC || backend == KFMI_BK_COOP_PACKED;
+  return backend == KFMI_BK_COOP || backend == KFMI_BK_COOP_AC || backend == KFMI_BK_COOP_PACKED ||
+         backend == KFMI_BK_COOP_MID;
 }
 
 /* ------------------------------------------------------------------------ */
@@ -491,7 +541,7 @@ static int32_t host_entries_for(const kfmi_fmi_t* f, int lay, kfmi_fmi_t** owned
 {
   *owned = nullptr;
   *use = f;
-  if (lay == LAY_INTER || lay == LAY_PACKED) {
+  if (lay == LAY_INTER || lay == LAY_PACKED || lay == LAY_MID) {
     if (f->tag == 101) return KFMI_SUCCESS;
     if (f->tag == 100) {
       int32_t e = kfmi_transform_interleave((void*) f, (void**) owned);
@@ -600,6 +650,40 @@ static int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx)
             hipSuccess ||
         hipStreamSynchronize(ctx->st) != hipSuccess)
       return fail(KFMI_E_KERNEL);
+  } else if (lay == LAY_MID) {
+    /* MID: pairs of blocks per line, built on the device from tag-101 entries;
+     * counters of the last line (odd block count) and of one padding line are
+     * "rows past n+1 read as A" extensions of the end counters. */
+    const uint32_t E = src->nentries;
+    const uint32_t nreal = (E + 1) / 2;
+    const uint32_t nl = nreal + 1;
+    const uint32_t lw = (uint32_t) pow2ceil((int) (2 * 2 * f->nbitmaps * f->steps + nc));
+    std::vector<uint32_t> endc(nc), ext(2 * nc);
+    end_counters(src, endc.data());
+    const uint64_t n1 = f->bwtsize;                                   /* n + 1 */
+    const uint64_t mid_last = (uint64_t) E * f->chunk;               /* midpoint of line nreal-1 when E is odd */
+    const uint64_t mid_pad = (uint64_t) nreal * 2 * f->chunk + f->chunk;
+    for (uint32_t c = 0; c < nc; ++c) {
+      ext[c] = endc[c] + (c == 0 ? (uint32_t) (mid_last - n1) : 0u);
+      ext[nc + c] = endc[c] + (c == 0 ? (uint32_t) (mid_pad - n1) : 0u);
+    }
+    uint32_t *tmp = nullptr, *d_ext = nullptr;
+    di->ent_bytes = 4ull * lw * nl;
+    if (hipMalloc((void**) &tmp, body + 16) != hipSuccess) return fail(KFMI_E_DEVICE_ALLOC);
+    if (hipMalloc((void**) &di->ent, di->ent_bytes) != hipSuccess ||
+        hipMalloc((void**) &d_ext, 8ull * nc) != hipSuccess) {
+      (void) hipFree(tmp);
+      if (d_ext) (void) hipFree(d_ext);
+      return fail(KFMI_E_DEVICE_ALLOC);
+    }
+    bool ok = hipMemcpyAsync(tmp, src->h_index, body, hipMemcpyHostToDevice, ctx->st) == hipSuccess &&
+              hipMemcpyAsync(d_ext, ext.data(), 8ull * nc, hipMemcpyHostToDevice, ctx->st) == hipSuccess &&
+              dispatch_build_mid(f->steps, f->nbitmaps, tmp, E, nl, di->ent, d_ext, d_ext + nc, ctx->st) ==
+                  hipSuccess &&
+              hipStreamSynchronize(ctx->st) == hipSuccess;
+    (void) hipFree(tmp);
+    (void) hipFree(d_ext);
+    if (!ok) return fail(KFMI_E_KERNEL);
   } else {
     /* packed: build on the device from tag-101 entries (+ the padding entry) */
     const uint32_t ne = src->nentries + 1;

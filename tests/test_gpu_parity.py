@@ -14,7 +14,7 @@ from util import GOLDEN, manifest, read_qry
 
 pytestmark = pytest.mark.gpu
 
-PLAIN = ("task", "coop", "task-packed", "coop-packed")
+PLAIN = ("task", "coop", "task-packed", "coop-packed", "task-mid", "coop-mid")
 ALT = ("task-ac", "coop-ac")
 
 
@@ -178,3 +178,27 @@ def test_config1_64mbase_md5_pinned(gpu):
     for b in PLAIN + ALT:
         res = gpu.search_array(idx, q, b)
         assert synth.results_md5(res) == synth.MD5["res64"], b
+
+
+@pytest.mark.parametrize("n", [63, 127, 191, 255, 1023, 4095, 100, 129])
+def test_b5_boundary_against_bruteforce(gpu, n):
+    """(n+1) % d == 0 (and % 2d == 0 for the MID layout's padding line): the
+    reference reads past the index end there; every plain-counter
+    backend must return the true suffix-rank interval instead."""
+    rng = np.random.default_rng(n)
+    text = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), size=n).tobytes()
+    bf = util.BruteForce(text.decode())
+    t = np.frombuffer(text, dtype=np.uint8)
+    for k, d in ((2, 64), (1, 32), (2, 32)):
+        idx = gpu.Index.build(text, k=k, d=d)
+        for m in (2, 4, 12):
+            if m > n:
+                continue
+            st = rng.integers(0, n - m + 1, size=64)
+            q = np.concatenate([t[st[:, None] + np.arange(m)[None, :]],
+                                rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), size=(32, m))])
+            want = np.array([x for i in range(q.shape[0]) for x in bf.interval(q[i].tobytes())], dtype=np.uint32)
+            for b in PLAIN:
+                if not coop_supported(b, k, d):
+                    continue
+                assert np.array_equal(gpu.search_array(idx, q, b), want), (n, k, d, m, b)
