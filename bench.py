@@ -44,7 +44,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--backend", default="task-packed")
+    p.add_argument("--backend", default="task-mid")
     p.add_argument("--ref-size", type=int, default=3_000_000_000)
     p.add_argument("--queries", type=int, default=10_000_000)
     p.add_argument("--qlen", type=int, default=100)

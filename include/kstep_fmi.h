@@ -115,10 +115,13 @@ char    *errorCommon(int32_t e);
  *   "coop-ac"     Coop-2Step-AltCounters                                    (tag 201 semantics)
  *   "task-packed" task-per-query on the 64-byte-line packed layout          (tag 101 semantics)
  *   "coop-packed" wave64 cooperative gather on the packed layout            (tag 101 semantics)
- * The default comes from KFMI_BACKEND, else "task-packed".  An index of any tag
- * is accepted and re-laid-out on upload; an AC backend applied to a tag-100/101
- * file first runs the tfmiAC transform, so its results are those of the
- * AltCounters searcher on that file. */
+ *   "task-mid"    task-per-query on the MID128 layout: one 128-byte line per LF (tag 101 semantics)
+ *   "coop-mid"    wave64 cooperative gather on the MID128 layout              (tag 101 semantics)
+ * The default comes from KFMI_BACKEND, else "task-mid".  transferCPUtoGPU
+ * re-lays-out the loaded index for the backend: plain-counter backends take
+ * tag 100 or 101 (an AC file returns 101, as the reference loader would);
+ * AC backends take any tag -- a tag-100/101 file first goes through the tfmiAC
+ * transform, so the results are those of the AltCounters searcher on it. */
 int32_t     kfmi_set_backend(const char *name);
 const char *kfmi_get_backend(void);
 /* The HIP device used by the calling thread (reference: compile-time DEVICE).

@@ -52,7 +52,7 @@ extern "C" kfmi_backend_t kfmi_backend(void)
 {
   if (t_backend < 0) {
     int b = backend_from_name(getenv("KFMI_BACKEND"));
-    t_backend = b >= 0 ? b : KFMI_BK_TASK_PACKED;
+    t_backend = b >= 0 ? b : KFMI_BK_TASK_MID;
   }
   return (kfmi_backend_t) t_backend;
 }
