@@ -38,6 +38,8 @@ def main():
     p.add_argument("--backends", default="task-packed,task,task-ac,coop,coop-ac,coop-packed")
     p.add_argument("--env", default="", help="semicolon list of VAR=v1,v2 knobs swept for every backend")
     p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--sort-suffix", type=int, default=0,
+                   help="experiment: order reads by their last N bases (backward-search order)")
     a = p.parse_args()
 
     K.load()
@@ -50,6 +52,11 @@ def main():
     idx = K.Index.build(text, k=a.k, d=a.d, gpu=True)
     log(f"build {time.perf_counter() - t:.1f}s")
     reads = synth.gather_reads(text, synth.read_starts(len(text), a.queries, a.qlen, 10), a.qlen)
+    if a.sort_suffix:
+        cols = [reads[:, a.qlen - 1 - j] for j in range(a.sort_suffix)]
+        order = np.lexsort(cols[::-1])            # primary key: the last base
+        reads = np.ascontiguousarray(reads[order])
+        log(f"reads ordered by their last {a.sort_suffix} bases")
     log("reads ready")
     q = K.Queries.from_array(reads)
     r = K.Results.alloc(reads.shape[0])
