@@ -76,9 +76,33 @@ struct IdxArgs {
   const uint32_t* __restrict__ ent;   // entries / lines (layout per backend)
   const uint32_t* __restrict__ sb;    // packed layout: superblock counters [nsb][NC]
   uint32_t bwtsize;
-  uint32_t pad_;
+  uint32_t nt_from;                   // K-steps >= nt_from load index lines non-temporally
   DollarArgs dl;
 };
+
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+
+// 16/8/4-byte loads, optionally non-temporal (global_load ... nt): deep-step
+// lines are touched once, so they should not evict the hot early-step lines.
+template <bool NT>
+__device__ __forceinline__ v4u ld4(const uint32_t* p)
+{
+  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+  else return *reinterpret_cast<const v4u*>(p);
+}
+template <bool NT>
+__device__ __forceinline__ v2u ld2(const uint32_t* p)
+{
+  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const v2u*>(p));
+  else return *reinterpret_cast<const v2u*>(p);
+}
+template <bool NT>
+__device__ __forceinline__ uint32_t ld1(const uint32_t* p)
+{
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
 
 // base2index restated on a byte (genFMindex.c:71-84)
 __device__ __forceinline__ uint32_t code_of(uint32_t x)
@@ -163,7 +187,7 @@ __device__ __forceinline__ Where<G> locate(const IdxArgs& ix, uint32_t b, uint32
   return w;
 }
 
-template <class G>
+template <class G, bool NT = false>
 __device__ __forceinline__ uint32_t load_counter(const IdxArgs& ix, const Where<G>& w, uint32_t b, uint32_t c)
 {
   if constexpr (G::LAY == LAY_PACKED) {
@@ -171,7 +195,7 @@ __device__ __forceinline__ uint32_t load_counter(const IdxArgs& ix, const Where<
     const uint32_t* ent = ix.ent + (uint64_t) b * G::EW;
     return ix.sb[(uint64_t) (b >> S) * G::NC + c] + reinterpret_cast<const uint16_t*>(ent)[G::DELTA16 + c];
   } else {
-    return *w.cnt;
+    return ld1<NT>(w.cnt);
   }
 }
 
@@ -198,35 +222,35 @@ struct Blk {
   bool e;
 };
 
-template <class G>
+template <class G, bool NT = false>
 __device__ __forceinline__ void load_planes(const uint32_t* __restrict__ p, uint32_t (&bm)[G::BMW])
 {
   if constexpr (G::BMW % 4 == 0 && ((G::BOFF + 0) % 4 == 0) && (G::EW % 4 == 0)) {
 #pragma unroll
     for (int i = 0; i < G::BMW / 4; ++i) {
-      uint4 v = *reinterpret_cast<const uint4*>(p + 4 * i);
+      const v4u v = ld4<NT>(p + 4 * i);
       bm[4 * i + 0] = v.x; bm[4 * i + 1] = v.y; bm[4 * i + 2] = v.z; bm[4 * i + 3] = v.w;
     }
   } else if constexpr (G::BMW % 2 == 0 && (G::BOFF % 2 == 0) && (G::EW % 2 == 0)) {
 #pragma unroll
     for (int i = 0; i < G::BMW / 2; ++i) {
-      uint2 v = *reinterpret_cast<const uint2*>(p + 2 * i);
+      const v2u v = ld2<NT>(p + 2 * i);
       bm[2 * i + 0] = v.x; bm[2 * i + 1] = v.y;
     }
   } else {
 #pragma unroll
-    for (int i = 0; i < G::BMW; ++i) bm[i] = p[i];
+    for (int i = 0; i < G::BMW; ++i) bm[i] = ld1<NT>(p + i);
   }
 }
 
-template <class G>
+template <class G, bool NT = false>
 __device__ __forceinline__ void fetch_block(const IdxArgs& ix, uint32_t b, uint32_t c, Blk<G>& k)
 {
   const Where<G> w = locate<G>(ix, b, c);
   k.b = b;
   k.e = w.e;
-  load_planes<G>(w.planes, k.bm);
-  k.cnt = load_counter<G>(ix, w, b, c);
+  load_planes<G, NT>(w.planes, k.bm);
+  k.cnt = load_counter<G, NT>(ix, w, b, c);
 }
 
 template <class G>

@@ -245,13 +245,24 @@ __global__ __launch_bounds__(256) void task_kernel(IdxArgs ix, const uint32_t* _
       for (int i = 0; i < QPT; ++i) c[i] = (word[i] >> (2 * G::K * j)) & (uint32_t) (G::NC - 1);
       if constexpr (G::SMALL) {
         Blk<G> kl[QPT], kr[QPT];
+        if (w * SPW + j >= ix.nt_from) {   /* wave-uniform: deep steps stream non-temporally */
 #pragma unroll
-        for (int i = 0; i < QPT; ++i) fetch_block<G>(ix, L[i] / (uint32_t) G::D, c[i], kl[i]);
+          for (int i = 0; i < QPT; ++i) fetch_block<G, true>(ix, L[i] / (uint32_t) G::D, c[i], kl[i]);
 #pragma unroll
-        for (int i = 0; i < QPT; ++i) {
-          const uint32_t br = R[i] / (uint32_t) G::D;
-          if (br != kl[i].b) fetch_block<G>(ix, br, c[i], kr[i]);
-          else kr[i] = kl[i];
+          for (int i = 0; i < QPT; ++i) {
+            const uint32_t br = R[i] / (uint32_t) G::D;
+            if (br != kl[i].b) fetch_block<G, true>(ix, br, c[i], kr[i]);
+            else kr[i] = kl[i];
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < QPT; ++i) fetch_block<G>(ix, L[i] / (uint32_t) G::D, c[i], kl[i]);
+#pragma unroll
+          for (int i = 0; i < QPT; ++i) {
+            const uint32_t br = R[i] / (uint32_t) G::D;
+            if (br != kl[i].b) fetch_block<G>(ix, br, c[i], kr[i]);
+            else kr[i] = kl[i];
+          }
         }
 #pragma unroll
         for (int i = 0; i < QPT; ++i) {
@@ -732,7 +743,8 @@ static IdxArgs idx_args(const kfmi_dev_index* di)
   ix.ent = di->ent;
   ix.sb = di->sb;
   ix.bwtsize = di->bwtsize;
-  ix.pad_ = 0;
+  const char* e = getenv("KFMI_NT_FROM");   /* K-step from which index loads are non-temporal */
+  ix.nt_from = e ? (uint32_t) atoi(e) : 0xFFFFFFFFu;
   ix.dl = di->dl;
   return ix;
 }
