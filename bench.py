@@ -213,13 +213,15 @@ def main():
     bytes_alg = blocks * b_lf
     lf_avg_ms = float(np.mean(lf_ms))
     achieved = bytes_alg / (lf_avg_ms / 1e3) / 1e9
-    traffic = None
+    # HBM bytes per launch from the committed PMC profile of the same config
+    # (scripts/traffic_from_pmc.py: TCC_EA0_RDREQ x line bytes, gfx950-corrected)
+    traffic, traffic_src = None, None
     tj = Path(a.traffic_json)
     if tj.exists():
         try:
             tr = json.loads(tj.read_text())
             if tr.get("backend") == a.backend and tr.get("queries") == a.queries and tr.get("ref_size") == a.ref_size:
-                traffic = tr.get("hbm_bytes_per_launch")
+                traffic, traffic_src = tr.get("hbm_bytes_per_launch"), tr.get("source")
         except Exception:
             traffic = None
 
@@ -277,7 +279,10 @@ def main():
                          "kernel": "LF kernel (task/coop search), HIP-event average over the timed steps",
                          "bytes_per_launch": bytes_alg, "distinct_blocks": blocks, "bytes_per_block": b_lf,
                          "lf_ms": round(lf_avg_ms, 4), "pack_ms": round(float(np.mean(pack_ms)), 4),
-                         "naive_bytes_per_launch": 2 * (a.qlen // a.k) * b_lf * a.queries},
+                         "naive_bytes_per_launch": 2 * (a.qlen // a.k) * b_lf * a.queries,
+                         "traffic_source": traffic_src,
+                         "traffic_GBs": round(traffic / (lf_avg_ms / 1e3) / 1e9, 1) if traffic else None,
+                         "traffic_frac": round(traffic / (lf_avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if traffic else None},
             "cpu_baseline": cpu,
             "parity": {"index_md5_pinned": index_md5_ok, "results_md5_pinned": results_md5_ok},
             "setup_s": {"gpu_index_build": round(build_s, 2), "h2d": round(upload_s, 2), "d2h": round(d2h_s, 3)},
