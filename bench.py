@@ -48,6 +48,7 @@ def parse():
     p.add_argument("--ref-size", type=int, default=3_000_000_000)
     p.add_argument("--queries", type=int, default=10_000_000)
     p.add_argument("--qlen", type=int, default=100)
+    p.add_argument("--e2e-steps", type=int, default=3, help="streamed host-to-host passes (0: skip)")
     p.add_argument("--k", type=int, default=2)
     p.add_argument("--d", type=int, default=64)
     p.add_argument("--cpu-sample", type=int, default=2_000_000,
@@ -240,6 +241,32 @@ def main():
             except K.KfmiError as e:
                 extra[b] = {"error": str(e)}
             idx.free_gpu()
+        # ---- end to end from host memory: streamed H2D + search + D2H ------
+        if a.e2e_steps > 0:
+            try:
+                K.set_backend(a.backend)
+                K.transfer_to_gpu(idx, None, None)
+                e2e = {}
+                pin = K.pinned_empty(reads.shape, np.uint8)
+                pin[:] = reads
+                pout = K.pinned_empty((2 * reads.shape[0],), np.uint32)
+                for kind, src, dst in (("pinned", pin, pout), ("pageable", reads, None)):
+                    out = K.search_stream(idx, src, out=dst)          # warm-up (buffer allocation)
+                    t = time.perf_counter()
+                    for _ in range(a.e2e_steps):
+                        out = K.search_stream(idx, src, out=dst)
+                    w = (time.perf_counter() - t) / a.e2e_steps
+                    e2e[kind] = {"mqps": round(reads.shape[0] / w / 1e6, 2), "ms": round(w * 1e3, 3),
+                                 "results_equal": bool(np.array_equal(out, res))}
+                e2e["chunk_queries"] = int(os.environ.get("KFMI_STREAM_CHUNK", 1 << 21))
+                e2e["what"] = "kfmi_search_stream: ASCII reads in host memory -> results in host memory, " \
+                              "chunked H2D / pack+LF / D2H overlapped on 3 HIP streams"
+                extra["end_to_end"] = e2e
+                log(f"end to end {e2e}")
+                del pin, pout
+                K.load().kfmi_stream_release()
+            except K.KfmiError as e:
+                extra["end_to_end"] = {"error": str(e)}
         # ---- CPU baseline: the oracle restatement on the host cores ---------
         if a.cpu_sample > 0:
             from oracle import oracle

@@ -170,6 +170,23 @@ int32_t kfmi_build_index_gpu(const char *text, uint64_t n, uint32_t k, uint32_t 
  * steps of distinct d-blocks touched (1 if L/d == R/d else 2), SURVEY 8(d). */
 int32_t kfmi_count_blocks(void *index, void *queries, uint64_t *blocks);
 
+/* Streamed search from host memory: `num` queries of `size`
+ * ASCII bytes at `ascii`, results [L0,R0,L1,R1,...] into `results` (2*num
+ * u32).  The index must already be on the device (transferCPUtoGPU(index,
+ * NULL, NULL)).  Chunks of `chunk` queries (0: KFMI_STREAM_CHUNK, else 2^21)
+ * rotate over 3 HIP streams so that query H2D, packing + LF and result D2H of
+ * successive chunks overlap.  Pinned buffers (kfmi_host_alloc) are DMA'd
+ * directly; pageable ones are staged through pinned buffers by
+ * KFMI_COPY_THREADS host threads (default 8).  Blocking; kfmi_last_timing's
+ * total is the wall time of the whole call.  Results equal kfmi_search's. */
+int32_t kfmi_search_stream(void *index, const char *ascii, uint64_t num, uint32_t size,
+                           uint32_t *results, uint64_t chunk);
+/* Pinned (page-locked) host memory for query/result buffers. */
+int32_t kfmi_host_alloc(uint64_t bytes, void **p);
+int32_t kfmi_host_free(void *p);
+/* Frees the staging and device buffers kfmi_search_stream keeps per device. */
+int32_t kfmi_stream_release(void);
+
 /* Bytes of the device-resident index for the current backend. */
 uint64_t kfmi_device_index_bytes(void *index);
 

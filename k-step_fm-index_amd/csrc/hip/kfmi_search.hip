@@ -13,7 +13,9 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <chrono>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "../kfmi_internal.h"
@@ -379,7 +381,7 @@ __global__ __launch_bounds__(256) void build_mid_kernel(const uint32_t* __restri
 /* ------------------------------------------------------------------------ */
 
 struct SearchLaunch {
-  const DevCtx* ctx;
+  hipStream_t st;
   IdxArgs ix;
   const uint32_t* qp;
   uint64_t num;
@@ -399,11 +401,11 @@ static hipError_t launch_task(const SearchLaunch& a)
 {
   if (task_qpt() == 2) {
     const uint64_t blocks = (a.num + 511) / 512;
-    hipLaunchKernelGGL((task_kernel<G, 2>), dim3((uint32_t) blocks), dim3(256), 0, a.ctx->st, a.ix, a.qp, a.num,
+    hipLaunchKernelGGL((task_kernel<G, 2>), dim3((uint32_t) blocks), dim3(256), 0, a.st, a.ix, a.qp, a.num,
                        a.steps, a.nwords, a.res);
   } else {
     const uint64_t blocks = (a.num + 255) / 256;
-    hipLaunchKernelGGL((task_kernel<G, 1>), dim3((uint32_t) blocks), dim3(256), 0, a.ctx->st, a.ix, a.qp, a.num,
+    hipLaunchKernelGGL((task_kernel<G, 1>), dim3((uint32_t) blocks), dim3(256), 0, a.st, a.ix, a.qp, a.num,
                        a.steps, a.nwords, a.res);
   }
   return hipGetLastError();
@@ -412,14 +414,14 @@ static hipError_t launch_task(const SearchLaunch& a)
 template <class G>
 static hipError_t launch_coop(const SearchLaunch& a)
 {
-  return coop_launch<G>(a.ctx->st, a.ix, a.qp, a.num, a.steps, a.nwords, a.res);
+  return coop_launch<G>(a.st, a.ix, a.qp, a.num, a.steps, a.nwords, a.res);
 }
 
 template <class G>
 static hipError_t launch_count(const SearchLaunch& a, unsigned long long* d_total)
 {
   const uint64_t blocks = (a.num + 255) / 256;
-  hipLaunchKernelGGL((count_blocks_kernel<G>), dim3((uint32_t) blocks), dim3(256), 0, a.ctx->st, a.ix, a.qp, a.num,
+  hipLaunchKernelGGL((count_blocks_kernel<G>), dim3((uint32_t) blocks), dim3(256), 0, a.st, a.ix, a.qp, a.num,
                      a.steps, a.nwords, d_total);
   return hipGetLastError();
 }
@@ -461,6 +463,28 @@ static hipError_t dispatch(Op op, uint32_t K, uint32_t nb, int lay, const Search
   KFMI_FOR_NB(KFMI_CASE, 2, LAY_MID)
 #undef KFMI_CASE
   return hipErrorInvalidValue;
+}
+
+/* Whether the backend's kernel exists for this geometry (the cooperative
+ * kernel needs 16-byte-aligned chunks, CoopCfg::OK). */
+static bool geometry_supported(int backend, uint32_t K, uint32_t nb, int lay)
+{
+  if (!nb_supported(nb) || (K != 1 && K != 2)) return false;
+  if (backend != KFMI_BK_COOP && backend != KFMI_BK_COOP_AC && backend != KFMI_BK_COOP_PACKED &&
+      backend != KFMI_BK_COOP_MID)
+    return true;
+#define KFMI_OKC(KK, NBV, LAYV) \
+  if (K == KK && nb == NBV && lay == LAYV) return CoopCfg<Geo<KK, NBV, LAYV>>::OK;
+  KFMI_FOR_NB(KFMI_OKC, 1, LAY_INTER)
+  KFMI_FOR_NB(KFMI_OKC, 2, LAY_INTER)
+  KFMI_FOR_NB(KFMI_OKC, 1, LAY_AC)
+  KFMI_FOR_NB(KFMI_OKC, 2, LAY_AC)
+  KFMI_FOR_NB(KFMI_OKC, 1, LAY_PACKED)
+  KFMI_FOR_NB(KFMI_OKC, 2, LAY_PACKED)
+  KFMI_FOR_NB(KFMI_OKC, 1, LAY_MID)
+  KFMI_FOR_NB(KFMI_OKC, 2, LAY_MID)
+#undef KFMI_OKC
+  return false;
 }
 
 static hipError_t dispatch_build_packed(uint32_t K, uint32_t nb, const uint32_t* inter, uint32_t nentries,
@@ -621,6 +645,7 @@ static int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx)
   if (f->steps < 1 || f->steps > 2) return KFMI_E_BAD_ARGUMENT;   /* GPU kernels: K in {1,2} */
   if (!nb_supported(f->nbitmaps)) return KFMI_E_BAD_ARGUMENT;
   const int lay = layout_of(backend);
+  if (!geometry_supported(backend, f->steps, f->nbitmaps, lay)) return KFMI_E_BAD_ARGUMENT;
   kfmi_fmi_t* owned = nullptr;
   const kfmi_fmi_t* src = nullptr;
   int32_t err = host_entries_for(f, lay, &owned, &src);
@@ -854,7 +879,7 @@ extern "C" int32_t kfmi_search(void* index, void* queries, void* results)
   if (err) return err;
 
   SearchLaunch a;
-  a.ctx = ctx;
+  a.st = ctx->st;
   a.ix = idx_args(di);
   a.qp = dq->packed;
   a.num = dq->num;
@@ -904,7 +929,7 @@ extern "C" int32_t kfmi_count_blocks(void* index, void* queries, uint64_t* block
   unsigned long long* d_total = nullptr;
   HIP_OK(hipMalloc((void**) &d_total, sizeof(unsigned long long)));
   SearchLaunch a;
-  a.ctx = ctx;
+  a.st = ctx->st;
   a.ix = idx_args(di);
   a.qp = dq->packed;
   a.num = dq->num;
@@ -972,4 +997,235 @@ extern "C" uint64_t kfmi_device_index_bytes(void* index)
   kfmi_fmi_t* f = (kfmi_fmi_t*) index;
   if (!f || !f->dev) return 0;
   return f->dev->ent_bytes + f->dev->sb_bytes;
+}
+
+/* ------------------------------------------------------------------------ */
+/* streamed search from host memory: query H2D, packing, LF  */
+/* and result D2H of successive chunks overlap on NSLOT HIP streams.  Host  */
+/* buffers that are pinned (kfmi_host_alloc / hipHostRegister) are DMA'd    */
+/* directly; pageable ones go through pinned staging filled by a few host   */
+/* threads while the GPU works on the previous chunks.                      */
+/* ------------------------------------------------------------------------ */
+
+namespace {
+
+constexpr int NSLOT = 3;
+
+struct StreamSlot {
+  hipStream_t st = nullptr;
+  hipEvent_t done = nullptr;
+  kfmi_dev_queries dq;         /* device ascii + packed of one chunk */
+  uint32_t* d_res = nullptr;
+  uint8_t* h_in = nullptr;     /* pinned staging */
+  uint32_t* h_out = nullptr;
+  uint64_t cap_q = 0, cap_in = 0, cap_words = 0;
+  uint64_t q0 = 0, n = 0;
+  bool busy = false;
+};
+
+struct StreamPool {
+  bool init = false;
+  StreamSlot slot[NSLOT];
+};
+StreamPool g_pool[64];
+
+void pool_free(int dev)
+{
+  StreamPool& p = g_pool[dev];
+  if (!p.init) return;
+  (void) hipSetDevice(dev);
+  for (StreamSlot& s : p.slot) {
+    if (s.st) (void) hipStreamSynchronize(s.st);
+    if (s.dq.ascii) (void) hipFree(s.dq.ascii);
+    if (s.dq.packed) (void) hipFree(s.dq.packed);
+    if (s.d_res) (void) hipFree(s.d_res);
+    if (s.h_in) (void) hipHostFree(s.h_in);
+    if (s.h_out) (void) hipHostFree(s.h_out);
+    if (s.done) (void) hipEventDestroy(s.done);
+    if (s.st) (void) hipStreamDestroy(s.st);
+    s = StreamSlot();
+  }
+  p.init = false;
+}
+
+/* Grows slot buffers to hold `cq` queries of `size` bytes packed in `words` words. */
+int32_t slot_reserve(StreamSlot& s, uint64_t cq, uint32_t size, uint32_t words, bool stage_in, bool stage_out)
+{
+  if (!s.st) {
+    if (hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess)
+      return KFMI_E_NO_DEVICE;
+  }
+  const uint64_t in = cq * size + 16;
+  if (in > s.cap_in) {
+    if (s.dq.ascii) (void) hipFree(s.dq.ascii);
+    if (s.h_in) { (void) hipHostFree(s.h_in); s.h_in = nullptr; }
+    s.dq.ascii = nullptr;
+    s.cap_in = 0;
+    if (hipMalloc((void**) &s.dq.ascii, in) != hipSuccess) return KFMI_E_DEVICE_ALLOC;
+    s.cap_in = in;
+  }
+  if (stage_in && !s.h_in && hipHostMalloc((void**) &s.h_in, s.cap_in, hipHostMallocDefault) != hipSuccess)
+    return KFMI_E_ALLOCATING_MFASTA;
+  if (cq > s.cap_q || (uint64_t) words * cq > s.cap_words) {
+    if (s.dq.packed) (void) hipFree(s.dq.packed);
+    if (s.d_res) (void) hipFree(s.d_res);
+    if (s.h_out) { (void) hipHostFree(s.h_out); s.h_out = nullptr; }
+    s.dq.packed = nullptr;
+    s.d_res = nullptr;
+    s.cap_q = s.cap_words = 0;
+    if (hipMalloc((void**) &s.dq.packed, 4ull * words * cq) != hipSuccess ||
+        hipMalloc((void**) &s.d_res, 8ull * cq) != hipSuccess)
+      return KFMI_E_DEVICE_ALLOC;
+    s.cap_q = cq;
+    s.cap_words = (uint64_t) words * cq;
+  }
+  if (stage_out && !s.h_out && hipHostMalloc((void**) &s.h_out, 8ull * s.cap_q, hipHostMallocDefault) != hipSuccess)
+    return KFMI_E_ALLOCATING_RESULTS;
+  return KFMI_SUCCESS;
+}
+
+bool host_pinned(const void* p)
+{
+  hipPointerAttribute_t at;
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void) hipGetLastError();
+    return false;
+  }
+  return at.type == hipMemoryTypeHost;
+}
+
+/* memcpy split over a few host threads (pageable <-> pinned staging) */
+void par_copy(void* dst, const void* src, uint64_t bytes)
+{
+  static const int nt = [] {
+    const char* e = getenv("KFMI_COPY_THREADS");
+    int v = e ? atoi(e) : 8;
+    return v < 1 ? 1 : (v > 64 ? 64 : v);
+  }();
+  if (nt == 1 || bytes < (8u << 20)) {
+    memcpy(dst, src, bytes);
+    return;
+  }
+  std::vector<std::thread> th;
+  const uint64_t part = ((bytes + nt - 1) / nt + 4095) & ~4095ull;
+  for (int t = 0; t < nt; ++t) {
+    const uint64_t b = part * t;
+    if (b >= bytes) break;
+    const uint64_t len = bytes - b < part ? bytes - b : part;
+    th.emplace_back([=] { memcpy((uint8_t*) dst + b, (const uint8_t*) src + b, len); });
+  }
+  for (auto& x : th) x.join();
+}
+
+}  // namespace
+
+extern "C" int32_t kfmi_host_alloc(uint64_t bytes, void** p)
+{
+  if (!p) return KFMI_E_BAD_ARGUMENT;
+  *p = nullptr;
+  if (hipSetDevice(kfmi_current_device()) != hipSuccess) return KFMI_E_NO_DEVICE;
+  if (hipHostMalloc(p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return KFMI_E_ALLOCATING_MFASTA;
+  return KFMI_SUCCESS;
+}
+
+extern "C" int32_t kfmi_host_free(void* p)
+{
+  if (p && hipHostFree(p) != hipSuccess) return KFMI_E_BAD_ARGUMENT;
+  return KFMI_SUCCESS;
+}
+
+extern "C" int32_t kfmi_stream_release(void)
+{
+  const int dev = kfmi_current_device();
+  if (dev < 0 || dev >= 64) return KFMI_E_NO_DEVICE;
+  std::lock_guard<std::mutex> lk(g_ctx_mu);
+  pool_free(dev);
+  return KFMI_SUCCESS;
+}
+
+extern "C" int32_t kfmi_search_stream(void* index, const char* ascii, uint64_t num, uint32_t size,
+                                      uint32_t* results, uint64_t chunk)
+{
+  kfmi_fmi_t* f = (kfmi_fmi_t*) index;
+  if (!f || (!ascii && num) || (!results && num)) return KFMI_E_BAD_ARGUMENT;
+  if (!f->dev) return KFMI_E_NOT_ON_DEVICE;
+  kfmi_dev_index* di = f->dev;
+  const uint32_t K = di->K;
+  if (size == 0 || size % K || 64ull * size > 160ull * 1024) return KFMI_E_BAD_ARGUMENT;
+  DevCtx* ctx = nullptr;
+  int32_t err = ctx_for(di->device, &ctx);
+  if (err) return err;
+  if (num == 0) return KFMI_SUCCESS;
+  if (chunk == 0) {
+    const char* e = getenv("KFMI_STREAM_CHUNK");
+    chunk = e ? strtoull(e, nullptr, 10) : (1ull << 21);
+  }
+  if (chunk == 0) chunk = 1ull << 21;
+  if (chunk > num) chunk = num;
+  const uint32_t steps = size / K, spw = 32 / (2 * K), nwords = (steps + spw - 1) / spw;
+  const bool pin_in = host_pinned(ascii), pin_out = host_pinned(results);
+
+  std::lock_guard<std::mutex> lk(g_ctx_mu);   /* one streamed search per device at a time */
+  StreamPool& pool = g_pool[di->device];
+  pool.init = true;
+  for (StreamSlot& s : pool.slot) {
+    err = slot_reserve(s, chunk, size, nwords, !pin_in, !pin_out);
+    if (err) return err;
+    s.busy = false;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  const Op op = is_coop(di->backend) ? Op::Coop : Op::Task;
+  const IdxArgs ix = idx_args(di);
+  int32_t status = KFMI_SUCCESS;
+  auto retire = [&](StreamSlot& s) {
+    if (!s.busy) return;
+    if (hipEventSynchronize(s.done) != hipSuccess) status = KFMI_E_KERNEL;
+    else if (!pin_out) par_copy(results + 2 * s.q0, s.h_out, 8ull * s.n);
+    s.busy = false;
+  };
+  const uint64_t nchunks = (num + chunk - 1) / chunk;
+  for (uint64_t i = 0; i < nchunks && status == KFMI_SUCCESS; ++i) {
+    StreamSlot& s = pool.slot[i % NSLOT];
+    retire(s);
+    if (status) break;
+    s.q0 = i * chunk;
+    s.n = num - s.q0 < chunk ? num - s.q0 : chunk;
+    const char* src = ascii + s.q0 * size;
+    const uint64_t bytes = s.n * size;
+    const void* hsrc = src;
+    if (!pin_in) {
+      par_copy(s.h_in, src, bytes);
+      hsrc = s.h_in;
+    }
+    s.dq.device = di->device;
+    s.dq.num = s.n;
+    s.dq.size = size;
+    s.dq.K = K;
+    s.dq.steps = steps;
+    s.dq.nwords = nwords;
+    SearchLaunch a;
+    a.st = s.st;
+    a.ix = ix;
+    a.qp = s.dq.packed;
+    a.num = s.n;
+    a.steps = steps;
+    a.nwords = nwords;
+    a.res = s.d_res;
+    void* hdst = pin_out ? (void*) (results + 2 * s.q0) : (void*) s.h_out;
+    if (hipMemcpyAsync(s.dq.ascii, hsrc, bytes, hipMemcpyHostToDevice, s.st) != hipSuccess ||
+        launch_pack(&s.dq, s.st) != hipSuccess || dispatch(op, K, di->nb, di->layout, a) != hipSuccess ||
+        hipMemcpyAsync(hdst, s.d_res, 8ull * s.n, hipMemcpyDeviceToHost, s.st) != hipSuccess ||
+        hipEventRecord(s.done, s.st) != hipSuccess) {
+      status = KFMI_E_KERNEL;
+      break;
+    }
+    s.busy = true;
+  }
+  for (StreamSlot& s : pool.slot) retire(s);
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  t_ms[0] = ms;
+  t_ms[1] = 0;
+  t_ms[2] = 0;
+  return status;
 }

@@ -93,6 +93,10 @@ def load() -> ctypes.CDLL:
         "kfmi_build_index_gpu": (i32, [vp, u64, u32, u32, i32, pvp]),
         "kfmi_count_blocks": (i32, [vp, vp, ctypes.POINTER(ctypes.c_uint64)]),
         "kfmi_device_index_bytes": (u64, [vp]),
+        "kfmi_search_stream": (i32, [vp, vp, u64, u32, vp, u64]),
+        "kfmi_host_alloc": (i32, [u64, pvp]),
+        "kfmi_host_free": (i32, [vp]),
+        "kfmi_stream_release": (i32, []),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -298,6 +302,41 @@ def count_blocks(index: Index, queries: Queries) -> int:
     n = ctypes.c_uint64()
     _check(load().kfmi_count_blocks(index.ptr, queries.ptr, ctypes.byref(n)), "count_blocks")
     return int(n.value)
+
+
+class _Pinned:
+    """Owner of a kfmi_host_alloc block (freed when the last view goes)."""
+
+    def __init__(self, nbytes: int):
+        self.ptr = ctypes.c_void_p()
+        _check(load().kfmi_host_alloc(int(nbytes), ctypes.byref(self.ptr)), "kfmi_host_alloc")
+        self.nbytes = int(nbytes)
+
+    def __del__(self):
+        if self.ptr and _lib is not None:
+            _lib.kfmi_host_free(self.ptr)
+            self.ptr = ctypes.c_void_p()
+
+
+def pinned_empty(shape, dtype=np.uint8) -> np.ndarray:
+    """numpy array in pinned host memory (DMA'd directly by search_stream)."""
+    dt = np.dtype(dtype)
+    n = int(np.prod(shape)) * dt.itemsize
+    owner = _Pinned(max(n, 1))
+    return _owned_view(owner.ptr.value, n, dt, owner).reshape(shape)
+
+
+def search_stream(index: Index, reads: np.ndarray, out: np.ndarray | None = None, chunk: int = 0) -> np.ndarray:
+    """Streamed search of uint8 [N, m] host reads against an index already on the
+    device (transfer_to_gpu(index, None, None)); returns uint32[2N]."""
+    reads = np.ascontiguousarray(reads, dtype=np.uint8)
+    n, m = reads.shape
+    if out is None:
+        out = np.empty(2 * n, dtype=np.uint32)
+    assert out.dtype == np.uint32 and out.flags.c_contiguous and out.size >= 2 * n
+    _check(load().kfmi_search_stream(index.ptr, reads.ctypes.data, n, m, out.ctypes.data, int(chunk)),
+           "kfmi_search_stream")
+    return out
 
 
 def search_array(index: Index, queries: np.ndarray, backend: str | None = None) -> np.ndarray:

@@ -64,8 +64,9 @@ def test_backend_matches_reference_results(gpu, oracle_mod, backend, case, key):
             want = oracle_mod.read_results_file(
                 GOLDEN / case / ent["results"][f"{m}.{200 if ac else 100}"]["file"])
             if not coop_supported(backend, k, d):
-                with pytest.raises(gpu.KfmiError):
+                with pytest.raises(gpu.KfmiError) as e:
                     gpu.search_array(idx, q, backend)
+                assert e.value.code == 33          # KFMI_E_BAD_ARGUMENT at transferCPUtoGPU
                 return
             got = gpu.search_array(idx, q, backend)
             assert np.array_equal(got, want), (backend, case, key, tag, m,
@@ -107,8 +108,9 @@ def test_backend_matches_oracle_random(gpu, oracle_mod, random_index, backend, k
         else:
             want, _ = oracle_mod.search(idx.image(), q)
         if not coop_supported(backend, k, d):
-            with pytest.raises(gpu.KfmiError):
+            with pytest.raises(gpu.KfmiError) as e:
                 gpu.search_array(idx, q, backend)
+            assert e.value.code == 33
             return
         got = gpu.search_array(idx, q, backend)
         assert np.array_equal(got, want), (backend, kd, m)

@@ -1,0 +1,84 @@
+"""Streamed search from host memory (kfmi_search_stream): chunked
+H2D / pack + LF / D2H overlap on three HIP streams must return exactly what the
+resident-batch path (kfmi_search) and the CPU oracle return, for ragged chunk
+sizes and for pinned and pageable host buffers."""
+import numpy as np
+import pytest
+
+import util
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def setup(kfmi_mod):
+    K = kfmi_mod
+    if K.device_count() < 1:
+        pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
+    K.set_device(0)
+    rng = np.random.default_rng(77)
+    text = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=300_001).tobytes()
+    idx = K.Index.build(text, k=2, d=64, gpu=True)
+    t = np.frombuffer(text, np.uint8)
+    starts = rng.integers(0, len(text) - 100, size=7_000)
+    reads = np.concatenate([t[starts[:, None] + np.arange(100)],
+                            rng.choice(np.frombuffer(b"ACGTN", np.uint8), size=(3_007, 100))])
+    return K, idx, reads
+
+
+@pytest.mark.parametrize("backend", ["task-mid", "coop-mid", "task", "coop-ac"])
+@pytest.mark.parametrize("chunk", [0, 1_000, 4_099])
+def test_stream_equals_batch_and_oracle(setup, oracle_mod, backend, chunk):
+    K, idx, reads = setup
+    want = K.search_array(idx, reads, backend)
+    got = K.search_stream(idx, reads, chunk=chunk)
+    assert np.array_equal(got, want)
+    if chunk == 1_000 and backend == "task-mid":
+        ores, _ = oracle_mod.search(idx.image(), reads, 8)
+        assert np.array_equal(got, ores)
+
+
+def test_stream_pinned_buffers(setup):
+    K, idx, reads = setup
+    K.set_backend("task-mid")
+    K.transfer_to_gpu(idx, None, None)
+    want = K.search_array(idx, reads)
+    pin_in = K.pinned_empty(reads.shape, np.uint8)
+    pin_in[:] = reads
+    pin_out = K.pinned_empty((2 * reads.shape[0],), np.uint32)
+    got = K.search_stream(idx, pin_in, out=pin_out, chunk=777)
+    assert np.array_equal(got, want)
+    # mixed: pinned in, pageable out
+    assert np.array_equal(K.search_stream(idx, pin_in, chunk=2_048), want)
+    assert K.last_timing()["total_ms"] > 0
+
+
+def test_stream_k1_and_150bp(kfmi_mod, oracle_mod):
+    K = kfmi_mod
+    K.set_device(0)
+    rng = np.random.default_rng(5)
+    text = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=50_000).tobytes()
+    idx = K.Index.build(text, k=1, d=64, gpu=True)
+    t = np.frombuffer(text, np.uint8)
+    reads = t[rng.integers(0, len(text) - 150, size=2_000)[:, None] + np.arange(150)]
+    K.set_backend("task-mid")
+    K.transfer_to_gpu(idx, None, None)
+    got = K.search_stream(idx, reads, chunk=300)
+    ores, _ = oracle_mod.search(idx.image(), reads, 8)
+    assert np.array_equal(got, ores)
+
+
+def test_stream_errors(setup):
+    K, idx, reads = setup
+    K.set_backend("task-mid")
+    K.transfer_to_gpu(idx, None, None)
+    assert K.search_stream(idx, reads[:0]).size == 0
+    odd = np.ascontiguousarray(reads[:10, :99])          # 99 % K != 0 (B6)
+    with pytest.raises(K.KfmiError) as e:
+        K.search_stream(idx, odd)
+    assert e.value.code == 33
+    fresh = K.Index.build(b"ACGTACGTTGCA" * 50, k=2, d=64, gpu=False)
+    with pytest.raises(K.KfmiError) as e:
+        K.search_stream(fresh, reads[:10])
+    assert e.value.code == 34
+    K.load().kfmi_stream_release()
