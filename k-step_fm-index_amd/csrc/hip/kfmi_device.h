@@ -112,6 +112,82 @@ __device__ __forceinline__ uint32_t code_of(uint32_t x)
   return (b1 | b0) >> 1;
 }
 
+// Four ASCII bases (byte j = base j of the group) -> one byte of 2-bit codes in
+// reverse order (base 3 at bits 0-1, base 0 at bits 6-7).  SWAR form of
+// code_of on every byte: code = (bit2 << 1) | (bit1 ^ bit2).
+__device__ __forceinline__ uint32_t group_codes_rev(uint32_t x)
+{
+  const uint32_t b1 = (x >> 2) & 0x01010101u;
+  const uint32_t y = (b1 << 1) | (((x >> 1) & 0x01010101u) ^ b1);
+  return ((y >> 24) & 0x03u) | ((y >> 14) & 0x0Cu) | ((y >> 4) & 0x30u) | ((y << 6) & 0xC0u);
+}
+
+// Shift the 2-bit code stream cw (cw[0] = lowest bits) left by `sh` bits
+// (sh in {2,4,6,8}, wave-uniform) and insert `v` (sh bits) at the bottom.
+template <int MAXW>
+__device__ __forceinline__ void push_codes(uint32_t (&cw)[MAXW], uint32_t v, uint32_t sh)
+{
+#pragma unroll
+  for (int k = MAXW - 1; k > 0; --k) cw[k] = __builtin_amdgcn_alignbit(cw[k], cw[k - 1], 32u - sh);
+  cw[0] = (cw[0] << sh) | v;
+}
+
+// One ASCII row of m bases at base + off (any alignment; base 16-byte aligned,
+// global or LDS) -> the reversed 2-bit stream the pack kernel writes: base
+// m-1-r at bits 2r, so word w is packed word w of the query and K-step t sits
+// at bits 2K*t (the order of fmIndexCPUBaseline.c:200-226).  Requires
+// m <= 16*MAXW and 8 readable bytes past the row.
+template <int MAXW>
+__device__ __forceinline__ void row_codes(const uint8_t* __restrict__ base, uint64_t off, uint32_t m,
+                                          uint32_t (&cw)[MAXW])
+{
+  const uint32_t* a = reinterpret_cast<const uint32_t*>(base + (off & ~3ull));
+  const uint32_t sh = (uint32_t) (off & 3u);
+#pragma unroll
+  for (int k = 0; k < MAXW; ++k) cw[k] = 0;
+  const uint32_t ng = m >> 2, rem = m & 3u;
+  uint32_t lo = a[0];
+#pragma unroll 8
+  for (uint32_t i = 0; i < ng; ++i) {
+    const uint32_t hi = a[i + 1];
+    push_codes<MAXW>(cw, group_codes_rev(__builtin_amdgcn_alignbyte(hi, lo, sh)), 8u);
+    lo = hi;
+  }
+  if (rem) {
+    const uint32_t x = __builtin_amdgcn_alignbyte(a[ng + 1], lo, sh);
+    push_codes<MAXW>(cw, group_codes_rev(x) >> (2u * (4u - rem)), 2u * rem);
+  }
+}
+
+// Fused query packing for a 256-thread block, one query per thread: each
+// wave copies its rows HBM -> LDS with coalesced 16-byte loads, RPR rows per
+// round, and the lanes owning those rows convert them from LDS (a lane reading
+// its own row from HBM would touch a different line per lane).  LDS per wave:
+// stage_slot_bytes(m).  Every thread of the block must call it.
+__host__ __device__ constexpr uint32_t stage_rows(uint32_t m) { return m <= 128 ? 32u : 16u; }
+__host__ __device__ constexpr uint32_t stage_slot_bytes(uint32_t m) { return (stage_rows(m) * m + 31u) & ~15u; }
+
+template <int MAXW>
+__device__ __forceinline__ void stage_query_codes(const uint8_t* __restrict__ ascii, uint64_t num, uint32_t m,
+                                                  uint8_t* __restrict__ lds, uint32_t (&cw)[MAXW])
+{
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint32_t rpr = stage_rows(m);
+  uint8_t* wl = lds + wv * stage_slot_bytes(m);
+  const uint64_t q0 = (uint64_t) blockIdx.x * 256 + wv * 64;
+#pragma unroll 1
+  for (uint32_t h = 0; h < 64u / rpr; ++h) {
+    const uint64_t r0 = q0 + h * rpr;
+    const uint64_t nr = r0 < num ? (num - r0 < rpr ? num - r0 : rpr) : 0;
+    const uint32_t n16 = (uint32_t) ((nr * m + 15) / 16);           /* <= 15 bytes of slack read */
+    const uint4* src = reinterpret_cast<const uint4*>(ascii + r0 * m);   /* r0*m % 16 == 0 */
+    for (uint32_t i = lane; i < n16; i += 64) reinterpret_cast<uint4*>(wl)[i] = src[i];
+    __syncthreads();
+    if (lane / rpr == h) row_codes<MAXW>(wl, (uint64_t) (lane % rpr) * m, m, cw);
+    __syncthreads();
+  }
+}
+
 // first-`sh`-rows mask of one 32-row word, MSB = first row; sh clamped to [0,32]
 __device__ __forceinline__ uint32_t row_mask(int sh)
 {

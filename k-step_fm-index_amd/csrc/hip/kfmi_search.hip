@@ -216,14 +216,25 @@ __global__ __launch_bounds__(256) void pack_queries_kernel(const uint8_t* __rest
 
 /* ------------------------------------------------------------------------ */
 /* task-per-query kernel: one thread owns QPT queries (both ends each)       */
+/* MAXW == 0: codes come from the pack kernel's words (qp);                 */
+/* MAXW  > 0: the thread reads its own ASCII row once and keeps the codes   */
+/*            in MAXW registers (fused packing, no pack launch, no qp).     */
 /* ------------------------------------------------------------------------ */
 
-template <class G, int QPT>
-__global__ __launch_bounds__(256) void task_kernel(IdxArgs ix, const uint32_t* __restrict__ qp, uint64_t num,
+template <class G, int QPT, int MAXW>
+__global__ __launch_bounds__(256) void task_kernel(IdxArgs ix, const uint32_t* __restrict__ qp,
+                                                   const uint8_t* __restrict__ ascii, uint32_t m, uint64_t num,
                                                    uint32_t steps, uint32_t nwords, uint32_t* __restrict__ res)
 {
   constexpr int SPW = G::SPW;
+  constexpr int CW = MAXW > 0 ? MAXW : 1;
+  static_assert(MAXW == 0 || QPT == 1, "fused packing: one query per thread");
   const uint64_t base = (uint64_t) blockIdx.x * (256 * QPT) + threadIdx.x;
+  uint32_t cw[QPT][CW];
+  if constexpr (MAXW > 0) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t stage[];
+    stage_query_codes<MAXW>(ascii, num, m, stage, cw[0]);   /* whole block, before any exit */
+  }
   if (base >= num) return;
   uint64_t q[QPT];
   uint32_t L[QPT], R[QPT];
@@ -237,7 +248,15 @@ __global__ __launch_bounds__(256) void task_kernel(IdxArgs ix, const uint32_t* _
   for (uint32_t w = 0; w < nwords; ++w) {
     uint32_t word[QPT];
 #pragma unroll
-    for (int i = 0; i < QPT; ++i) word[i] = qp[(uint64_t) w * num + q[i]];
+    for (int i = 0; i < QPT; ++i) {
+      if constexpr (MAXW > 0) {
+        word[i] = cw[i][0];
+#pragma unroll
+        for (int k = 0; k + 1 < CW; ++k) cw[i][k] = cw[i][k + 1];
+      } else {
+        word[i] = qp[(uint64_t) w * num + q[i]];
+      }
+    }
     const uint32_t left = steps - w * SPW;
 #pragma unroll
     for (int j = 0; j < SPW; ++j) {
@@ -384,6 +403,9 @@ struct SearchLaunch {
   hipStream_t st;
   IdxArgs ix;
   const uint32_t* qp;
+  const uint8_t* ascii;   /* fused packing: ASCII rows of m bases */
+  uint32_t m;
+  int maxw;               /* 0: packed words in qp; 8/16: fused packing */
   uint64_t num;
   uint32_t steps, nwords;
   uint32_t* res;
@@ -396,17 +418,38 @@ static int task_qpt(void)
   return v == 2 ? 2 : 1;
 }
 
+/* Code registers the task kernel needs to pack a query itself (0: use the
+ * pack kernel).  KFMI_FUSED=0 forces the separate pack launch. */
+static bool is_coop(int backend);
+
+static int fused_maxw(int backend, uint32_t nwords)
+{
+  if (is_coop(backend)) return 0;
+  const char* e = getenv("KFMI_FUSED");
+  if (e && !atoi(e)) return 0;
+  return nwords <= 8 ? 8 : (nwords <= 16 ? 16 : 0);
+}
+
 template <class G>
 static hipError_t launch_task(const SearchLaunch& a)
 {
-  if (task_qpt() == 2) {
+  if (a.maxw) {
+    const uint64_t blocks = (a.num + 255) / 256;
+    const size_t lds = 4 * (size_t) stage_slot_bytes(a.m);
+    if (a.maxw == 8)
+      hipLaunchKernelGGL((task_kernel<G, 1, 8>), dim3((uint32_t) blocks), dim3(256), lds, a.st, a.ix, a.qp, a.ascii,
+                         a.m, a.num, a.steps, a.nwords, a.res);
+    else
+      hipLaunchKernelGGL((task_kernel<G, 1, 16>), dim3((uint32_t) blocks), dim3(256), lds, a.st, a.ix, a.qp,
+                         a.ascii, a.m, a.num, a.steps, a.nwords, a.res);
+  } else if (task_qpt() == 2) {
     const uint64_t blocks = (a.num + 511) / 512;
-    hipLaunchKernelGGL((task_kernel<G, 2>), dim3((uint32_t) blocks), dim3(256), 0, a.st, a.ix, a.qp, a.num,
-                       a.steps, a.nwords, a.res);
+    hipLaunchKernelGGL((task_kernel<G, 2, 0>), dim3((uint32_t) blocks), dim3(256), 0, a.st, a.ix, a.qp, a.ascii,
+                       a.m, a.num, a.steps, a.nwords, a.res);
   } else {
     const uint64_t blocks = (a.num + 255) / 256;
-    hipLaunchKernelGGL((task_kernel<G, 1>), dim3((uint32_t) blocks), dim3(256), 0, a.st, a.ix, a.qp, a.num,
-                       a.steps, a.nwords, a.res);
+    hipLaunchKernelGGL((task_kernel<G, 1, 0>), dim3((uint32_t) blocks), dim3(256), 0, a.st, a.ix, a.qp, a.ascii,
+                       a.m, a.num, a.steps, a.nwords, a.res);
   }
   return hipGetLastError();
 }
@@ -882,13 +925,16 @@ extern "C" int32_t kfmi_search(void* index, void* queries, void* results)
   a.st = ctx->st;
   a.ix = idx_args(di);
   a.qp = dq->packed;
+  a.ascii = dq->ascii;
+  a.m = dq->size;
+  a.maxw = fused_maxw(di->backend, dq->nwords);
   a.num = dq->num;
   a.steps = dq->steps;
   a.nwords = dq->nwords;
   a.res = r->d_results;
 
   HIP_OK(hipEventRecord(ctx->ev[0], ctx->st));
-  HIP_OK(launch_pack(dq, ctx->st));
+  if (!a.maxw) HIP_OK(launch_pack(dq, ctx->st));
   HIP_OK(hipEventRecord(ctx->ev[1], ctx->st));
   if (dq->num) {
     const Op op = is_coop(di->backend) ? Op::Coop : Op::Task;
@@ -932,6 +978,9 @@ extern "C" int32_t kfmi_count_blocks(void* index, void* queries, uint64_t* block
   a.st = ctx->st;
   a.ix = idx_args(di);
   a.qp = dq->packed;
+  a.ascii = dq->ascii;
+  a.m = dq->size;
+  a.maxw = 0;
   a.num = dq->num;
   a.steps = dq->steps;
   a.nwords = dq->nwords;
@@ -1208,13 +1257,16 @@ extern "C" int32_t kfmi_search_stream(void* index, const char* ascii, uint64_t n
     a.st = s.st;
     a.ix = ix;
     a.qp = s.dq.packed;
+    a.ascii = s.dq.ascii;
+    a.m = size;
+    a.maxw = fused_maxw(di->backend, nwords);
     a.num = s.n;
     a.steps = steps;
     a.nwords = nwords;
     a.res = s.d_res;
     void* hdst = pin_out ? (void*) (results + 2 * s.q0) : (void*) s.h_out;
     if (hipMemcpyAsync(s.dq.ascii, hsrc, bytes, hipMemcpyHostToDevice, s.st) != hipSuccess ||
-        launch_pack(&s.dq, s.st) != hipSuccess || dispatch(op, K, di->nb, di->layout, a) != hipSuccess ||
+        (!a.maxw && launch_pack(&s.dq, s.st) != hipSuccess) || dispatch(op, K, di->nb, di->layout, a) != hipSuccess ||
         hipMemcpyAsync(hdst, s.d_res, 8ull * s.n, hipMemcpyDeviceToHost, s.st) != hipSuccess ||
         hipEventRecord(s.done, s.st) != hipSuccess) {
       status = KFMI_E_KERNEL;
