@@ -59,6 +59,9 @@ def parse():
     p.add_argument("--variant-steps", type=int, default=3)
     p.add_argument("--no-md5", action="store_true")
     p.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic.json"))
+    p.add_argument("--sa-rate", type=int, default=32,
+                   help="SA sampling rate of the index for the locate leg (0 = no locate)")
+    p.add_argument("--locate-steps", type=int, default=3)
     return p.parse_args()
 
 
@@ -154,7 +157,7 @@ def main():
     text = make_text(a.ref_size)
     log(f"rank {D.rank}: text {len(text)} bases in {time.perf_counter() - t:.1f}s")
     t = time.perf_counter()
-    idx = K.Index.build(text, k=a.k, d=a.d, gpu=True)
+    idx = K.Index.build(text, k=a.k, d=a.d, gpu=True, sa_rate=a.sa_rate)
     build_s = time.perf_counter() - t
     log(f"rank {D.rank}: GPU index build {build_s:.1f}s")
     pinned = (a.ref_size == 3_000_000_000 and a.k == 2 and a.d == 64)
@@ -228,6 +231,34 @@ def main():
 
     extra = {}
     cpu = None
+    if D.rank == 0 and D.world == 1 and a.sa_rate:
+        # ---- locate: text positions of every [L, R) ---------
+        loc = K.locate(idx, r)                                  # warm-up (SA upload)
+        loc.close()
+        lms, kms = [], []
+        for _ in range(a.locate_steps):
+            t = time.perf_counter()
+            loc = K.locate(idx, r)
+            lms.append((time.perf_counter() - t) * 1e3)
+            kms.append(K.last_timing()["lf_ms"])
+            if _ < a.locate_steps - 1:
+                loc.close()
+        off, pos = loc.offsets(), loc.positions()
+        # property check on a sample: every first position starts its read
+        t8 = np.frombuffer(text, dtype=np.uint8)
+        smp = np.arange(0, reads.shape[0], max(1, reads.shape[0] // 100_000))
+        has = off[smp + 1] > off[smp]
+        p0 = pos[off[smp[has]].astype(np.int64)].astype(np.int64)
+        ok = bool(has.all()) and bool(np.array_equal(t8[p0[:, None] + np.arange(a.qlen)[None, :]], reads[smp[has]]))
+        extra["locate"] = {"sa_rate": a.sa_rate, "positions": int(loc.total()),
+                           "kernel_ms": round(float(np.median(kms)), 3),
+                           "call_ms": round(float(np.median(lms)), 3),
+                           "Mpositions_per_s": round(loc.total() / (float(np.median(kms)) / 1e3) / 1e6, 1),
+                           "sample_checked": int(has.sum()), "positions_start_reads": ok,
+                           "what": "kfmi_locate on the timed batch's device results: count + scan + LF_K walk "
+                                   "to a sampled row (kernel_ms = walk kernel, call_ms = incl. D2H of positions)"}
+        log(f"locate {extra['locate']}")
+        loc.close()
     if D.rank == 0 and D.world == 1:
         # ---- other backends (same index, same reads) ------------------------
         for b in [x for x in a.variants.split(",") if x and x != a.backend]:

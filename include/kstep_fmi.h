@@ -187,8 +187,36 @@ int32_t kfmi_host_free(void *p);
 /* Frees the staging and device buffers kfmi_search_stream keeps per device. */
 int32_t kfmi_stream_release(void);
 
-/* Bytes of the device-resident index for the current backend. */
+/* Bytes of the device-resident index for the current backend (incl. SA samples). */
 uint64_t kfmi_device_index_bytes(void *index);
+
+/* ---- locate: SA interval -> text positions --------------
+ * Not in the reference, which stops at [L, R) (fmIndexCPUBaseline.c:288-290).
+ * The index keeps a row-sampled suffix array, SA[r] for rows r % rate == 0
+ * (rate a power of two <= 65536; 1 = the full SA, 4 B per row), and every other
+ * row is walked back with LF_K to a sampled or '$' row on the device. */
+
+/* kfmi_build_index_cpu/_gpu plus SA samples (sa_rate 0: none); `on_device`
+ * selects the GPU builder. */
+int32_t kfmi_build_index_ex(const char *text, uint64_t n, uint32_t k, uint32_t d, uint32_t sa_rate,
+                            int32_t on_device, void **index);
+/* The index's samples (count 0 / rate 0 when it has none); owned by the index. */
+int32_t kfmi_index_sa(void *index, const uint32_t **sa, uint64_t *count, uint32_t *rate);
+/* Sample file: u32 "KSA1", rate, bwtsize, 0; u64 count; u32 samples[count].
+ * kfmi_load_sa attaches a file's samples to an index of the same text. */
+int32_t kfmi_save_sa(const char *fn, void *index);
+int32_t kfmi_load_sa(const char *fn, void *index);
+/* Text positions of the rows of every query's [L, R) -- at most max_occ per
+ * query (the first rows; 0 = all) -- from results still on the device (after
+ * searchIndexGPU / kfmi_search) and an index with samples on the device.
+ * Query q's positions are positions[offsets[q] .. offsets[q+1]), in row order
+ * (positions[offsets[q] + j] = SA[L_q + j]).  kfmi_last_timing: total, scan,
+ * locate kernel (ms).  Errors: 34 before transfer/search, 33 without samples. */
+int32_t         kfmi_locate(void *index, void *results, uint32_t max_occ, void **locations);
+uint64_t        kfmi_locations_total(void *locations);
+const uint64_t *kfmi_locations_offsets(void *locations);    /* num + 1 */
+const uint32_t *kfmi_locations_positions(void *locations);  /* total */
+int32_t         kfmi_locations_free(void **locations);
 
 #ifdef __cplusplus
 }

@@ -184,6 +184,16 @@ __global__ __launch_bounds__(256) void k_fill(const uint32_t* __restrict__ occ, 
   for (uint32_t c = 0; c < nc; ++c) e[c] = occ[(uint64_t) c * nentries + b] + cprime[c];
 }
 
+/* row-sampled suffix array: out[i] = SA[i * rate] (row 0 is the '$' suffix, SA = n) */
+__global__ __launch_bounds__(256) void k_sample(const uint32_t* __restrict__ sa, uint64_t n, uint32_t rate,
+                                                uint64_t count, uint32_t* __restrict__ out)
+{
+  const uint64_t i = (uint64_t) blockIdx.x * 256 + threadIdx.x;
+  if (i >= count) return;
+  const uint64_t r = i * rate;
+  out[i] = r == 0 ? (uint32_t) n : sa[r - 1];
+}
+
 struct DevBuf {
   void* p = nullptr;
   ~DevBuf() { if (p) (void) hipFree(p); }
@@ -205,7 +215,7 @@ struct SuffixLess {
   }
 };
 
-int32_t build_gpu(const char* text, uint64_t n, uint32_t k, uint32_t d, int dev, kfmi_fmi_t** out)
+int32_t build_gpu(const char* text, uint64_t n, uint32_t k, uint32_t d, uint32_t sa_rate, int dev, kfmi_fmi_t** out)
 {
   /* n + 1 >= k: every D_s (s < k) exists -- SA = s is a suffix of T for s < n and
    * the '$' row 0 for s == n -- and (SA - 1 - s) wraps at most once. */
@@ -332,6 +342,18 @@ int32_t build_gpu(const char* text, uint64_t n, uint32_t k, uint32_t d, int dev,
     le = hipGetLastError();
     if (le != hipSuccess) return fail(KFMI_E_BUILDING_FMI);
   }
+  if (sa_rate) {   /* locate samples, before the SA is released */
+    err = kfmi_sa_alloc(f, sa_rate);
+    if (err) return fail(err);
+    DevBuf smp;
+    if (smp.alloc(4 * f->sa_count) != hipSuccess) return fail(KFMI_E_ALLOCATING_FMI);
+    hipLaunchKernelGGL(k_sample, dim3((uint32_t) ((f->sa_count + 255) / 256)), dim3(256), 0, st, sa.as<uint32_t>(), n,
+                       sa_rate, f->sa_count, smp.as<uint32_t>());
+    if (hipGetLastError() != hipSuccess ||
+        hipMemcpyAsync(f->h_sa, smp.p, 4 * f->sa_count, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+      return fail(KFMI_E_BUILDING_FMI);
+  }
   sa.release();
   /* 6. per-code exclusive scans over blocks */
   {
@@ -405,15 +427,22 @@ int32_t build_gpu(const char* text, uint64_t n, uint32_t k, uint32_t d, int dev,
 
 }  // namespace
 
+extern "C" int32_t kfmi_build_index_gpu_sa(const char* text, uint64_t n, uint32_t k, uint32_t d, uint32_t sa_rate,
+                                           void** index)
+{
+  if (sa_rate && !kfmi_sa_rate_ok(sa_rate)) return KFMI_E_BAD_ARGUMENT;
+  if (kfmi_device_count() < 1) return KFMI_E_NO_DEVICE;
+  int32_t e = build_gpu(text, n, k, d, sa_rate, kfmi_current_device(), (kfmi_fmi_t**) index);
+  if (e == KFMI_E_NOT_IMPLEMENTED) {
+    fprintf(stderr, "kstepfmi build: text too repetitive for the GPU tie breaker, using the host builder\n");
+    return kfmi_build_index_cpu_sa(text, n, k, d, sa_rate, index);
+  }
+  return e;
+}
+
 extern "C" int32_t kfmi_build_index_gpu(const char* text, uint64_t n, uint32_t k, uint32_t d,
                                         int32_t want_host_image, void** index)
 {
   (void) want_host_image;   /* the host image is always produced (saveIndex, oracle, md5 pins) */
-  if (kfmi_device_count() < 1) return KFMI_E_NO_DEVICE;
-  int32_t e = build_gpu(text, n, k, d, kfmi_current_device(), (kfmi_fmi_t**) index);
-  if (e == KFMI_E_NOT_IMPLEMENTED) {
-    fprintf(stderr, "kstepfmi build: text too repetitive for the GPU tie breaker, using the host builder\n");
-    return kfmi_build_index_cpu(text, n, k, d, index);
-  }
-  return e;
+  return kfmi_build_index_gpu_sa(text, n, k, d, 0, index);
 }

@@ -10,6 +10,7 @@
  * defects B1-B4 of SURVEY.md Appendix B.
  */
 #include <hip/hip_runtime.h>
+#include <rocprim/device/device_scan.hpp>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -21,6 +22,7 @@
 #include "../kfmi_internal.h"
 #include "kfmi_device.h"
 #include "kfmi_coop.h"
+#include "kfmi_locate.h"
 
 using namespace kfmi;
 
@@ -158,6 +160,9 @@ struct kfmi_dev_index {
   uint64_t ent_bytes = 0;
   uint32_t* sb = nullptr;      /* packed: superblock counters */
   uint64_t sb_bytes = 0;
+  uint32_t* sa = nullptr;      /* locate: row-sampled suffix array */
+  uint64_t sa_bytes = 0;
+  uint32_t sa_log2 = 0, sa_gen = 0;
 };
 
 struct kfmi_dev_queries {
@@ -409,6 +414,13 @@ struct SearchLaunch {
   uint64_t num;
   uint32_t steps, nwords;
   uint32_t* res;
+  /* locate */
+  const uint32_t* sa;
+  uint32_t sa_log2;
+  const uint64_t* off;
+  const uint32_t* owner;
+  uint64_t total;
+  uint32_t* pos;
 };
 
 static int task_qpt(void)
@@ -478,7 +490,23 @@ static bool nb_supported(uint32_t nb)
   return nb == 1 || nb == 2 || nb == 4 || nb == 6 || nb == 8 || nb == 14 || nb == 30;
 }
 
-enum class Op { Task, Coop, Count };
+/* Locate: enough lanes to fill every CU (8 workgroups of 256 per CU), each
+ * lane walking slot after slot. */
+template <class G>
+static hipError_t launch_locate(const SearchLaunch& a)
+{
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+    cus = 256;
+  uint64_t blocks = (a.total + 255) / 256;
+  if (blocks > (uint64_t) cus * 8) blocks = (uint64_t) cus * 8;
+  hipLaunchKernelGGL((locate_kernel<G>), dim3((uint32_t) blocks), dim3(256), 0, a.st, a.ix, a.sa, a.sa_log2, a.owner,
+                     a.total, a.pos);
+  return hipGetLastError();
+}
+
+enum class Op { Task, Coop, Count, Locate };
 
 template <int K, int NB, int LAY>
 static hipError_t dispatch_one(Op op, const SearchLaunch& a, unsigned long long* d_total)
@@ -487,6 +515,7 @@ static hipError_t dispatch_one(Op op, const SearchLaunch& a, unsigned long long*
   switch (op) {
     case Op::Task: return launch_task<G>(a);
     case Op::Coop: return launch_coop<G>(a);
+    case Op::Locate: return launch_locate<G>(a);
     default: return launch_count<G>(a, d_total);
   }
 }
@@ -680,7 +709,32 @@ static void free_dev_index(kfmi_dev_index* di)
   if (di->device >= 0) (void) hipSetDevice(di->device);
   if (di->ent) (void) hipFree(di->ent);
   if (di->sb) (void) hipFree(di->sb);
+  if (di->sa) (void) hipFree(di->sa);
   delete di;
+}
+
+/* Device copy of the index's SA samples (locate); none when it has none. */
+static int32_t upload_sa(const kfmi_fmi_t* f, kfmi_dev_index* di, DevCtx* ctx)
+{
+  if (di->sa) (void) hipFree(di->sa);
+  di->sa = nullptr;
+  di->sa_bytes = 0;
+  di->sa_gen = f->sa_gen;
+  if (!f->h_sa || !f->sa_rate) return KFMI_SUCCESS;
+  const uint64_t bytes = 4ull * f->sa_count;
+  if (hipMalloc((void**) &di->sa, bytes + 4) != hipSuccess) {
+    di->sa = nullptr;
+    return KFMI_E_DEVICE_ALLOC;
+  }
+  if (hipMemcpyAsync(di->sa, f->h_sa, bytes, hipMemcpyHostToDevice, ctx->st) != hipSuccess ||
+      hipStreamSynchronize(ctx->st) != hipSuccess) {
+    (void) hipFree(di->sa);
+    di->sa = nullptr;
+    return KFMI_E_KERNEL;
+  }
+  di->sa_bytes = bytes;
+  di->sa_log2 = (uint32_t) __builtin_ctz(f->sa_rate);
+  return KFMI_SUCCESS;
 }
 
 static int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx)
@@ -800,6 +854,13 @@ static int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx)
     }
   }
   if (owned) freeIndex((void**) &owned);
+  if (f->h_sa) {
+    err = upload_sa(f, di, ctx);
+    if (err) {
+      free_dev_index(di);
+      return err;
+    }
+  }
   if (f->dev) free_dev_index(f->dev);
   f->dev = di;
   return KFMI_SUCCESS;
@@ -1045,7 +1106,149 @@ extern "C" uint64_t kfmi_device_index_bytes(void* index)
 {
   kfmi_fmi_t* f = (kfmi_fmi_t*) index;
   if (!f || !f->dev) return 0;
-  return f->dev->ent_bytes + f->dev->sb_bytes;
+  return f->dev->ent_bytes + f->dev->sb_bytes + f->dev->sa_bytes;
+}
+
+/* ------------------------------------------------------------------------ */
+/* locate: [L, R) of every query -> text positions          */
+/* ------------------------------------------------------------------------ */
+
+struct kfmi_locations {
+  uint64_t num = 0, total = 0;
+  uint64_t* h_off = nullptr;   /* num + 1 */
+  uint32_t* h_pos = nullptr;   /* total */
+};
+
+extern "C" int32_t kfmi_locations_free(void** locations)
+{
+  kfmi_locations* L = locations ? (kfmi_locations*) *locations : nullptr;
+  if (L) {
+    free(L->h_off);
+    free(L->h_pos);
+    delete L;
+    *locations = nullptr;
+  }
+  return KFMI_SUCCESS;
+}
+
+extern "C" uint64_t kfmi_locations_total(void* locations)
+{
+  return locations ? ((kfmi_locations*) locations)->total : 0;
+}
+
+extern "C" const uint64_t* kfmi_locations_offsets(void* locations)
+{
+  return locations ? ((kfmi_locations*) locations)->h_off : nullptr;
+}
+
+extern "C" const uint32_t* kfmi_locations_positions(void* locations)
+{
+  return locations ? ((kfmi_locations*) locations)->h_pos : nullptr;
+}
+
+extern "C" int32_t kfmi_locate(void* index, void* results, uint32_t max_occ, void** locations)
+{
+  kfmi_fmi_t* f = (kfmi_fmi_t*) index;
+  kfmi_res_t* r = (kfmi_res_t*) results;
+  if (!locations) return KFMI_E_BAD_ARGUMENT;
+  *locations = nullptr;
+  if (!f || !r) return KFMI_E_BAD_ARGUMENT;
+  if (!f->dev || !r->d_results) return KFMI_E_NOT_ON_DEVICE;
+  if (!f->h_sa || !f->sa_rate) return KFMI_E_BAD_ARGUMENT;   /* index built without SA samples */
+  kfmi_dev_index* di = f->dev;
+  DevCtx* ctx = nullptr;
+  int32_t err = ctx_for(di->device, &ctx);
+  if (err) return err;
+  if (!di->sa || di->sa_gen != f->sa_gen) {
+    err = upload_sa(f, di, ctx);
+    if (err) return err;
+  }
+  const uint64_t num = r->num;
+  kfmi_locations* L = new kfmi_locations();
+  L->num = num;
+  L->h_off = (uint64_t*) malloc(8 * (num + 1));
+  if (!L->h_off) {
+    kfmi_locations_free((void**) &L);
+    return KFMI_E_ALLOCATING_RESULTS;
+  }
+  uint64_t *d_cnt = nullptr, *d_off = nullptr;
+  uint32_t *d_pos = nullptr, *d_own = nullptr;
+  void *tmp = nullptr, *tmp2 = nullptr;
+  size_t tb = 0, tb2 = 0;
+  uint64_t total = 0;
+  auto done = [&](int32_t code) {
+    if (d_cnt) (void) hipFree(d_cnt);
+    if (d_off) (void) hipFree(d_off);
+    if (d_pos) (void) hipFree(d_pos);
+    if (d_own) (void) hipFree(d_own);
+    if (tmp) (void) hipFree(tmp);
+    if (tmp2) (void) hipFree(tmp2);
+    if (code) kfmi_locations_free((void**) &L);
+    else *locations = L;
+    return code;
+  };
+  const hipStream_t st = ctx->st;
+  bool ok = hipMalloc((void**) &d_cnt, 8 * (num + 1)) == hipSuccess &&
+            hipMalloc((void**) &d_off, 8 * (num + 1)) == hipSuccess &&
+            rocprim::exclusive_scan(nullptr, tb, d_cnt, d_off, (uint64_t) 0, (size_t) (num + 1),
+                                    rocprim::plus<uint64_t>(), st) == hipSuccess &&
+            hipMalloc(&tmp, tb ? tb : 1) == hipSuccess;
+  if (!ok) return done(KFMI_E_DEVICE_ALLOC);
+  if (hipEventRecord(ctx->ev[0], st) != hipSuccess) return done(KFMI_E_KERNEL);
+  hipLaunchKernelGGL(loc_count_kernel, dim3((uint32_t) ((num + 1 + 255) / 256)), dim3(256), 0, st, r->d_results, num,
+                     max_occ, d_cnt);
+  ok = hipGetLastError() == hipSuccess &&
+       rocprim::exclusive_scan(tmp, tb, d_cnt, d_off, (uint64_t) 0, (size_t) (num + 1), rocprim::plus<uint64_t>(),
+                               st) == hipSuccess &&
+       hipMemcpyAsync(&total, d_off + num, 8, hipMemcpyDeviceToHost, st) == hipSuccess &&
+       hipStreamSynchronize(st) == hipSuccess;
+  if (!ok) return done(KFMI_E_KERNEL);
+  L->total = total;
+  L->h_pos = (uint32_t*) malloc(4 * total + 4);
+  if (!L->h_pos) return done(KFMI_E_ALLOCATING_RESULTS);
+  if (hipMalloc((void**) &d_pos, 4 * total + 4) != hipSuccess ||
+      hipMalloc((void**) &d_own, 4 * total + 4) != hipSuccess ||
+      rocprim::inclusive_scan(nullptr, tb2, d_pos, d_own, (size_t) total, rocprim::maximum<uint32_t>(), st) !=
+          hipSuccess ||
+      hipMalloc(&tmp2, tb2 ? tb2 : 1) != hipSuccess)
+    return done(KFMI_E_DEVICE_ALLOC);
+  if (total) {   /* owner[i] = query of slot i: heads at each query's first slot, then a max-scan */
+    if (hipMemsetAsync(d_pos, 0, 4 * total, st) != hipSuccess) return done(KFMI_E_KERNEL);   /* heads in d_pos */
+    hipLaunchKernelGGL(loc_heads_kernel, dim3((uint32_t) ((num + 255) / 256)), dim3(256), 0, st, d_cnt, d_off, num,
+                       d_pos);
+    if (hipGetLastError() != hipSuccess ||
+        rocprim::inclusive_scan(tmp2, tb2, d_pos, d_own, (size_t) total, rocprim::maximum<uint32_t>(), st) !=
+            hipSuccess)
+      return done(KFMI_E_KERNEL);
+    hipLaunchKernelGGL(loc_rows_kernel, dim3((uint32_t) ((total + 255) / 256)), dim3(256), 0, st, r->d_results, d_off,
+                       total, d_own);   /* owner -> first row of each slot, in place */
+    if (hipGetLastError() != hipSuccess) return done(KFMI_E_KERNEL);
+  }
+  SearchLaunch a{};
+  a.st = st;
+  a.ix = idx_args(di);
+  a.res = r->d_results;
+  a.num = num;
+  a.sa = di->sa;
+  a.sa_log2 = di->sa_log2;
+  a.off = d_off;
+  a.owner = d_own;
+  a.total = total;
+  a.pos = d_pos;
+  ok = hipEventRecord(ctx->ev[1], st) == hipSuccess &&
+       (total == 0 || dispatch(Op::Locate, di->K, di->nb, di->layout, a) == hipSuccess) &&
+       hipEventRecord(ctx->ev[2], st) == hipSuccess &&
+       hipMemcpyAsync(L->h_off, d_off, 8 * (num + 1), hipMemcpyDeviceToHost, st) == hipSuccess &&
+       (total == 0 || hipMemcpyAsync(L->h_pos, d_pos, 4 * total, hipMemcpyDeviceToHost, st) == hipSuccess) &&
+       hipStreamSynchronize(st) == hipSuccess;
+  if (!ok) return done(KFMI_E_KERNEL);
+  float ms01 = 0, ms12 = 0;
+  (void) hipEventElapsedTime(&ms01, ctx->ev[0], ctx->ev[1]);
+  (void) hipEventElapsedTime(&ms12, ctx->ev[1], ctx->ev[2]);
+  t_ms[0] = ms01 + ms12;   /* scan + walk (the host read of the total sits between) */
+  t_ms[1] = ms01;
+  t_ms[2] = ms12;          /* the locate kernel alone */
+  return done(KFMI_SUCCESS);
 }
 
 /* ------------------------------------------------------------------------ */

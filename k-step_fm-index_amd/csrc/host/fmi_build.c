@@ -258,12 +258,21 @@ static int text_to_codes(const char *text, uint64_t n, uint8_t *codes)
 
 int32_t kfmi_build_index_cpu(const char *text, uint64_t n, uint32_t k, uint32_t d, void **index)
 {
+  return kfmi_build_index_cpu_sa(text, n, k, d, 0, index);
+}
+
+/* Tag-100 index plus, when sa_rate != 0, the row-sampled suffix array
+ * SA[i * sa_rate] (locate). */
+int32_t kfmi_build_index_cpu_sa(const char *text, uint64_t n, uint32_t k, uint32_t d, uint32_t sa_rate,
+                                void **index)
+{
   uint8_t *codes, *sym;
   uint32_t *sa;
   uint64_t i;
   int32_t err;
   if (n == 0 || n + 1 < k || n + 1 > 0xFFFFFFFEull) return KFMI_E_BAD_ARGUMENT;
   if (k < 1 || k > KFMI_MAX_STEPS || d == 0 || d % 32) return KFMI_E_BAD_ARGUMENT;
+  if (sa_rate && !kfmi_sa_rate_ok(sa_rate)) return KFMI_E_BAD_ARGUMENT;
   codes = (uint8_t *) malloc(n);
   sym = (uint8_t *) malloc(n + 1);
   sa = (uint32_t *) malloc(sizeof(uint32_t) * (n + 1));
@@ -274,9 +283,24 @@ int32_t kfmi_build_index_cpu(const char *text, uint64_t n, uint32_t k, uint32_t 
   err = kfmi_sais(sym, sa, (uint32_t) (n + 1), 5);
   free(sym);
   if (!err) err = kfmi_index_from_sa(codes, sa, n, k, d, (kfmi_fmi_t **) index);
+  if (!err && sa_rate) {
+    kfmi_fmi_t *f = (kfmi_fmi_t *) *index;
+    err = kfmi_sa_alloc(f, sa_rate);
+    if (err) freeIndex(index);
+    else
+      for (i = 0; i < f->sa_count; i++) f->h_sa[i] = sa[i * sa_rate];
+  }
   free(codes);
   free(sa);
   return err;
+}
+
+int32_t kfmi_build_index_ex(const char *text, uint64_t n, uint32_t k, uint32_t d, uint32_t sa_rate,
+                            int32_t on_device, void **index)
+{
+  if (sa_rate && !kfmi_sa_rate_ok(sa_rate)) return KFMI_E_BAD_ARGUMENT;
+  if (on_device) return kfmi_build_index_gpu_sa(text, n, k, d, sa_rate, index);
+  return kfmi_build_index_cpu_sa(text, n, k, d, sa_rate, index);
 }
 
 /* interface.h:35: K, d from KFMI_K / KFMI_D (the reference: -DK_STEPS, -DNUM_CHUNK). */

@@ -206,9 +206,91 @@ int32_t freeIndex(void **index)
   kfmi_fmi_t *f = index ? (kfmi_fmi_t *) *index : NULL;
   if (!f) return KFMI_SUCCESS;
   if (f->dev) freeIndexGPU(index);
+  free(f->h_sa);
   free(f->image);
   free(f);
   *index = NULL;
+  return KFMI_SUCCESS;
+}
+
+/* ----------------------------------------------------------------------- */
+/* sampled suffix array (locate; not in the reference)      */
+/* File: u32 magic "KSA1", rate, bwtsize, 0; u64 count; u32 samples[count]. */
+/* ----------------------------------------------------------------------- */
+
+#define KFMI_SA_MAGIC 0x3141534Bu   /* "KSA1" little-endian */
+
+int kfmi_sa_rate_ok(uint32_t rate)
+{
+  return rate != 0 && (rate & (rate - 1)) == 0 && rate <= (1u << 16);
+}
+
+int32_t kfmi_sa_alloc(kfmi_fmi_t *f, uint32_t rate)
+{
+  uint64_t count;
+  if (!f || !kfmi_sa_rate_ok(rate)) return KFMI_E_BAD_ARGUMENT;
+  count = ((uint64_t) f->bwtsize + rate - 1) / rate;
+  free(f->h_sa);
+  f->h_sa = (uint32_t *) malloc(4 * count + 4);
+  f->sa_gen++;
+  if (!f->h_sa) { f->sa_rate = 0; f->sa_count = 0; return KFMI_E_ALLOCATING_FMI; }
+  f->sa_rate = rate;
+  f->sa_count = count;
+  return KFMI_SUCCESS;
+}
+
+int32_t kfmi_index_sa(void *index, const uint32_t **sa, uint64_t *count, uint32_t *rate)
+{
+  kfmi_fmi_t *f = (kfmi_fmi_t *) index;
+  if (!f) return KFMI_E_BAD_ARGUMENT;
+  if (sa) *sa = f->h_sa;
+  if (count) *count = f->h_sa ? f->sa_count : 0;
+  if (rate) *rate = f->h_sa ? f->sa_rate : 0;
+  return KFMI_SUCCESS;
+}
+
+int32_t kfmi_save_sa(const char *fn, void *index)
+{
+  kfmi_fmi_t *f = (kfmi_fmi_t *) index;
+  uint32_t h[4];
+  FILE *fp;
+  if (!f || !fn || !f->h_sa) return KFMI_E_BAD_ARGUMENT;
+  h[0] = KFMI_SA_MAGIC; h[1] = f->sa_rate; h[2] = f->bwtsize; h[3] = 0;
+  fp = fopen(fn, "wb");
+  if (!fp) return KFMI_E_SAVING_INDEX_FILE;
+  if (fwrite(h, 4, 4, fp) != 4 || fwrite(&f->sa_count, 8, 1, fp) != 1 ||
+      fwrite(f->h_sa, 4, f->sa_count, fp) != f->sa_count) {
+    fclose(fp);
+    return KFMI_E_SAVING_INDEX_FILE;
+  }
+  fclose(fp);
+  return KFMI_SUCCESS;
+}
+
+/* Attaches the samples of `fn` to an index of the same text (bwtsize checked). */
+int32_t kfmi_load_sa(const char *fn, void *index)
+{
+  kfmi_fmi_t *f = (kfmi_fmi_t *) index;
+  uint32_t h[4];
+  uint64_t count;
+  int32_t err;
+  FILE *fp;
+  if (!f || !fn) return KFMI_E_BAD_ARGUMENT;
+  fp = fopen(fn, "rb");
+  if (!fp) return KFMI_E_OPENING_INDEX_FILE;
+  if (fread(h, 4, 4, fp) != 4 || fread(&count, 8, 1, fp) != 1 || h[0] != KFMI_SA_MAGIC ||
+      !kfmi_sa_rate_ok(h[1]) || h[2] != f->bwtsize || count != ((uint64_t) f->bwtsize + h[1] - 1) / h[1]) {
+    fclose(fp);
+    return KFMI_E_READING_FMI;
+  }
+  err = kfmi_sa_alloc(f, h[1]);
+  if (err) { fclose(fp); return err; }
+  if (fread(f->h_sa, 4, count, fp) != count) {
+    free(f->h_sa); f->h_sa = NULL; f->sa_rate = 0; f->sa_count = 0;
+    fclose(fp);
+    return KFMI_E_READING_FMI;
+  }
+  fclose(fp);
   return KFMI_SUCCESS;
 }
 

@@ -37,6 +37,14 @@ typedef struct {
   uint32_t *h_index;       /* = (uint32_t *)(image + header_bytes), may be unaligned to 16 */
   struct kfmi_dev_index *dev;
   char      src_name[512]; /* file the index came from (for saveIndex/saveResults naming) */
+  /* row-sampled suffix array for locate (not in the reference):
+   * h_sa[i] = SA[i * sa_rate] for i < sa_count = ceil(bwtsize / sa_rate);
+   * sa_rate 0 = none, else a power of two (1 = the full SA).  sa_gen changes
+   * whenever the samples do, so a stale device copy is re-uploaded. */
+  uint32_t  sa_rate;
+  uint32_t  sa_gen;
+  uint64_t  sa_count;
+  uint32_t *h_sa;
 } kfmi_fmi_t;
 
 typedef struct {
@@ -73,6 +81,16 @@ kfmi_backend_t kfmi_backend(void);
 uint32_t       kfmi_backend_tag(kfmi_backend_t b);   /* 101 or 201 */
 int32_t        kfmi_current_device(void);
 void           kfmi_set_last_error(int32_t e);
+
+/* sampled suffix array (fmi_index.c): (re)allocates h_sa for `rate` */
+int32_t kfmi_sa_alloc(kfmi_fmi_t *f, uint32_t rate);
+int     kfmi_sa_rate_ok(uint32_t rate);
+
+/* builders with SA sampling (fmi_build.c, kfmi_build.hip) */
+int32_t kfmi_build_index_cpu_sa(const char *text, uint64_t n, uint32_t k, uint32_t d, uint32_t sa_rate,
+                                void **index);
+int32_t kfmi_build_index_gpu_sa(const char *text, uint64_t n, uint32_t k, uint32_t d, uint32_t sa_rate,
+                                void **index);
 
 /* suffix array construction, fmi_build.c */
 int32_t kfmi_sais(const uint8_t *text_codes, uint32_t *sa, uint32_t n, uint32_t alpha);

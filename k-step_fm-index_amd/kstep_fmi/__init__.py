@@ -97,6 +97,15 @@ def load() -> ctypes.CDLL:
         "kfmi_host_alloc": (i32, [u64, pvp]),
         "kfmi_host_free": (i32, [vp]),
         "kfmi_stream_release": (i32, []),
+        "kfmi_build_index_ex": (i32, [vp, u64, u32, u32, u32, i32, pvp]),
+        "kfmi_index_sa": (i32, [vp, pvp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32)]),
+        "kfmi_save_sa": (i32, [ctypes.c_char_p, vp]),
+        "kfmi_load_sa": (i32, [ctypes.c_char_p, vp]),
+        "kfmi_locate": (i32, [vp, vp, u32, pvp]),
+        "kfmi_locations_total": (u64, [vp]),
+        "kfmi_locations_offsets": (vp, [vp]),
+        "kfmi_locations_positions": (vp, [vp]),
+        "kfmi_locations_free": (i32, [pvp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -191,11 +200,16 @@ class Index(_Handle):
         return cls(p.value)
 
     @classmethod
-    def build(cls, text: bytes, k: int = 2, d: int = 64, gpu: bool = False, host_image: bool = True) -> "Index":
+    def build(cls, text: bytes, k: int = 2, d: int = 64, gpu: bool = False, host_image: bool = True,
+              sa_rate: int = 0) -> "Index":
+        """Tag-100 index of `text`; sa_rate > 0 also keeps SA[r] for rows r % sa_rate == 0 (locate)."""
         L = load()
         buf = np.frombuffer(text, dtype=np.uint8)
         p = ctypes.c_void_p()
-        if gpu:
+        if sa_rate:
+            err = L.kfmi_build_index_ex(buf.ctypes.data, buf.size, k, d, int(sa_rate), int(bool(gpu)),
+                                        ctypes.byref(p))
+        elif gpu:
             err = L.kfmi_build_index_gpu(buf.ctypes.data, buf.size, k, d, int(host_image), ctypes.byref(p))
         else:
             err = L.kfmi_build_index_cpu(buf.ctypes.data, buf.size, k, d, ctypes.byref(p))
@@ -233,6 +247,22 @@ class Index(_Handle):
 
     def device_bytes(self) -> int:
         return int(load().kfmi_device_index_bytes(self._p))
+
+    def sa(self):
+        """(rate, uint32 view of the row-sampled suffix array); (0, empty) when absent."""
+        p = ctypes.c_void_p()
+        n = ctypes.c_uint64()
+        rate = ctypes.c_uint32()
+        _check(load().kfmi_index_sa(self._p, ctypes.byref(p), ctypes.byref(n), ctypes.byref(rate)), "index_sa")
+        if not n.value:
+            return 0, np.zeros(0, dtype=np.uint32)
+        return int(rate.value), _owned_view(p.value, 4 * n.value, np.uint32, self)
+
+    def save_sa(self, fn) -> None:
+        _check(load().kfmi_save_sa(str(fn).encode(), self._p), f"save_sa {fn}")
+
+    def load_sa(self, fn) -> None:
+        _check(load().kfmi_load_sa(str(fn).encode(), self._p), f"load_sa {fn}")
 
     def free_gpu(self) -> None:
         load().freeIndexGPU(ctypes.byref(self._p))
@@ -302,6 +332,53 @@ def count_blocks(index: Index, queries: Queries) -> int:
     n = ctypes.c_uint64()
     _check(load().kfmi_count_blocks(index.ptr, queries.ptr, ctypes.byref(n)), "count_blocks")
     return int(n.value)
+
+
+class Locations(_Handle):
+    """Output of kfmi_locate: offsets uint64[num+1], positions uint32[total]."""
+    _free = "kfmi_locations_free"
+
+    _num = 0
+
+    def offsets(self) -> np.ndarray:
+        return _owned_view(load().kfmi_locations_offsets(self._p), 8 * (self._num + 1), np.uint64, self)
+
+    def positions(self) -> np.ndarray:
+        L = load()
+        t = self.total()
+        if not t:
+            return np.zeros(0, dtype=np.uint32)
+        return _owned_view(L.kfmi_locations_positions(self._p), 4 * t, np.uint32, self)
+
+    def total(self) -> int:
+        return int(load().kfmi_locations_total(self._p))
+
+
+def locate(index: Index, results: Results, max_occ: int = 0) -> Locations:
+    """Text positions of every row of each query's [L, R) (results on the device)."""
+    p = ctypes.c_void_p()
+    _check(load().kfmi_locate(index.ptr, results.ptr, int(max_occ), ctypes.byref(p)), "kfmi_locate")
+    loc = Locations(p.value)
+    loc._num = int(load().kfmi_results_num(results.ptr))
+    return loc
+
+
+def locate_array(index: Index, queries: np.ndarray, backend: str | None = None, max_occ: int = 0):
+    """Search + locate of uint8 [N, m] reads; returns (results uint32[2N],
+    offsets uint64[N+1], positions uint32[total])."""
+    if backend:
+        set_backend(backend)
+    q = Queries.from_array(queries)
+    r = Results.alloc(queries.shape[0])
+    transfer_to_gpu(index, q, r)
+    search(index, q, r)
+    loc = locate(index, r, max_occ)
+    transfer_to_cpu(r)
+    out = (r.array().copy(), loc.offsets().copy(), loc.positions().copy())
+    loc.close()
+    q.close()
+    r.close()
+    return out
 
 
 class _Pinned:

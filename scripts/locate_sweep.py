@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Locate throughput vs SA sampling rate on the 3 Gbase index
+(dev tool, not the bench contract): one text, one read batch, one index build
+per rate; prints one JSON line per (rate, backend)."""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "k-step_fm-index_amd"))
+import kstep_fmi as K  # noqa: E402
+from kstep_fmi import synth  # noqa: E402
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--ref-size", type=int, default=3_000_000_000)
+    p.add_argument("--queries", type=int, default=10_000_000)
+    p.add_argument("--qlen", type=int, default=100)
+    p.add_argument("--rates", default="1,4,16,32,64")
+    p.add_argument("--backends", default="task-mid,task-ac")
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--regs", default="0,1", help="KFMI_LOC_REGS values (one-round-trip walk step)")
+    a = p.parse_args()
+    K.load()
+    K.set_device(0)
+    text = synth.text_3g(a.ref_size) if a.ref_size == 3_000_000_000 else \
+        np.random.default_rng(1).choice(np.frombuffer(b"ACGT", dtype=np.uint8), size=a.ref_size).tobytes()
+    reads = synth.gather_reads(text, synth.read_starts(len(text), a.queries, a.qlen, 10), a.qlen)
+    q = K.Queries.from_array(reads)
+    r = K.Results.alloc(reads.shape[0])
+    t8 = np.frombuffer(text, dtype=np.uint8)
+    for rate in [int(x) for x in a.rates.split(",")]:
+        t = time.perf_counter()
+        idx = K.Index.build(text, k=2, d=64, gpu=True, sa_rate=rate)
+        build_s = time.perf_counter() - t
+        for b, regs in [(b, g) for b in a.backends.split(",") for g in a.regs.split(",")]:
+            os.environ["KFMI_LOC_REGS"] = regs
+            K.set_backend(b)
+            K.transfer_to_gpu(idx, q, r)
+            K.search(idx, q, r)
+            loc = K.locate(idx, r)
+            loc.close()
+            kms = []
+            for _ in range(a.steps):
+                loc = K.locate(idx, r)
+                kms.append(K.last_timing()["lf_ms"])
+                if _ < a.steps - 1:
+                    loc.close()
+            off, pos = loc.offsets(), loc.positions()
+            smp = np.arange(0, reads.shape[0], max(1, reads.shape[0] // 20_000))
+            p0 = pos[off[smp].astype(np.int64)].astype(np.int64)
+            ok = bool(np.array_equal(t8[p0[:, None] + np.arange(a.qlen)[None, :]], reads[smp]))
+            ms = float(np.median(kms))
+            out = {"rate": rate, "backend": b, "regs": int(regs), "positions": int(loc.total()), "kernel_ms": round(ms, 3),
+                   "Mpos_per_s": round(loc.total() / ms / 1e3, 1), "sa_bytes": int(idx.sa()[1].nbytes),
+                   "build_s": round(build_s, 2), "positions_start_reads": ok}
+            print(json.dumps(out), flush=True)
+            loc.close()
+            idx.free_gpu()
+        idx.close()
+
+
+if __name__ == "__main__":
+    main()

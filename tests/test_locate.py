@@ -1,0 +1,208 @@
+"""Locate: SA interval -> text positions.
+
+The reference has no locate (it stops at [L, R), fmIndexCPUBaseline.c:288-290),
+so there is no reference vector for this row: it is pinned against the
+brute-force suffix array of T$ (tests/util.suffix_array, '$' lowest), and at
+any size by the property text[p : p+m] == read for every reported p.
+
+CPU tests: the builders' SA samples, the sample file, argument checks.
+GPU tests (-m gpu): the device walk on every backend / (K, d) / sampling rate.
+"""
+import numpy as np
+import pytest
+
+import util
+
+ACGT = np.frombuffer(b"ACGT", dtype=np.uint8)
+PLAIN = ("task", "coop", "task-packed", "coop-packed", "task-mid", "coop-mid")
+ALT = ("task-ac", "coop-ac")
+
+
+def _text(n, seed):
+    return np.random.default_rng(seed).choice(ACGT, size=n).tobytes()
+
+
+# ----------------------------------------------------------------- CPU ------
+
+@pytest.mark.parametrize("k", [1, 2])
+def test_cpu_builder_sa_samples_equal_bruteforce(kfmi_mod, k):
+    for n in (1, 2, 5, 63, 64, 65, 1000, 20_000):
+        if n + 1 < k:
+            continue
+        text = _text(n, n + k)
+        sa = util.suffix_array(text + b"$")
+        for rate in (1, 2, 8, 32):
+            idx = kfmi_mod.Index.build(text, k=k, d=64, sa_rate=rate)
+            got_rate, got = idx.sa()
+            assert got_rate == rate
+            assert np.array_equal(got, sa[::rate].astype(np.uint32)), (n, k, rate)
+            idx.close()
+
+
+def test_sa_samples_leave_the_index_unchanged(kfmi_mod):
+    text = _text(5000, 3)
+    a = kfmi_mod.Index.build(text, k=2, d=64).image().tobytes()
+    b = kfmi_mod.Index.build(text, k=2, d=64, sa_rate=4).image().tobytes()
+    assert a == b
+
+
+def test_sa_file_roundtrip(kfmi_mod, tmp_path):
+    text = _text(3000, 4)
+    idx = kfmi_mod.Index.build(text, k=2, d=64, sa_rate=4)
+    idx.save_sa(tmp_path / "x.sa")
+    other = kfmi_mod.Index.from_image(idx.image())
+    assert other.sa()[0] == 0
+    other.load_sa(tmp_path / "x.sa")
+    rate, s = other.sa()
+    assert rate == 4 and np.array_equal(s, idx.sa()[1])
+    # a different text length is refused, a missing file reported
+    small = kfmi_mod.Index.build(_text(2999, 4), k=2, d=64)
+    with pytest.raises(kfmi_mod.KfmiError) as e:
+        small.load_sa(tmp_path / "x.sa")
+    assert e.value.code == 5
+    with pytest.raises(kfmi_mod.KfmiError) as e:
+        small.load_sa(tmp_path / "missing.sa")
+    assert e.value.code == 1
+    with pytest.raises(kfmi_mod.KfmiError):
+        small.save_sa(tmp_path / "y.sa")          # no samples to save
+
+
+def test_sa_rate_must_be_power_of_two(kfmi_mod):
+    for rate in (3, 6, 1 << 17):
+        with pytest.raises(kfmi_mod.KfmiError) as e:
+            kfmi_mod.Index.build(b"ACGTACGTAC", k=2, d=64, sa_rate=rate)
+        assert e.value.code == 33
+
+
+def test_locate_argument_errors_without_device(kfmi_mod):
+    idx = kfmi_mod.Index.build(_text(500, 5), k=2, d=64, sa_rate=4)
+    r = kfmi_mod.Results.alloc(4)
+    with pytest.raises(kfmi_mod.KfmiError) as e:
+        kfmi_mod.locate(idx, r)
+    assert e.value.code == 34                    # nothing on the device yet
+
+
+# ----------------------------------------------------------------- GPU ------
+
+def _expected(sa, res, max_occ=0):
+    offs, pos = [0], []
+    for q in range(res.size // 2):
+        L, R = int(res[2 * q]), int(res[2 * q + 1])
+        hi = R if not max_occ else min(R, L + max_occ)
+        rows = sa[L:hi] if hi > L else sa[:0]
+        pos.append(rows)
+        offs.append(offs[-1] + rows.size)
+    return np.array(offs, dtype=np.uint64), np.concatenate(pos).astype(np.uint32)
+
+
+def _reads(text, rng):
+    t = np.frombuffer(text, dtype=np.uint8)
+    n = len(t)
+    out = []
+    for m, cnt in ((2, 64), (4, 256), (6, 512), (12, 512), (100, 256)):
+        if m > n:
+            continue
+        st = rng.integers(0, n - m + 1, size=cnt)
+        reads = t[st[:, None] + np.arange(m)[None, :]]
+        # '$' edges: the text's own prefix and suffix of length m
+        edge = np.stack([t[:m], t[n - m:]])
+        rnd = rng.choice(ACGT, size=(cnt // 4, m))
+        out.append(np.concatenate([reads, edge, rnd]))
+    return out
+
+
+@pytest.fixture(scope="module")
+def gpu(kfmi_mod):
+    if kfmi_mod.device_count() < 1:
+        pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
+    kfmi_mod.set_device(0)
+    return kfmi_mod
+
+
+def _coop_ok(backend, k, d):
+    if not backend.startswith("coop"):
+        return True
+    bmw = 2 * (d // 32) * k
+    if backend == "coop-ac":
+        return k == 2 and bmw % 4 == 0
+    if backend == "coop":
+        return bmw % 4 == 0 and (bmw + 4 ** k) % 4 == 0
+    return bmw % 4 == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("backend", PLAIN + ALT)
+@pytest.mark.parametrize("k,d", [(2, 64), (1, 64), (2, 192), (1, 32)], ids=lambda x: str(x))
+def test_locate_equals_bruteforce_sa(gpu, backend, k, d):
+    if not _coop_ok(backend, k, d):
+        pytest.skip("geometry not offered by this cooperative backend")
+    text = _text(30_001, 100 * k + d)
+    sa = util.suffix_array(text + b"$")
+    rng = np.random.default_rng(k * d)
+    for rate in (1, 8, 64):
+        idx = gpu.Index.build(text, k=k, d=d, gpu=True, sa_rate=rate)
+        for q in _reads(text, rng):
+            if q.shape[1] % k:
+                continue
+            res, off, pos = gpu.locate_array(idx, q, backend)
+            w_off, w_pos = _expected(sa, res)
+            assert np.array_equal(off, w_off), (backend, k, d, rate, q.shape)
+            assert np.array_equal(pos, w_pos), (backend, k, d, rate, q.shape)
+        idx.close()
+
+
+@pytest.mark.gpu
+def test_locate_gpu_builder_samples_equal_host_builder(gpu):
+    for n in (1, 64, 65, 4097, 100_000):
+        text = _text(n, n)
+        for k, rate in ((2, 1), (2, 16), (1, 4)):
+            if n + 1 < k:
+                continue
+            a = gpu.Index.build(text, k=k, d=64, gpu=True, sa_rate=rate)
+            b = gpu.Index.build(text, k=k, d=64, gpu=False, sa_rate=rate)
+            assert a.image().tobytes() == b.image().tobytes()
+            assert np.array_equal(a.sa()[1], b.sa()[1]), (n, k, rate)
+
+
+@pytest.mark.gpu
+def test_locate_max_occ_repeats_and_empty(gpu):
+    # long runs: intervals of thousands of rows and long LF walks
+    text = b"A" * 3000 + b"C" + b"ACGT" * 700 + b"G"
+    sa = util.suffix_array(text + b"$")
+    idx = gpu.Index.build(text, k=2, d=64, gpu=True, sa_rate=32)
+    q = np.frombuffer(b"AAAA" + b"ACGT" + b"GGGG" + b"TACG", dtype=np.uint8).reshape(4, 4)
+    for max_occ in (0, 1, 7, 5000):
+        res, off, pos = gpu.locate_array(idx, q, "task-mid", max_occ=max_occ)
+        w_off, w_pos = _expected(sa, res, max_occ)
+        assert np.array_equal(off, w_off) and np.array_equal(pos, w_pos), max_occ
+    # every reported position really starts an occurrence
+    t = np.frombuffer(text, dtype=np.uint8)
+    res, off, pos = gpu.locate_array(idx, q, "task-mid")
+    for i in range(4):
+        for p in pos[off[i]:off[i + 1]]:
+            assert t[p:p + 4].tobytes() == q[i].tobytes()
+    # empty batch
+    res, off, pos = gpu.locate_array(idx, np.zeros((0, 4), dtype=np.uint8), "task-mid")
+    assert res.size == 0 and off.tolist() == [0] and pos.size == 0
+
+
+@pytest.mark.gpu
+def test_locate_errors(gpu):
+    text = _text(2000, 9)
+    idx = gpu.Index.build(text, k=2, d=64, gpu=True)          # no samples
+    q = gpu.Queries.from_array(np.frombuffer(text[:16], dtype=np.uint8).reshape(1, 16))
+    r = gpu.Results.alloc(1)
+    gpu.set_backend("task-mid")
+    gpu.transfer_to_gpu(idx, q, r)
+    gpu.search(idx, q, r)
+    with pytest.raises(gpu.KfmiError) as e:
+        gpu.locate(idx, r)
+    assert e.value.code == 33
+    # samples attached after the upload are picked up by the next locate
+    idx2 = gpu.Index.build(text, k=2, d=64, sa_rate=2)
+    import tempfile, os
+    with tempfile.TemporaryDirectory() as d:
+        idx2.save_sa(os.path.join(d, "s.sa"))
+        idx.load_sa(os.path.join(d, "s.sa"))
+    loc = gpu.locate(idx, r)
+    assert loc.total() == 1 and int(loc.positions()[0]) == 0
