@@ -214,7 +214,13 @@ def main():
     # ---- roofline: algorithmic bytes of the LF kernel ------------------------
     blocks = K.count_blocks(idx, q)
     b_lf = a.k * a.d // 4 + 4                               # bit planes of one block + one counter
-    bytes_alg = blocks * b_lf
+    # + what the LF kernel reads per query (ASCII row when packing is fused into
+    # the task kernel, else the packed code words) and the (L, R) it writes
+    spw = 16 // a.k
+    nwords = (a.qlen // a.k + spw - 1) // spw
+    fused = a.backend.startswith("task") and os.environ.get("KFMI_FUSED", "1") != "0" and nwords <= 16
+    q_in = a.qlen if fused else 4 * nwords
+    bytes_alg = blocks * b_lf + reads.shape[0] * (q_in + 8)
     lf_avg_ms = float(np.mean(lf_ms))
     achieved = bytes_alg / (lf_avg_ms / 1e3) / 1e9
     # HBM bytes per launch from the committed PMC profile of the same config
@@ -336,6 +342,7 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": "LF kernel (task/coop search), HIP-event average over the timed steps",
                          "bytes_per_launch": bytes_alg, "distinct_blocks": blocks, "bytes_per_block": b_lf,
+                         "bytes_per_query_io": q_in + 8,
                          "lf_ms": round(lf_avg_ms, 4), "pack_ms": round(float(np.mean(pack_ms)), 4),
                          "naive_bytes_per_launch": 2 * (a.qlen // a.k) * b_lf * a.queries,
                          "traffic_source": traffic_src,
