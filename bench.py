@@ -54,6 +54,8 @@ def parse():
     p.add_argument("--cpu-sample", type=int, default=2_000_000,
                    help="queries of the CPU-oracle baseline sample (0 = skip)")
     p.add_argument("--cpu-threads", type=int, default=0)
+    p.add_argument("--cpu-port-only", action="store_true",
+                   help="time only our restatement, not the reference's CPU binary (oracle/_ref)")
     p.add_argument("--variants", default="task,coop,task-ac,coop-ac,task-packed,coop-packed,task-mid,coop-mid",
                    help="other backends timed on rank 0 at N=1 (empty = none)")
     p.add_argument("--variant-steps", type=int, default=3)
@@ -117,6 +119,43 @@ def make_text(n: int) -> bytes:
     import random
     rng = random.Random(n)
     return rng.randbytes(n).translate(synth.TBL)
+
+
+def cpu_reference_baseline(idx, reads, ns, k, d, thr, res_gpu):
+    """The reference's own CPU searcher (common/searchQueries.c +
+    src/fmIndexCPUBaseline.c, compiled from /root/reference sources into
+    oracle/_ref by oracle/Makefile) on the first `ns` reads: its file interface
+    (tag-100 index file, multi-FASTA queries, 5 timed iterations, "TIME:" = mean
+    seconds per iteration, results in <index>.res.cpu).  None when the binary
+    for (k, d) is not there."""
+    import subprocess
+    import tempfile
+    binp = ROOT / "oracle" / "_ref" / f"cpu_{k}_{d}"
+    if not binp.exists():
+        return None
+    m = reads.shape[1]
+    with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
+        ip, qp = Path(td) / "index.fmi", Path(td) / "q.qry"
+        idx.image().tofile(ip)
+        rec = np.empty((ns, m + 4), dtype=np.uint8)
+        rec[:, :3] = np.frombuffer(b">r\n", dtype=np.uint8)
+        rec[:, 3:3 + m] = reads[:ns]
+        rec[:, -1] = 10
+        rec.tofile(qp)
+        env = dict(os.environ, OMP_NUM_THREADS=str(thr))
+        p = subprocess.run([str(binp), str(ip), str(qp), str(m), str(ns)], env=env, capture_output=True,
+                           text=True, timeout=900)
+        if p.returncode != 0 or "TIME:" not in p.stdout:
+            log(f"reference cpu baseline failed: rc={p.returncode} {p.stdout[-300:]} {p.stderr[-300:]}")
+            return None
+        t_iter = float(p.stdout.split("TIME:")[1].split()[0])
+        vals = np.array((Path(str(ip) + ".res.cpu")).read_bytes().split(), dtype=np.uint64)
+    ok = int(vals[0]) == ns and bool(np.array_equal(vals[1:].astype(np.uint32), res_gpu[:2 * ns]))
+    return {"value": round(ns / t_iter / 1e6, 4), "unit": "Mqueries/s", "cores": thr, "kind": "reference",
+            "sample": f"first {ns} of the same 10M reads; oracle/_ref/cpu_{k}_{d} = the reference's "
+                      f"searchQueries.c + fmIndexCPUBaseline.c built from its sources, OMP threads={thr}, "
+                      f"5 iterations, TIME {t_iter:.3f} s/iteration",
+            "parity_with_gpu": ok}
 
 
 def time_backend(idx, q, r, backend, steps, warmup):
@@ -313,10 +352,21 @@ def main():
             t = time.perf_counter()
             cres, _ = oracle.search(img, reads[:ns], nthreads=thr)
             cpu_s = time.perf_counter() - t
-            cpu = {"value": round(ns / cpu_s / 1e6, 4), "unit": "Mqueries/s", "cores": thr, "kind": "port",
-                   "sample": f"first {ns} of the same 10M reads, 1 pass, oracle/fmi_oracle.c "
-                             f"(restatement of fmIndexCPUBaseline.c), OMP threads={thr}, {cpu_s:.2f}s",
-                   "parity_with_gpu": bool(np.array_equal(cres, res[:2 * ns]))}
+            port = {"value": round(ns / cpu_s / 1e6, 4), "unit": "Mqueries/s", "cores": thr, "kind": "port",
+                    "sample": f"first {ns} of the same 10M reads, 1 pass, oracle/fmi_oracle.c "
+                              f"(restatement of fmIndexCPUBaseline.c), OMP threads={thr}, {cpu_s:.2f}s",
+                    "parity_with_gpu": bool(np.array_equal(cres, res[:2 * ns]))}
+            log(f"cpu baseline (port) {port}")
+            cpu = None
+            if not a.cpu_port_only:
+                try:
+                    cpu = cpu_reference_baseline(idx, reads, ns, a.k, a.d, thr, res)
+                except Exception as e:          # the reference binary is a baseline, never the product
+                    log(f"reference cpu baseline unavailable: {e}")
+            if cpu is None:
+                cpu = port
+            else:
+                extra["cpu_port"] = port
             log(f"cpu baseline {cpu}")
 
     if D.rank == 0:
