@@ -56,7 +56,8 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=0)
     p.add_argument("--cpu-port-only", action="store_true",
                    help="time only our restatement, not the reference's CPU binary (oracle/_ref)")
-    p.add_argument("--variants", default="task,coop,task-ac,coop-ac,task-packed,coop-packed,task-mid,coop-mid",
+    p.add_argument("--variants", default="task,coop,task-ac,coop-ac,task-ac128,coop-ac128,task-packed,coop-packed,"
+                                         "task-mid,coop-mid",
                    help="other backends timed on rank 0 at N=1 (empty = none)")
     p.add_argument("--variant-steps", type=int, default=3)
     p.add_argument("--no-md5", action="store_true")

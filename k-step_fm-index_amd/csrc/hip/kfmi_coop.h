@@ -34,7 +34,7 @@ struct CoopCfg {
   static constexpr int WPB0 = 65536 / WAVE_LDS;
   static constexpr int WPB = WPB0 < 1 ? 1 : (WPB0 > 4 ? 4 : WPB0);   // waves per block
   static constexpr bool OK = (G::BMW % 4 == 0) && (G::EW % 4 == 0) && (G::BOFF % 4 == 0) &&
-                             (G::LAY != LAY_AC || G::HALF >= 4) && (G::LAY != LAY_MID || G::NC >= 4) &&
+                             (!G::ACRULE || G::HALF >= 4) && (G::LAY != LAY_MID || G::NC >= 4) &&
                              TPR <= 64;
 };
 
@@ -49,6 +49,11 @@ __device__ __forceinline__ const uint8_t* coop_chunk_addr(const IdxArgs& ix, uin
     const uint64_t lb = (uint64_t) (b >> 1) * (G::EW * 4);
     if (k < C::BC) return base + lb + ((b & 1u) * G::BMW + 4 * k) * 4;
     return base + lb + (G::MIDCNT + (c & ~3u)) * 4;
+  }
+  if constexpr (G::LAY == LAY_AC128) {
+    if (k < C::BC) return base + eb + 4 * k * 4;
+    const bool e = ((b & 1u) != 0) == (c < (uint32_t) G::HALF);
+    return base + eb + (G::BMW + (e ? G::HALF : 0) + ((c & (G::HALF - 1)) & ~3u)) * 4;
   }
   if (k < C::BC) return base + eb + (G::BOFF + 4 * k) * 4;
   if constexpr (G::LAY == LAY_INTER) {
@@ -68,7 +73,7 @@ __device__ __forceinline__ uint32_t coop_lf(const IdxArgs& ix, const uint8_t* sl
   using C = CoopCfg<G>;
   const int o = (int) (X - b * (uint32_t) G::D);
   bool e = false;
-  if constexpr (G::LAY == LAY_AC) e = ((b & 1u) != 0) == (c < (uint32_t) G::HALF);
+  if constexpr (G::ACRULE) e = ((b & 1u) != 0) == (c < (uint32_t) G::HALF);
   if constexpr (G::LAY == LAY_MID) e = (b & 1u) == 0;
   uint32_t pop = 0;
 #pragma unroll

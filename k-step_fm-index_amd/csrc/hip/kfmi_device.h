@@ -22,6 +22,11 @@
  *                searched backward (e = 1) and an odd block forward from the SAME
  *                line.  K=2, d=64: one 128-byte line per LF and nothing else --
  *                the AltCounters idea packed into one 128-B HBM request.
+ *   LAY_AC128  : tag-201 (AltCounters) semantics, one power-of-two line per
+ *                d-block: [planes of block b | cnt_half_b | cnt_half_{b+1}],
+ *                so both counters the AC rule may pick (entry b or b+1,
+ *                fmIndexCPUBaseline-AltCounters.c:218-225) sit in the block's
+ *                own line.  K=2, d=64: 96 B in a 128-B line, one request per LF.
  */
 #ifndef KFMI_DEVICE_H_
 #define KFMI_DEVICE_H_
@@ -31,7 +36,7 @@
 
 namespace kfmi {
 
-enum Layout : int { LAY_INTER = 0, LAY_AC = 1, LAY_PACKED = 2, LAY_MID = 3 };
+enum Layout : int { LAY_INTER = 0, LAY_AC = 1, LAY_PACKED = 2, LAY_MID = 3, LAY_AC128 = 4 };
 
 __host__ __device__ constexpr int pow2ceil(int x) { int p = 1; while (p < x) p <<= 1; return p; }
 
@@ -49,13 +54,15 @@ struct Geo {
   static constexpr int EW = LAY == LAY_INTER ? BMW + NC
                           : LAY == LAY_AC    ? HALF + BMW
                           : LAY == LAY_PACKED ? pow2ceil(BMW + NC / 2)
+                          : LAY == LAY_AC128  ? pow2ceil(BMW + NC)
                           : pow2ceil(2 * BMW + NC);
   static constexpr int BOFF = LAY == LAY_AC ? HALF : 0;   // first bitmap word
   static constexpr int DELTA16 = 2 * BMW;                 // first u16 delta (packed)
   static constexpr int MIDCNT = 2 * BMW;                  // first mid counter (mid)
+  static constexpr bool ACRULE = LAY == LAY_AC || LAY == LAY_AC128;   // AltCounters direction rule
   static constexpr int SPW = 32 / (2 * K);                // K-steps per packed query word
   static constexpr bool SMALL = BMW <= 16;                // whole bitmap fits in registers
-  static constexpr bool TWO_SIDED = LAY == LAY_AC || LAY == LAY_MID;
+  static constexpr bool TWO_SIDED = LAY == LAY_AC || LAY == LAY_MID || LAY == LAY_AC128;
 };
 
 // Superblock shift of the packed layout: the largest S with (2^S - 1) * d <= 65535.
@@ -249,6 +256,11 @@ __device__ __forceinline__ Where<G> locate(const IdxArgs& ix, uint32_t b, uint32
     w.e = ((b & 1u) != 0) == (c < (uint32_t) G::HALF);
     w.planes = ent + G::BOFF;
     w.cnt = ix.ent + (uint64_t) (b + (w.e ? 1u : 0u)) * G::EW + (c & (G::HALF - 1));
+  } else if constexpr (G::LAY == LAY_AC128) {
+    const uint32_t* line = ix.ent + (uint64_t) b * G::EW;
+    w.e = ((b & 1u) != 0) == (c < (uint32_t) G::HALF);
+    w.planes = line;
+    w.cnt = line + G::BMW + (w.e ? G::HALF : 0) + (c & (G::HALF - 1));
   } else if constexpr (G::LAY == LAY_PACKED) {
     const uint32_t* ent = ix.ent + (uint64_t) b * G::EW;
     w.planes = ent;

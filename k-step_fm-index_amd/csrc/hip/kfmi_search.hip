@@ -31,7 +31,8 @@ using namespace kfmi;
 /* ------------------------------------------------------------------------ */
 
 static const char* kBackendNames[KFMI_BK_COUNT] = {
-    "task", "coop", "task-ac", "coop-ac", "task-packed", "coop-packed", "task-mid", "coop-mid"};
+    "task", "coop", "task-ac", "coop-ac", "task-packed", "coop-packed", "task-mid", "coop-mid",
+    "task-ac128", "coop-ac128"};
 
 static thread_local int t_backend = -1;
 static thread_local int t_device = -1;
@@ -63,7 +64,8 @@ extern "C" kfmi_backend_t kfmi_backend(void)
 
 extern "C" uint32_t kfmi_backend_tag(kfmi_backend_t b)
 {
-  return (b == KFMI_BK_TASK_AC || b == KFMI_BK_COOP_AC) ? 201u : 101u;
+  return (b == KFMI_BK_TASK_AC || b == KFMI_BK_COOP_AC || b == KFMI_BK_TASK_AC128 || b == KFMI_BK_COOP_AC128)
+             ? 201u : 101u;
 }
 
 extern "C" int32_t kfmi_set_backend(const char* name)
@@ -400,6 +402,29 @@ __global__ __launch_bounds__(256) void build_mid_kernel(const uint32_t* __restri
   for (int i = GM::MIDCNT + GI::NC; i < GM::EW; ++i) dst[i] = 0;
 }
 
+/* AC128 layout construction from tag-201 entries (E + 1 of them, the last
+ * being the sentinel): line b = [planes of b | cnt_half_b | cnt_half_{b+1}],
+ * the counters of entries past the sentinel read as 0 (as the AC backend's
+ * zero padding entries do).  Lines 0 .. E plus one padding line. */
+template <int K, int NB>
+__global__ __launch_bounds__(256) void build_ac128_kernel(const uint32_t* __restrict__ ac, uint32_t nent,
+                                                          uint32_t nlines, uint32_t* __restrict__ lines)
+{
+  using GA = Geo<K, NB, LAY_AC>;
+  using GL = Geo<K, NB, LAY_AC128>;
+  const uint64_t b = (uint64_t) blockIdx.x * 256 + threadIdx.x;
+  if (b >= nlines) return;
+  uint32_t* dst = lines + b * GL::EW;
+  const uint32_t* src = ac + b * GA::EW;
+  const uint32_t* nxt = ac + (b + 1) * GA::EW;
+  for (int i = 0; i < GA::BMW; ++i) dst[i] = b < nent ? src[GA::BOFF + i] : 0u;
+  for (int c = 0; c < GA::HALF; ++c) {
+    dst[GA::BMW + c] = b < nent ? src[c] : 0u;
+    dst[GA::BMW + GA::HALF + c] = b + 1 < nent ? nxt[c] : 0u;
+  }
+  for (int i = GA::BMW + 2 * GA::HALF; i < GL::EW; ++i) dst[i] = 0;
+}
+
 /* ------------------------------------------------------------------------ */
 /* dispatch tables                                                          */
 /* ------------------------------------------------------------------------ */
@@ -533,6 +558,8 @@ static hipError_t dispatch(Op op, uint32_t K, uint32_t nb, int lay, const Search
   KFMI_FOR_NB(KFMI_CASE, 2, LAY_PACKED)
   KFMI_FOR_NB(KFMI_CASE, 1, LAY_MID)
   KFMI_FOR_NB(KFMI_CASE, 2, LAY_MID)
+  KFMI_FOR_NB(KFMI_CASE, 1, LAY_AC128)
+  KFMI_FOR_NB(KFMI_CASE, 2, LAY_AC128)
 #undef KFMI_CASE
   return hipErrorInvalidValue;
 }
@@ -542,9 +569,7 @@ static hipError_t dispatch(Op op, uint32_t K, uint32_t nb, int lay, const Search
 static bool geometry_supported(int backend, uint32_t K, uint32_t nb, int lay)
 {
   if (!nb_supported(nb) || (K != 1 && K != 2)) return false;
-  if (backend != KFMI_BK_COOP && backend != KFMI_BK_COOP_AC && backend != KFMI_BK_COOP_PACKED &&
-      backend != KFMI_BK_COOP_MID)
-    return true;
+  if (!is_coop(backend)) return true;
 #define KFMI_OKC(KK, NBV, LAYV) \
   if (K == KK && nb == NBV && lay == LAYV) return CoopCfg<Geo<KK, NBV, LAYV>>::OK;
   KFMI_FOR_NB(KFMI_OKC, 1, LAY_INTER)
@@ -555,6 +580,8 @@ static bool geometry_supported(int backend, uint32_t K, uint32_t nb, int lay)
   KFMI_FOR_NB(KFMI_OKC, 2, LAY_PACKED)
   KFMI_FOR_NB(KFMI_OKC, 1, LAY_MID)
   KFMI_FOR_NB(KFMI_OKC, 2, LAY_MID)
+  KFMI_FOR_NB(KFMI_OKC, 1, LAY_AC128)
+  KFMI_FOR_NB(KFMI_OKC, 2, LAY_AC128)
 #undef KFMI_OKC
   return false;
 }
@@ -592,12 +619,28 @@ static hipError_t dispatch_build_mid(uint32_t K, uint32_t nb, const uint32_t* in
   return hipErrorInvalidValue;
 }
 
+static hipError_t dispatch_build_ac128(uint32_t K, uint32_t nb, const uint32_t* ac, uint32_t nent, uint32_t nlines,
+                                       uint32_t* lines, hipStream_t st)
+{
+  const uint32_t blocks = (nlines + 255) / 256;
+#define KFMI_BA(KK, NBV, LAYV)                                                                          \
+  if (K == KK && nb == NBV) {                                                                           \
+    hipLaunchKernelGGL((build_ac128_kernel<KK, NBV>), dim3(blocks), dim3(256), 0, st, ac, nent, nlines, lines); \
+    return hipGetLastError();                                                                           \
+  }
+  KFMI_FOR_NB(KFMI_BA, 1, 0)
+  KFMI_FOR_NB(KFMI_BA, 2, 0)
+#undef KFMI_BA
+  return hipErrorInvalidValue;
+}
+
 static int layout_of(int backend)
 {
   switch (backend) {
     case KFMI_BK_TASK: case KFMI_BK_COOP: return LAY_INTER;
     case KFMI_BK_TASK_AC: case KFMI_BK_COOP_AC: return LAY_AC;
     case KFMI_BK_TASK_MID: case KFMI_BK_COOP_MID: return LAY_MID;
+    case KFMI_BK_TASK_AC128: case KFMI_BK_COOP_AC128: return LAY_AC128;
     default: return LAY_PACKED;
   }
 }
@@ -605,7 +648,7 @@ static int layout_of(int backend)
 static bool is_coop(int backend)
 {
   return backend == KFMI_BK_COOP || backend == KFMI_BK_COOP_AC || backend == KFMI_BK_COOP_PACKED ||
-         backend == KFMI_BK_COOP_MID;
+         backend == KFMI_BK_COOP_MID || backend == KFMI_BK_COOP_AC128;
 }
 
 /* ------------------------------------------------------------------------ */
@@ -658,7 +701,7 @@ static int32_t host_entries_for(const kfmi_fmi_t* f, int lay, kfmi_fmi_t** owned
     }
     return KFMI_INDEX_VER_INTERLEAVE;   /* an AC file cannot feed a plain-counter backend */
   }
-  /* AC */
+  /* AC, AC128 */
   if (f->tag == 201) return KFMI_SUCCESS;
   kfmi_fmi_t* t100 = nullptr;
   const kfmi_fmi_t* src100 = f;
@@ -783,6 +826,24 @@ static int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx)
             hipSuccess ||
         hipStreamSynchronize(ctx->st) != hipSuccess)
       return fail(KFMI_E_KERNEL);
+  } else if (lay == LAY_AC128) {
+    /* one line per tag-201 entry (sentinel included) + one padding line, built on
+     * the device from the entries; padding entry b+1 of the sentinel reads 0 */
+    const uint32_t E = src->nentries;                 /* tag-201 entries incl. the sentinel */
+    const uint32_t nl = E + 1;
+    const uint32_t lw = (uint32_t) pow2ceil((int) (2 * f->nbitmaps * f->steps + nc));
+    uint32_t* tmp = nullptr;
+    di->ent_bytes = 4ull * lw * nl;
+    if (hipMalloc((void**) &tmp, body + 16) != hipSuccess) return fail(KFMI_E_DEVICE_ALLOC);
+    if (hipMalloc((void**) &di->ent, di->ent_bytes) != hipSuccess) {
+      (void) hipFree(tmp);
+      return fail(KFMI_E_DEVICE_ALLOC);
+    }
+    bool ok = hipMemcpyAsync(tmp, src->h_index, body, hipMemcpyHostToDevice, ctx->st) == hipSuccess &&
+              dispatch_build_ac128(f->steps, f->nbitmaps, tmp, E, nl, di->ent, ctx->st) == hipSuccess &&
+              hipStreamSynchronize(ctx->st) == hipSuccess;
+    (void) hipFree(tmp);
+    if (!ok) return fail(KFMI_E_KERNEL);
   } else if (lay == LAY_MID) {
     /* MID: pairs of blocks per line, built on the device from tag-101 entries;
      * counters of the last line (odd block count) and of one padding line are

@@ -17,6 +17,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <stdint.h>
+#include <string.h>
 
 #define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
 
@@ -117,7 +118,36 @@ int main(int argc, char** argv)
   const uint64_t bytes = (uint64_t) (gb * 1e9) & ~(uint64_t) 127;
   uint4* t;
   uint32_t* sink;
-  CHECK(hipMalloc(&t, bytes));
+  /* PROBE_ALLOC: default (hipMalloc) | contig (hipDeviceMallocContiguous) |
+   * vmm (hipMemCreate + 1 GiB-aligned hipMemAddressReserve) -- translation reach */
+  const char* mode = getenv("PROBE_ALLOC") ? getenv("PROBE_ALLOC") : "default";
+  if (!strcmp(mode, "contig")) {
+    CHECK(hipExtMallocWithFlags((void**) &t, bytes, hipDeviceMallocContiguous));
+  } else if (!strcmp(mode, "vmm")) {
+    hipMemAllocationProp prop = {};
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = 0;
+    size_t gmin = 0, grec = 0;
+    CHECK(hipMemGetAllocationGranularity(&gmin, &prop, hipMemAllocationGranularityMinimum));
+    CHECK(hipMemGetAllocationGranularity(&grec, &prop, hipMemAllocationGranularityRecommended));
+    const size_t g = grec > gmin ? grec : gmin;
+    const size_t sz = (bytes + g - 1) / g * g;
+    hipMemGenericAllocationHandle_t h;
+    CHECK(hipMemCreate(&h, sz, &prop, 0));
+    void* va = nullptr;
+    CHECK(hipMemAddressReserve(&va, sz, 1ull << 30, nullptr, 0));
+    CHECK(hipMemMap(va, sz, 0, h, 0));
+    hipMemAccessDesc acc = {};
+    acc.location = prop.location;
+    acc.flags = hipMemAccessFlagsProtReadWrite;
+    CHECK(hipMemSetAccess(va, sz, &acc, 1));
+    t = (uint4*) va;
+    printf("{\"vmm_granularity_min\": %zu, \"recommended\": %zu}\n", gmin, grec);
+  } else {
+    CHECK(hipMalloc(&t, bytes));
+  }
+  printf("{\"alloc\": \"%s\"}\n", mode);
   CHECK(hipMalloc(&sink, 4));
   CHECK(hipMemset(t, 0x5a, bytes));
   hipEvent_t e0, e1;
@@ -167,6 +197,6 @@ int main(int argc, char** argv)
     printf("{\"table_bytes\": %llu}\n", (unsigned long long) sb);
     run("indep", 64, [&] { hipLaunchKernelGGL((k_indep<64>), grid, blk, 0, 0, t, sb / 64, pt, sink); }, (double) pt * threads);
   }
-  CHECK(hipFree(t));
+  if (strcmp(mode, "vmm")) CHECK(hipFree(t));
   return 0;
 }

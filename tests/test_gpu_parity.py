@@ -15,7 +15,7 @@ from util import GOLDEN, manifest, read_qry
 pytestmark = pytest.mark.gpu
 
 PLAIN = ("task", "coop", "task-packed", "coop-packed", "task-mid", "coop-mid")
-ALT = ("task-ac", "coop-ac")
+ALT = ("task-ac", "coop-ac", "task-ac128", "coop-ac128")
 
 
 def coop_supported(backend, k, d):
@@ -24,7 +24,7 @@ def coop_supported(backend, k, d):
         return True
     nb = d // 32
     bmw = 2 * nb * k
-    if backend == "coop-ac":
+    if backend in ("coop-ac", "coop-ac128"):
         return k == 2 and bmw % 4 == 0
     if backend == "coop":
         return bmw % 4 == 0 and (bmw + 4 ** k) % 4 == 0

@@ -26,7 +26,7 @@ def setup(kfmi_mod):
     return K, idx, reads
 
 
-@pytest.mark.parametrize("backend", ["task-mid", "coop-mid", "task", "coop-ac"])
+@pytest.mark.parametrize("backend", ["task-mid", "coop-mid", "task", "coop-ac", "task-ac128"])
 @pytest.mark.parametrize("chunk", [0, 1_000, 4_099])
 def test_stream_equals_batch_and_oracle(setup, oracle_mod, backend, chunk):
     K, idx, reads = setup
