@@ -57,7 +57,7 @@ def parse():
     p.add_argument("--cpu-port-only", action="store_true",
                    help="time only our restatement, not the reference's CPU binary (oracle/_ref)")
     p.add_argument("--variants", default="task,coop,task-ac,coop-ac,task-ac128,coop-ac128,task-packed,coop-packed,"
-                                         "task-mid,coop-mid",
+                                         "task-mid,coop-mid,task-mid+ftab14",
                    help="other backends timed on rank 0 at N=1 (empty = none)")
     p.add_argument("--variant-steps", type=int, default=3)
     p.add_argument("--no-md5", action="store_true")
@@ -160,7 +160,10 @@ def cpu_reference_baseline(idx, reads, ns, k, d, thr, res_gpu):
 
 
 def time_backend(idx, q, r, backend, steps, warmup):
-    K.set_backend(backend)
+    """`backend` may carry "+ftabN": the Bowtie-style jump-start table of N bases."""
+    name, _, opt = backend.partition("+")
+    K.set_backend(name)
+    K.set_ftab(int(opt[4:]) if opt.startswith("ftab") else 0)
     K.transfer_to_gpu(idx, q, r)
     for _ in range(warmup):
         K.search(idx, q, r)
@@ -173,6 +176,7 @@ def time_backend(idx, q, r, backend, steps, warmup):
         tot.append(t["total_ms"])
     wall = time.perf_counter() - t0
     K.transfer_to_cpu(r)
+    K.set_ftab(0)
     return wall, float(np.mean(lf)), float(np.mean(tot))
 
 

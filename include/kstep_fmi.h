@@ -132,6 +132,13 @@ int32_t     kfmi_device_count(void);
 int32_t     kfmi_last_error(void);
 /* searchIndexGPU with a status return. */
 int32_t     kfmi_search(void *index, void *queries, void *results);
+/* ftab (Bowtie-style jump start; not in the reference): the task backends look
+ * up [L, R) after the first `bases` bases of each query in a table of all
+ * 4^bases codes (8 B each: 134 MB at 12) built on the device with the search's
+ * own LF steps, then continue from there -- results are unchanged.  0 = off
+ * (default; KFMI_FTAB sets it process-wide), at most 16, a multiple of K to
+ * take effect; per calling thread like the backend. */
+int32_t     kfmi_set_ftab(uint32_t bases);
 /* Device-side timing of the last search, from HIP events on the library's
  * stream: total (pack + LF), query packing, and the LF kernel alone (ms). */
 int32_t     kfmi_last_timing(double *ms_total, double *ms_pack, double *ms_lf);

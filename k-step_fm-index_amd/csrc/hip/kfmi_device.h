@@ -85,6 +85,10 @@ struct IdxArgs {
   uint32_t bwtsize;
   uint32_t nt_from;                   // K-steps >= nt_from load index lines non-temporally
   DollarArgs dl;
+  // ftab (Bowtie-style jump start): [L, R) after the first ftab_steps K-steps,
+  // indexed by the low 2*K*ftab_steps bits of the query's code stream; null = off
+  const uint2* __restrict__ ftab;
+  uint32_t ftab_steps, ftab_mask;
 };
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));

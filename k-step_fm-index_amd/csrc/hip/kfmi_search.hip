@@ -38,6 +38,7 @@ static thread_local int t_backend = -1;
 static thread_local int t_device = -1;
 static thread_local int32_t t_last_error = KFMI_SUCCESS;
 static thread_local double t_ms[3] = {0, 0, 0};
+static thread_local int t_ftab = -1;   /* ftab bases for the task kernels; -1: KFMI_FTAB, else 0 */
 
 static int backend_from_name(const char* n)
 {
@@ -103,6 +104,21 @@ extern "C" int32_t kfmi_set_device(int32_t device)
 }
 
 extern "C" void kfmi_set_last_error(int32_t e) { t_last_error = e; }
+
+extern "C" int32_t kfmi_set_ftab(uint32_t bases)
+{
+  if (bases > 16) return KFMI_E_BAD_ARGUMENT;
+  t_ftab = (int) bases;
+  return KFMI_SUCCESS;
+}
+
+static uint32_t ftab_bases(void)
+{
+  if (t_ftab >= 0) return (uint32_t) t_ftab;
+  const char* e = getenv("KFMI_FTAB");
+  const int v = e ? atoi(e) : 0;
+  return v > 0 && v <= 16 ? (uint32_t) v : 0u;
+}
 extern "C" int32_t kfmi_last_error(void) { return t_last_error; }
 
 extern "C" int32_t kfmi_last_timing(double* ms_total, double* ms_pack, double* ms_lf)
@@ -165,6 +181,8 @@ struct kfmi_dev_index {
   uint32_t* sa = nullptr;      /* locate: row-sampled suffix array */
   uint64_t sa_bytes = 0;
   uint32_t sa_log2 = 0, sa_gen = 0;
+  uint2* ftab = nullptr;       /* jump-start table of ftab_chars bases (0 = none) */
+  uint32_t ftab_chars = 0;
 };
 
 struct kfmi_dev_queries {
@@ -252,6 +270,19 @@ __global__ __launch_bounds__(256) void task_kernel(IdxArgs ix, const uint32_t* _
     L[i] = 0;
     R[i] = ix.bwtsize;
   }
+  uint32_t skip = 0;
+  if (ix.ftab && steps >= ix.ftab_steps) {   /* wave-uniform: jump start from the ftab */
+    skip = ix.ftab_steps;
+#pragma unroll
+    for (int i = 0; i < QPT; ++i) {
+      uint32_t w0;
+      if constexpr (MAXW > 0) w0 = cw[i][0];
+      else w0 = qp[q[i]];
+      const uint2 lr = ix.ftab[w0 & ix.ftab_mask];
+      L[i] = lr.x;
+      R[i] = lr.y;
+    }
+  }
   for (uint32_t w = 0; w < nwords; ++w) {
     uint32_t word[QPT];
 #pragma unroll
@@ -268,6 +299,7 @@ __global__ __launch_bounds__(256) void task_kernel(IdxArgs ix, const uint32_t* _
 #pragma unroll
     for (int j = 0; j < SPW; ++j) {
       if ((uint32_t) j >= left) continue;   /* only the last word is partial (wave-uniform) */
+      if (w * SPW + j < skip) continue;      /* steps covered by the ftab (wave-uniform) */
       uint32_t c[QPT];
 #pragma unroll
       for (int i = 0; i < QPT; ++i) c[i] = (word[i] >> (2 * G::K * j)) & (uint32_t) (G::NC - 1);
@@ -315,6 +347,25 @@ __global__ __launch_bounds__(256) void task_kernel(IdxArgs ix, const uint32_t* _
     const uint64_t qi = base + (uint64_t) i * 256;
     if (qi < num) *reinterpret_cast<uint2*>(res + 2 * qi) = make_uint2(L[i], R[i]);
   }
+}
+
+/* ftab construction: [L, R) of every code stream v of ftab_steps K-steps
+ * (the search's own first steps, from [0, n+1)). */
+template <class G>
+__global__ __launch_bounds__(256) void ftab_build_kernel(IdxArgs ix, uint32_t fsteps, uint64_t n,
+                                                         uint2* __restrict__ out)
+{
+  const uint64_t v = (uint64_t) blockIdx.x * 256 + threadIdx.x;
+  if (v >= n) return;
+  uint32_t L = 0, R = ix.bwtsize;
+  for (uint32_t t = 0; t < fsteps; ++t) {
+    const uint32_t c = (uint32_t) (v >> (2 * G::K * t)) & (uint32_t) (G::NC - 1);
+    uint32_t sx[2 * G::K];
+    plane_xor<G::K>(c, sx);
+    L = lf_stream<G>(ix, L, c, sx);
+    R = lf_stream<G>(ix, R, c, sx);
+  }
+  out[v] = make_uint2(L, R);
 }
 
 /* distinct d-blocks touched per step (1 if L/d == R/d else 2): the
@@ -446,6 +497,10 @@ struct SearchLaunch {
   const uint32_t* owner;
   uint64_t total;
   uint32_t* pos;
+  /* ftab build */
+  uint2* ftab_out;
+  uint32_t ftab_steps;
+  uint64_t ftab_n;
 };
 
 static int task_qpt(void)
@@ -531,7 +586,15 @@ static hipError_t launch_locate(const SearchLaunch& a)
   return hipGetLastError();
 }
 
-enum class Op { Task, Coop, Count, Locate };
+template <class G>
+static hipError_t launch_ftab(const SearchLaunch& a)
+{
+  hipLaunchKernelGGL((ftab_build_kernel<G>), dim3((uint32_t) ((a.ftab_n + 255) / 256)), dim3(256), 0, a.st, a.ix,
+                     a.ftab_steps, a.ftab_n, a.ftab_out);
+  return hipGetLastError();
+}
+
+enum class Op { Task, Coop, Count, Locate, Ftab };
 
 template <int K, int NB, int LAY>
 static hipError_t dispatch_one(Op op, const SearchLaunch& a, unsigned long long* d_total)
@@ -541,6 +604,7 @@ static hipError_t dispatch_one(Op op, const SearchLaunch& a, unsigned long long*
     case Op::Task: return launch_task<G>(a);
     case Op::Coop: return launch_coop<G>(a);
     case Op::Locate: return launch_locate<G>(a);
+    case Op::Ftab: return launch_ftab<G>(a);
     default: return launch_count<G>(a, d_total);
   }
 }
@@ -753,6 +817,7 @@ static void free_dev_index(kfmi_dev_index* di)
   if (di->ent) (void) hipFree(di->ent);
   if (di->sb) (void) hipFree(di->sb);
   if (di->sa) (void) hipFree(di->sa);
+  if (di->ftab) (void) hipFree(di->ftab);
   delete di;
 }
 
@@ -936,7 +1001,46 @@ static IdxArgs idx_args(const kfmi_dev_index* di)
   const char* e = getenv("KFMI_NT_FROM");   /* K-step from which index loads are non-temporal */
   ix.nt_from = e ? (uint32_t) atoi(e) : 0xFFFFFFFFu;
   ix.dl = di->dl;
+  ix.ftab = nullptr;
+  ix.ftab_steps = 0;
+  ix.ftab_mask = 0;
   return ix;
+}
+
+/* The ftab of `bases` bases for a task backend, (re)built on the device from the
+ * uploaded layout with the search's own LF steps; sets ix.ftab (null when off,
+ * for coop backends, or when bases is not a multiple of K). */
+static int32_t use_ftab(kfmi_dev_index* di, DevCtx* ctx, IdxArgs& ix)
+{
+  ix.ftab = nullptr;
+  ix.ftab_steps = 0;
+  ix.ftab_mask = 0;
+  const uint32_t bases = ftab_bases();
+  if (!bases || is_coop(di->backend) || bases % di->K) return KFMI_SUCCESS;
+  if (di->ftab_chars != bases) {
+    if (di->ftab) (void) hipFree(di->ftab);
+    di->ftab = nullptr;
+    di->ftab_chars = 0;
+    const uint64_t n = 1ull << (2 * bases);
+    if (hipMalloc((void**) &di->ftab, 8 * n) != hipSuccess) {
+      di->ftab = nullptr;
+      return KFMI_E_DEVICE_ALLOC;
+    }
+    SearchLaunch a{};
+    a.st = ctx->st;
+    a.ix = idx_args(di);
+    a.ftab_out = di->ftab;
+    a.ftab_steps = bases / di->K;
+    a.ftab_n = n;
+    if (dispatch(Op::Ftab, di->K, di->nb, di->layout, a) != hipSuccess ||
+        hipStreamSynchronize(ctx->st) != hipSuccess)
+      return KFMI_E_KERNEL;
+    di->ftab_chars = bases;
+  }
+  ix.ftab = di->ftab;
+  ix.ftab_steps = bases / di->K;
+  ix.ftab_mask = bases >= 16 ? 0xFFFFFFFFu : (1u << (2 * bases)) - 1u;
+  return KFMI_SUCCESS;
 }
 
 static void free_dev_queries(kfmi_dev_queries* dq)
@@ -1043,9 +1147,11 @@ extern "C" int32_t kfmi_search(void* index, void* queries, void* results)
   int32_t err = ctx_for(di->device, &ctx);
   if (err) return err;
 
-  SearchLaunch a;
+  SearchLaunch a{};
   a.st = ctx->st;
   a.ix = idx_args(di);
+  err = use_ftab(di, ctx, a.ix);
+  if (err) return err;
   a.qp = dq->packed;
   a.ascii = dq->ascii;
   a.m = dq->size;
@@ -1489,7 +1595,9 @@ extern "C" int32_t kfmi_search_stream(void* index, const char* ascii, uint64_t n
   }
   const auto t0 = std::chrono::steady_clock::now();
   const Op op = is_coop(di->backend) ? Op::Coop : Op::Task;
-  const IdxArgs ix = idx_args(di);
+  IdxArgs ix = idx_args(di);
+  err = use_ftab(di, ctx, ix);
+  if (err) return err;
   int32_t status = KFMI_SUCCESS;
   auto retire = [&](StreamSlot& s) {
     if (!s.busy) return;

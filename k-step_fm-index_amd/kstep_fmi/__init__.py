@@ -100,6 +100,7 @@ def load() -> ctypes.CDLL:
         "kfmi_host_free": (i32, [vp]),
         "kfmi_stream_release": (i32, []),
         "kfmi_build_index_ex": (i32, [vp, u64, u32, u32, u32, i32, pvp]),
+        "kfmi_set_ftab": (i32, [u32]),
         "kfmi_index_sa": (i32, [vp, pvp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32)]),
         "kfmi_save_sa": (i32, [ctypes.c_char_p, vp]),
         "kfmi_load_sa": (i32, [ctypes.c_char_p, vp]),
@@ -134,6 +135,11 @@ def set_backend(name: str) -> None:
 
 def get_backend() -> str:
     return load().kfmi_get_backend().decode()
+
+
+def set_ftab(bases: int) -> None:
+    """Bowtie-style jump-start table of `bases` bases for the task backends (0 = off)."""
+    _check(load().kfmi_set_ftab(int(bases)), f"set_ftab({bases})")
 
 
 def set_device(dev: int) -> None:

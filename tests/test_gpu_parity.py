@@ -204,3 +204,26 @@ def test_b5_boundary_against_bruteforce(gpu, n):
                 if not coop_supported(b, k, d):
                     continue
                 assert np.array_equal(gpu.search_array(idx, q, b), want), (n, k, d, m, b)
+
+
+@pytest.mark.parametrize("bases", [2, 8, 12])
+@pytest.mark.parametrize("backend", ["task-mid", "task", "task-packed", "task-ac", "task-ac128"])
+def test_ftab_jump_start_equals_oracle(gpu, oracle_mod, random_index, backend, bases):
+    """The ftab replaces the first bases/K LF steps by a table built with the
+    same LF steps: results must not change (reads shorter than the table keep
+    the plain path)."""
+    text, idxs = random_index
+    gpu.set_ftab(bases)
+    try:
+        for k, d in ((2, 64), (1, 64), (2, 192)):
+            idx = idxs[(k, d)]
+            ref_img = idx.alt_counters()[0].image() if backend in ALT else idx.image()
+            for m, n in ((100, 6000), (150, 1500), (bases, 800), (2 * k, 300)):
+                if m % k:
+                    continue
+                q = _reads(text, n, m, seed=m + 31 * k + bases)
+                want, _ = oracle_mod.search(ref_img, q)
+                got = gpu.search_array(idx, q, backend)
+                assert np.array_equal(got, want), (backend, bases, k, d, m)
+    finally:
+        gpu.set_ftab(0)
