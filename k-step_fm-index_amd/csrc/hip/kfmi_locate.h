@@ -89,10 +89,10 @@ __global__ __launch_bounds__(256) void loc_rows_kernel(const uint32_t* __restric
                                                        const uint64_t* __restrict__ off, uint64_t total,
                                                        uint32_t* __restrict__ own_rows)
 {
-  const uint64_t i = (uint64_t) blockIdx.x * 256 + threadIdx.x;
-  if (i >= total) return;
-  const uint32_t q = own_rows[i];
-  own_rows[i] = res[2 * (uint64_t) q] + (uint32_t) (i - off[q]);
+  for (uint64_t i = (uint64_t) blockIdx.x * 256 + threadIdx.x; i < total; i += (uint64_t) gridDim.x * 256) {
+    const uint32_t q = own_rows[i];   /* grid-stride: a batch may hold more than 2^32 positions */
+    own_rows[i] = res[2 * (uint64_t) q] + (uint32_t) (i - off[q]);
+  }
 }
 
 // Each lane walks slot after slot (i, i + stride, ...).  Per iteration a lane

@@ -355,17 +355,18 @@ template <class G>
 __global__ __launch_bounds__(256) void ftab_build_kernel(IdxArgs ix, uint32_t fsteps, uint64_t n,
                                                          uint2* __restrict__ out)
 {
-  const uint64_t v = (uint64_t) blockIdx.x * 256 + threadIdx.x;
-  if (v >= n) return;
-  uint32_t L = 0, R = ix.bwtsize;
-  for (uint32_t t = 0; t < fsteps; ++t) {
-    const uint32_t c = (uint32_t) (v >> (2 * G::K * t)) & (uint32_t) (G::NC - 1);
-    uint32_t sx[2 * G::K];
-    plane_xor<G::K>(c, sx);
-    L = lf_stream<G>(ix, L, c, sx);
-    R = lf_stream<G>(ix, R, c, sx);
+  /* grid-stride: 4^16 entries exceed the 2^32 work-items of one dispatch */
+  for (uint64_t v = (uint64_t) blockIdx.x * 256 + threadIdx.x; v < n; v += (uint64_t) gridDim.x * 256) {
+    uint32_t L = 0, R = ix.bwtsize;
+    for (uint32_t t = 0; t < fsteps; ++t) {
+      const uint32_t c = (uint32_t) (v >> (2 * G::K * t)) & (uint32_t) (G::NC - 1);
+      uint32_t sx[2 * G::K];
+      plane_xor<G::K>(c, sx);
+      L = lf_stream<G>(ix, L, c, sx);
+      R = lf_stream<G>(ix, R, c, sx);
+    }
+    out[v] = make_uint2(L, R);
   }
-  out[v] = make_uint2(L, R);
 }
 
 /* distinct d-blocks touched per step (1 if L/d == R/d else 2): the
@@ -589,8 +590,9 @@ static hipError_t launch_locate(const SearchLaunch& a)
 template <class G>
 static hipError_t launch_ftab(const SearchLaunch& a)
 {
-  hipLaunchKernelGGL((ftab_build_kernel<G>), dim3((uint32_t) ((a.ftab_n + 255) / 256)), dim3(256), 0, a.st, a.ix,
-                     a.ftab_steps, a.ftab_n, a.ftab_out);
+  const uint64_t blocks = (a.ftab_n + 255) / 256;
+  hipLaunchKernelGGL((ftab_build_kernel<G>), dim3((uint32_t) (blocks < (1u << 20) ? blocks : (1u << 20))), dim3(256), 0,
+                     a.st, a.ix, a.ftab_steps, a.ftab_n, a.ftab_out);
   return hipGetLastError();
 }
 
@@ -1387,8 +1389,9 @@ extern "C" int32_t kfmi_locate(void* index, void* results, uint32_t max_occ, voi
         rocprim::inclusive_scan(tmp2, tb2, d_pos, d_own, (size_t) total, rocprim::maximum<uint32_t>(), st) !=
             hipSuccess)
       return done(KFMI_E_KERNEL);
-    hipLaunchKernelGGL(loc_rows_kernel, dim3((uint32_t) ((total + 255) / 256)), dim3(256), 0, st, r->d_results, d_off,
-                       total, d_own);   /* owner -> first row of each slot, in place */
+    const uint64_t rb = (total + 255) / 256;
+    hipLaunchKernelGGL(loc_rows_kernel, dim3((uint32_t) (rb < (1u << 20) ? rb : (1u << 20))), dim3(256), 0, st,
+                       r->d_results, d_off, total, d_own);   /* owner -> first row of each slot, in place */
     if (hipGetLastError() != hipSuccess) return done(KFMI_E_KERNEL);
   }
   SearchLaunch a{};
