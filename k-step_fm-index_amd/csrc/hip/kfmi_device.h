@@ -361,8 +361,10 @@ __device__ __forceinline__ uint32_t lf_from_block(const IdxArgs& ix, const Blk<G
 }
 
 // ---------------------------------------------------------------------------
-// Streaming LF for large blocks (d >= 192 with K=2): planes read word group by
-// word group; all words are read (as the reference does).
+// Streaming LF for large blocks (d >= 192 with K=2): the planes are loaded in
+// chunks of up to 8 words, every load of a chunk issued before any of its
+// popcounts so the chunk's lines are in flight together; all words are read
+// (as the reference does) and masked.
 // ---------------------------------------------------------------------------
 template <class G>
 __device__ __forceinline__ uint32_t lf_stream(const IdxArgs& ix, uint32_t X, uint32_t c,
@@ -373,23 +375,34 @@ __device__ __forceinline__ uint32_t lf_stream(const IdxArgs& ix, uint32_t X, uin
   const Where<G> wh = locate<G>(ix, b, c);
   const uint32_t cnt = load_counter<G>(ix, wh, b, c);
   const uint32_t* pl = wh.planes;
+  constexpr int CH = G::NB < 8 ? G::NB : 8;
   uint32_t pop = 0;
-#pragma unroll 2
-  for (int w = 0; w < G::NB; ++w) {
-    uint32_t v[G::PW];
-    if constexpr (G::PW == 4 && (G::BOFF % 4 == 0) && (G::EW % 4 == 0)) {
-      uint4 q = *reinterpret_cast<const uint4*>(pl + 4 * w);
-      v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
-    } else if constexpr (G::PW == 2 && (G::BOFF % 2 == 0) && (G::EW % 2 == 0)) {
-      uint2 q = *reinterpret_cast<const uint2*>(pl + 2 * w);
-      v[0] = q.x; v[1] = q.y;
-    } else {
 #pragma unroll
-      for (int p = 0; p < G::PW; ++p) v[p] = pl[G::PW * w + p];
+  for (int w0 = 0; w0 < G::NB; w0 += CH) {
+    uint32_t v[CH][G::PW];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      const int w = w0 + j;
+      if (w >= G::NB) break;
+      if constexpr (G::PW == 4 && (G::BOFF % 4 == 0) && (G::EW % 4 == 0)) {
+        const uint4 q = *reinterpret_cast<const uint4*>(pl + 4 * w);
+        v[j][0] = q.x; v[j][1] = q.y; v[j][2] = q.z; v[j][3] = q.w;
+      } else if constexpr (G::PW == 2 && (G::BOFF % 2 == 0) && (G::EW % 2 == 0)) {
+        const uint2 q = *reinterpret_cast<const uint2*>(pl + 2 * w);
+        v[j][0] = q.x; v[j][1] = q.y;
+      } else {
+#pragma unroll
+        for (int p = 0; p < G::PW; ++p) v[j][p] = pl[G::PW * w + p];
+      }
     }
-    uint32_t m = row_mask(o - 32 * w);
-    if constexpr (G::TWO_SIDED) m = wh.e ? ~m : m;
-    pop += __popc(m & select_rows<G::K>(v, sx));
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      const int w = w0 + j;
+      if (w >= G::NB) break;
+      uint32_t m = row_mask(o - 32 * w);
+      if constexpr (G::TWO_SIDED) m = wh.e ? ~m : m;
+      pop += __popc(m & select_rows<G::K>(v[j], sx));
+    }
   }
   return finish<G>(ix, cnt, pop, b, c, X, wh.e);
 }

@@ -227,3 +227,21 @@ def test_ftab_jump_start_equals_oracle(gpu, oracle_mod, random_index, backend, b
                 assert np.array_equal(got, want), (backend, bases, k, d, m)
     finally:
         gpu.set_ftab(0)
+
+
+@pytest.mark.parametrize("backend", ["task-mid", "task-ac", "coop-mid", "task"])
+def test_long_reads_fused_limit_and_pack_fallback(gpu, oracle_mod, random_index, backend):
+    """Fused packing keeps up to 16 code words per query in registers (256 bases
+    at K=2, 256 at K=1); longer reads fall back to the pack kernel.  Both sides
+    of that limit, odd alignments (m % 4 != 0) and long reads must match."""
+    text, idxs = random_index
+    for k, d in ((2, 64), (1, 64)):
+        idx = idxs[(k, d)]
+        ref_img = idx.alt_counters()[0].image() if backend in ALT else idx.image()
+        for m in (254, 256, 258, 300, 1000):
+            if m % k:
+                continue
+            q = _reads(text, 1500, m, seed=m * 3 + k)
+            want, _ = oracle_mod.search(ref_img, q)
+            got = gpu.search_array(idx, q, backend)
+            assert np.array_equal(got, want), (backend, k, m)
