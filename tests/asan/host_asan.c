@@ -1,0 +1,174 @@
+/*
+ * host_asan.c -- TEST HARNESS: the engine's host C layer (csrc/host/*.c)
+ * built alone with AddressSanitizer + UBSan (gcc), driven over the golden
+ * fixtures: index load / transforms / save, the host builder with SA samples,
+ * query and result I/O, sample files, and the error paths (missing, wrong-tag
+ * and truncated files).  The HIP layer is replaced by the stubs below (the
+ * handles never reach a device here).
+ *
+ *   host_asan <golden_dir> <tmp_dir> <case> <k> <d> <m> <num>
+ * Prints "OK <checks>" and exits 0 when every check passes.
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include "../../k-step_fm-index_amd/csrc/kfmi_internal.h"
+
+/* ---- stubs for the HIP layer (csrc/hip) ---- */
+int32_t freeIndexGPU(void **index) { (void) index; return KFMI_SUCCESS; }
+int32_t freeQueriesGPU(void **q) { (void) q; return KFMI_SUCCESS; }
+int32_t freeResultsGPU(void **r) { (void) r; return KFMI_SUCCESS; }
+kfmi_backend_t kfmi_backend(void) { return KFMI_BK_TASK_MID; }
+uint32_t kfmi_backend_tag(kfmi_backend_t b) { (void) b; return 101u; }
+int32_t kfmi_device_count(void) { return 0; }
+int32_t kfmi_build_index_gpu_sa(const char *t, uint64_t n, uint32_t k, uint32_t d, uint32_t r, void **i)
+{ (void) t; (void) n; (void) k; (void) d; (void) r; (void) i; return KFMI_E_NO_DEVICE; }
+int32_t kfmi_build_index_gpu(const char *t, uint64_t n, uint32_t k, uint32_t d, int32_t h, void **i)
+{ (void) h; return kfmi_build_index_gpu_sa(t, n, k, d, 0, i); }
+
+static int checks = 0, failures = 0;
+#define CHECK(cond, ...) do { checks++; if (!(cond)) { failures++; fprintf(stderr, "FAIL %s:%d: ", __FILE__, __LINE__); \
+  fprintf(stderr, __VA_ARGS__); fputc('\n', stderr); } } while (0)
+
+static unsigned char *slurp(const char *fn, size_t *len)
+{
+  FILE *fp = fopen(fn, "rb");
+  unsigned char *b;
+  long n;
+  if (!fp) return NULL;
+  fseek(fp, 0, SEEK_END); n = ftell(fp); fseek(fp, 0, SEEK_SET);
+  b = (unsigned char *) malloc((size_t) n + 1);
+  if (fread(b, 1, (size_t) n, fp) != (size_t) n) { free(b); fclose(fp); return NULL; }
+  fclose(fp);
+  *len = (size_t) n;
+  return b;
+}
+
+static int same_image(void *index, const char *fn)
+{
+  size_t len = 0;
+  const void *img; uint64_t bytes;
+  unsigned char *want = slurp(fn, &len);
+  int ok = want && kfmi_index_image(index, &img, &bytes) == 0 && bytes == len && !memcmp(img, want, len);
+  free(want);
+  return ok;
+}
+
+int main(int argc, char **argv)
+{
+  char p[1024], q[1024];
+  const char *g, *tmp, *cs;
+  uint32_t k, d, m, num, tag;
+  void *idx = NULL, *t101 = NULL, *t200 = NULL, *t201 = NULL, *re = NULL;
+  if (argc < 8) { fprintf(stderr, "usage\n"); return 2; }
+  g = argv[1]; tmp = argv[2]; cs = argv[3];
+  k = (uint32_t) atoi(argv[4]); d = (uint32_t) atoi(argv[5]); m = (uint32_t) atoi(argv[6]); num = (uint32_t) atoi(argv[7]);
+
+  /* 1. every tag loads byte-identically; transforms reproduce the reference files */
+  for (tag = 100; tag <= 201; tag += (tag == 101 ? 99 : 1)) {
+    void *x = NULL;
+    snprintf(p, sizeof p, "%s/%s/k%u_d%u.%u.fmi", g, cs, k, d, tag);
+    CHECK(loadIndex(p, &x) == 0 && same_image(x, p), "load %s", p);
+    freeIndex(&x);
+  }
+  snprintf(p, sizeof p, "%s/%s/k%u_d%u.100.fmi", g, cs, k, d);
+  CHECK(loadIndex(p, &idx) == 0, "load 100");
+  CHECK(kfmi_transform_interleave(idx, &t101) == 0, "interleave");
+  CHECK(kfmi_transform_ac(idx, &t200, &t201) == 0, "ac");
+  snprintf(q, sizeof q, "%s/%s/k%u_d%u.101.fmi", g, cs, k, d); CHECK(same_image(t101, q), "101 bytes");
+  snprintf(q, sizeof q, "%s/%s/k%u_d%u.200.fmi", g, cs, k, d); CHECK(same_image(t200, q), "200 bytes");
+  snprintf(q, sizeof q, "%s/%s/k%u_d%u.201.fmi", g, cs, k, d); CHECK(same_image(t201, q), "201 bytes");
+  CHECK(kfmi_transform_interleave(t101, &re) == KFMI_INDEX_VER_BASELINE, "transform needs tag 100");
+
+  /* 2. save + reload round trip under the reference file names */
+  snprintf(q, sizeof q, "%s/x.fmi", tmp);
+  CHECK(saveIndex(q, t201) == 0, "save 201");
+  snprintf(q, sizeof q, "%s/x.fmi.interleaving.ac", tmp);
+  CHECK(loadIndex(q, &re) == 0 && same_image(re, q), "reload 201");
+  freeIndex(&re);
+
+  /* 3. strict loader and broken files */
+  CHECK(kfmi_load_index_tag(p, 101, &re) == 101 && re == NULL, "strict tag");
+  snprintf(q, sizeof q, "%s/missing.fmi", tmp);
+  CHECK(loadIndex(q, &re) == KFMI_E_OPENING_INDEX_FILE, "missing file");
+  {
+    size_t len = 0;
+    unsigned char *b = slurp(p, &len);
+    FILE *fp;
+    snprintf(q, sizeof q, "%s/trunc.fmi", tmp);
+    fp = fopen(q, "wb"); fwrite(b, 1, len / 2, fp); fclose(fp);
+    CHECK(loadIndex(q, &re) == KFMI_E_READING_FMI && re == NULL, "truncated body");
+    fp = fopen(q, "wb"); fwrite(b, 1, 10, fp); fclose(fp);
+    CHECK(loadIndex(q, &re) != 0 && re == NULL, "truncated header");
+    CHECK(kfmi_index_from_image(b, 20, &re) != 0 && re == NULL, "short image");
+    b[0] = 77;
+    CHECK(kfmi_index_from_image(b, len, &re) != 0 && re == NULL, "bad tag");
+    free(b);
+  }
+
+  /* 4. host builder (SA-IS) equals the reference builder's file; SA samples; sample file */
+  {
+    size_t len = 0, i, n = 0;
+    char *fa, *text;
+    snprintf(q, sizeof q, "%s/%s/ref.fa", g, cs);
+    fa = (char *) slurp(q, &len);
+    CHECK(fa != NULL, "ref.fa");
+    text = (char *) malloc(len + 1);
+    for (i = 0; fa && i < len && fa[i] != '\n'; i++) {}
+    for (; fa && i < len; i++) if (fa[i] != '\n') text[n++] = fa[i];
+    CHECK(kfmi_build_index_ex(text, n, k, d, 8, 0, &re) == 0 && same_image(re, p), "host builder");
+    {
+      const uint32_t *sa; uint64_t cnt; uint32_t rate;
+      void *x = NULL;
+      CHECK(kfmi_index_sa(re, &sa, &cnt, &rate) == 0 && rate == 8 && cnt == (n + 1 + 7) / 8 && sa[0] == n, "sa");
+      snprintf(q, sizeof q, "%s/x.sa", tmp);
+      CHECK(kfmi_save_sa(q, re) == 0, "save sa");
+      CHECK(loadIndex(p, &x) == 0 && kfmi_load_sa(q, x) == 0, "load sa");
+      { const uint32_t *sb; uint64_t c2; uint32_t r2;
+        kfmi_index_sa(x, &sb, &c2, &r2);
+        CHECK(c2 == cnt && r2 == rate && !memcmp(sa, sb, 4 * cnt), "sa roundtrip"); }
+      CHECK(kfmi_load_sa(p, x) == KFMI_E_READING_FMI, "not a sample file");
+      freeIndex(&x);
+    }
+    freeIndex(&re);
+    CHECK(kfmi_build_index_ex(text, n, k, d, 3, 0, &re) == KFMI_E_BAD_ARGUMENT && re == NULL, "rate 3");
+    CHECK(kfmi_build_index_ex("ACGN", 4, k, d, 0, 0, &re) != 0 && re == NULL, "non-ACGT");
+    CHECK(kfmi_build_index_ex(text, n, k, d, 0, 1, &re) == KFMI_E_NO_DEVICE, "no device");
+    /* tiny and odd texts, every K, a few d */
+    for (uint32_t kk = 1; kk <= 4; kk++)
+      for (uint32_t dd = 32; dd <= 96; dd += 32)
+        for (size_t nn = 1; nn < 70 && nn <= n; nn += 7) {
+          int e = kfmi_build_index_ex(text, nn, kk, dd, 2, 0, &re);
+          CHECK(nn + 1 < kk ? e != 0 : e == 0, "tiny build k=%u d=%u n=%zu -> %d", kk, dd, nn, e);
+          freeIndex(&re);
+        }
+    free(text);
+    free(fa);
+  }
+
+  /* 5. queries, results */
+  {
+    void *qs = NULL, *rs = NULL, *rl = NULL;
+    snprintf(q, sizeof q, "%s/%s/q%u.qry", g, cs, m);
+    CHECK(loadQueries(q, m, num, &qs) == 0, "queries");
+    freeQueries(&qs);
+    CHECK(loadQueries(q, m + 1, num, &qs) != 0 && qs == NULL, "wrong length");
+    CHECK(loadQueries(q, m, num + 1, &qs) != 0 && qs == NULL, "too few reads");
+    snprintf(q, sizeof q, "%s/%s/k%u_d%u.q%u.cpu.res", g, cs, k, d, m);
+    CHECK(loadResults(q, &rs) == 0, "results");
+    snprintf(p, sizeof p, "%s/out", tmp);
+    CHECK(saveResults(p, rs, NULL) == 0, "save results");
+    snprintf(p, sizeof p, "%s/out.res.gpu", tmp);
+    {
+      size_t l1 = 0, l2 = 0;
+      unsigned char *a = slurp(q, &l1), *b = slurp(p, &l2);
+      CHECK(a && b && l1 == l2 && !memcmp(a, b, l1), "results bytes");
+      free(a); free(b);
+    }
+    CHECK(loadResults(p, &rl) == 0, "reload results");
+    freeResults(&rs); freeResults(&rl);
+  }
+  freeIndex(&idx); freeIndex(&t101); freeIndex(&t200); freeIndex(&t201);
+  printf("%s %d checks, %d failures\n", failures ? "FAILED" : "OK", checks, failures);
+  return failures ? 1 : 0;
+}
