@@ -33,6 +33,7 @@ import kstep_fmi as K  # noqa: E402
 from kstep_fmi import synth  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+PROBE_CEILING_GLINES = 52.7   # gather_probe, 3 GB table, one random line per lane (profiles/r01)
 
 
 def log(*a):
@@ -269,13 +270,14 @@ def main():
     achieved = bytes_alg / (lf_avg_ms / 1e3) / 1e9
     # HBM bytes per launch from the committed PMC profile of the same config
     # (scripts/traffic_from_pmc.py: TCC_EA0_RDREQ x line bytes, gfx950-corrected)
-    traffic, traffic_src = None, None
+    traffic, traffic_src, rdreq = None, None, None
     tj = Path(a.traffic_json)
     if tj.exists():
         try:
             tr = json.loads(tj.read_text())
             if tr.get("backend") == a.backend and tr.get("queries") == a.queries and tr.get("ref_size") == a.ref_size:
                 traffic, traffic_src = tr.get("hbm_bytes_per_launch"), tr.get("source")
+                rdreq = tr.get("rdreq_per_launch")
         except Exception:
             traffic = None
 
@@ -402,7 +404,12 @@ def main():
                          "naive_bytes_per_launch": 2 * (a.qlen // a.k) * b_lf * a.queries,
                          "traffic_source": traffic_src,
                          "traffic_GBs": round(traffic / (lf_avg_ms / 1e3) / 1e9, 1) if traffic else None,
-                         "traffic_frac": round(traffic / (lf_avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if traffic else None},
+                         "traffic_frac": round(traffic / (lf_avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
+                         # every LF is a random 128-B line: the binding limit is the rate of random line
+                         # requests, calibrated by gather_probe on the same 3 GB table size
+                         # (profiles/r01/gather_probe_table_size.txt, per-lane 64-B lines)
+                         "line_requests_G_per_s": round(rdreq / (lf_avg_ms / 1e3) / 1e9, 2) if rdreq else None,
+                         "line_request_ceiling_G_per_s": PROBE_CEILING_GLINES},
             "cpu_baseline": cpu,
             "parity": {"index_md5_pinned": index_md5_ok, "results_md5_pinned": results_md5_ok},
             "setup_s": {"gpu_index_build": round(build_s, 2), "h2d": round(upload_s, 2), "d2h": round(d2h_s, 3)},
