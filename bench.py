@@ -259,13 +259,15 @@ def main():
     # ---- roofline: algorithmic bytes of the LF kernel ------------------------
     blocks = K.count_blocks(idx, q)
     b_lf = a.k * a.d // 4 + 4                               # bit planes of one block + one counter
-    # + what the LF kernel reads per query (ASCII row when packing is fused into
-    # the task kernel, else the packed code words) and the (L, R) it writes
+    bytes_alg = blocks * b_lf                               # 36 B x distinct blocks
+    # reported beside it: what the LF kernel also reads per query (the ASCII row
+    # when packing is fused into the task kernel, else the packed code words)
+    # and the (L, R) it writes
     spw = 16 // a.k
     nwords = (a.qlen // a.k + spw - 1) // spw
     fused = a.backend.startswith("task") and os.environ.get("KFMI_FUSED", "1") != "0" and nwords <= 16
     q_in = a.qlen if fused else 4 * nwords
-    bytes_alg = blocks * b_lf + reads.shape[0] * (q_in + 8)
+    bytes_io = reads.shape[0] * (q_in + 8)
     lf_avg_ms = float(np.mean(lf_ms))
     achieved = bytes_alg / (lf_avg_ms / 1e3) / 1e9
     # HBM bytes per launch from the committed PMC profile of the same config
@@ -275,7 +277,8 @@ def main():
     if tj.exists():
         try:
             tr = json.loads(tj.read_text())
-            if tr.get("backend") == a.backend and tr.get("queries") == a.queries and tr.get("ref_size") == a.ref_size:
+            if (tr.get("backend") == a.backend and tr.get("queries") == a.queries and tr.get("ref_size") == a.ref_size
+                    and tr.get("qlen", 100) == a.qlen and tr.get("k", 2) == a.k and tr.get("d", 64) == a.d):
                 traffic, traffic_src = tr.get("hbm_bytes_per_launch"), tr.get("source")
                 rdreq = tr.get("rdreq_per_launch")
         except Exception:
@@ -378,7 +381,7 @@ def main():
 
     if D.rank == 0:
         line = {
-            "metric": "Mqueries/s (100 bp reads, 3 Gbase index)",
+            "metric": f"Mqueries/s ({a.qlen} bp reads, {a.ref_size / 1e9:g} Gbase index)",
             "value": round(value, 3),
             "unit": "Mqueries/s",
             "n_gpus": D.world,
@@ -400,6 +403,7 @@ def main():
                          "kernel": "LF kernel (task/coop search), HIP-event average over the timed steps",
                          "bytes_per_launch": bytes_alg, "distinct_blocks": blocks, "bytes_per_block": b_lf,
                          "bytes_per_query_io": q_in + 8,
+                         "achieved_incl_query_io": round((bytes_alg + bytes_io) / (lf_avg_ms / 1e3) / 1e9, 1),
                          "lf_ms": round(lf_avg_ms, 4), "pack_ms": round(float(np.mean(pack_ms)), 4),
                          "naive_bytes_per_launch": 2 * (a.qlen // a.k) * b_lf * a.queries,
                          "traffic_source": traffic_src,

@@ -132,7 +132,7 @@ int32_t     kfmi_device_count(void);
 int32_t     kfmi_last_error(void);
 /* searchIndexGPU with a status return. */
 int32_t     kfmi_search(void *index, void *queries, void *results);
-/* ftab (Bowtie-style jump start; not in the reference): the task backends look
+/* ftab (Bowtie-style jump start; not in the reference): every backend looks
  * up [L, R) after the first `bases` bases of each query in a table of all
  * 4^bases codes (8 B each: 134 MB at 12) built on the device with the search's
  * own LF steps, then continue from there -- results are unchanged.  0 = off

@@ -116,6 +116,13 @@ __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, 
   const int g = lane / C::TPR;
   uint32_t L = 0, R = ix.bwtsize;
   constexpr int S = sb_shift_for(G::D);
+  uint32_t skip = 0;
+  if (ix.ftab && steps >= ix.ftab_steps) {   // wave-uniform: jump start from the ftab
+    skip = ix.ftab_steps;
+    const uint2 lr = ix.ftab[qp[qs] & ix.ftab_mask];
+    L = lr.x;
+    R = lr.y;
+  }
 
   for (uint32_t w = 0; w < nwords; ++w) {
     const uint32_t word = qp[(uint64_t) w * num + qs];
@@ -123,6 +130,7 @@ __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, 
 #pragma unroll 1
     for (int j = 0; j < G::SPW; ++j) {
       if ((uint32_t) j >= left) break;
+      if (w * G::SPW + j < skip) continue;   // steps covered by the ftab (wave-uniform)
       const uint32_t c = (word >> (2 * G::K * j)) & (uint32_t) (G::NC - 1);
       const uint32_t bl = L / (uint32_t) G::D, br = R / (uint32_t) G::D;
       const bool needR = br != bl;

@@ -1009,16 +1009,16 @@ static IdxArgs idx_args(const kfmi_dev_index* di)
   return ix;
 }
 
-/* The ftab of `bases` bases for a task backend, (re)built on the device from the
- * uploaded layout with the search's own LF steps; sets ix.ftab (null when off,
- * for coop backends, or when bases is not a multiple of K). */
+/* The ftab of `bases` bases, (re)built on the device from the uploaded layout
+ * with the search's own LF steps; sets ix.ftab (null when off or when bases is
+ * not a multiple of K). */
 static int32_t use_ftab(kfmi_dev_index* di, DevCtx* ctx, IdxArgs& ix)
 {
   ix.ftab = nullptr;
   ix.ftab_steps = 0;
   ix.ftab_mask = 0;
   const uint32_t bases = ftab_bases();
-  if (!bases || is_coop(di->backend) || bases % di->K) return KFMI_SUCCESS;
+  if (!bases || bases % di->K) return KFMI_SUCCESS;
   if (di->ftab_chars != bases) {
     if (di->ftab) (void) hipFree(di->ftab);
     di->ftab = nullptr;

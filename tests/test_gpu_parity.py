@@ -207,7 +207,8 @@ def test_b5_boundary_against_bruteforce(gpu, n):
 
 
 @pytest.mark.parametrize("bases", [2, 8, 12])
-@pytest.mark.parametrize("backend", ["task-mid", "task", "task-packed", "task-ac", "task-ac128"])
+@pytest.mark.parametrize("backend", ["task-mid", "task", "task-packed", "task-ac", "task-ac128", "coop-mid",
+                                     "coop-ac128", "coop"])
 def test_ftab_jump_start_equals_oracle(gpu, oracle_mod, random_index, backend, bases):
     """The ftab replaces the first bases/K LF steps by a table built with the
     same LF steps: results must not change (reads shorter than the table keep
@@ -216,6 +217,8 @@ def test_ftab_jump_start_equals_oracle(gpu, oracle_mod, random_index, backend, b
     gpu.set_ftab(bases)
     try:
         for k, d in ((2, 64), (1, 64), (2, 192)):
+            if not coop_supported(backend, k, d):
+                continue
             idx = idxs[(k, d)]
             ref_img = idx.alt_counters()[0].image() if backend in ALT else idx.image()
             for m, n in ((100, 6000), (150, 1500), (bases, 800), (2 * k, 300)):
