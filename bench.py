@@ -265,7 +265,7 @@ def main():
     # and the (L, R) it writes
     spw = 16 // a.k
     nwords = (a.qlen // a.k + spw - 1) // spw
-    fused = a.backend.startswith("task") and os.environ.get("KFMI_FUSED", "1") != "0" and nwords <= 16
+    fused = os.environ.get("KFMI_FUSED", "1") != "0" and nwords <= 16
     q_in = a.qlen if fused else 4 * nwords
     bytes_io = reads.shape[0] * (q_in + 8)
     lf_avg_ms = float(np.mean(lf_ms))

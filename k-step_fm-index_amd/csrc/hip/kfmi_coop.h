@@ -97,12 +97,30 @@ __device__ __forceinline__ uint32_t coop_lf(const IdxArgs& ix, const uint8_t* sl
   return finish<G>(ix, cnt, pop, b, c, X, e);
 }
 
+// Rows per staging round of the fused coop kernel: a multiple of 16 (so every
+// round's source stays 16-byte aligned) whose bytes fit the wave's LDS area;
+// 0 = the rows do not fit (use the pack kernel).
 template <class G>
+__host__ __device__ constexpr uint32_t coop_stage_rows(uint32_t m)
+{
+  uint32_t r = 64;
+  while (r >= 16 && r * m + 16 > (uint32_t) CoopCfg<G>::WAVE_LDS) r >>= 1;
+  return r >= 16 ? r : 0u;
+}
+
+// MAXW == 0: codes from the pack kernel's words (qp).  MAXW > 0: fused packing
+// -- before its loop each wave copies its 64 ASCII rows HBM -> its own LDS area
+// (coalesced 16-B loads, rounds of coop_stage_rows rows) and every lane turns
+// its row into MAXW registers of codes; lanes past the batch end take the
+// all-A query (valid rows for their DMA requests, never stored).
+template <class G, int MAXW>
 __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, const uint32_t* __restrict__ qp,
+                                                                    const uint8_t* __restrict__ ascii, uint32_t m,
                                                                     uint64_t num, uint32_t steps, uint32_t nwords,
                                                                     uint32_t* __restrict__ res)
 {
   using C = CoopCfg<G>;
+  constexpr int CW = MAXW > 0 ? MAXW : 1;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
@@ -114,18 +132,47 @@ __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, 
   const uint64_t qs = q < num ? q : num - 1;   // tail lanes replay a valid query, never stored
   const int k = lane % C::TPR;
   const int g = lane / C::TPR;
+  uint32_t cw[CW];
+  if constexpr (MAXW > 0) {
+    const uint32_t rpr = coop_stage_rows<G>(m);
+#pragma unroll 1
+    for (uint32_t h = 0; h < 64u / rpr; ++h) {
+      const uint64_t r0 = q0 + h * rpr;
+      const uint64_t nr = r0 < num ? (num - r0 < rpr ? num - r0 : rpr) : 0;
+      const uint32_t n16 = (uint32_t) ((nr * m + 15) / 16);
+      const uint4* src = reinterpret_cast<const uint4*>(ascii + r0 * m);
+      for (uint32_t i = lane; i < n16; i += 64) reinterpret_cast<uint4*>(wl)[i] = src[i];
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      if ((uint32_t) lane / rpr == h) row_codes<MAXW>(wl, (uint64_t) (lane % rpr) * m, m, cw);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    if (q >= num) {
+#pragma unroll
+      for (int i = 0; i < CW; ++i) cw[i] = 0;
+    }
+  }
   uint32_t L = 0, R = ix.bwtsize;
   constexpr int S = sb_shift_for(G::D);
   uint32_t skip = 0;
   if (ix.ftab && steps >= ix.ftab_steps) {   // wave-uniform: jump start from the ftab
     skip = ix.ftab_steps;
-    const uint2 lr = ix.ftab[qp[qs] & ix.ftab_mask];
+    uint32_t w0;
+    if constexpr (MAXW > 0) w0 = cw[0];
+    else w0 = qp[qs];
+    const uint2 lr = ix.ftab[w0 & ix.ftab_mask];
     L = lr.x;
     R = lr.y;
   }
 
   for (uint32_t w = 0; w < nwords; ++w) {
-    const uint32_t word = qp[(uint64_t) w * num + qs];
+    uint32_t word;
+    if constexpr (MAXW > 0) {
+      word = cw[0];
+#pragma unroll
+      for (int i = 0; i + 1 < CW; ++i) cw[i] = cw[i + 1];
+    } else {
+      word = qp[(uint64_t) w * num + qs];
+    }
     const uint32_t left = steps - w * G::SPW;
 #pragma unroll 1
     for (int j = 0; j < G::SPW; ++j) {
@@ -172,8 +219,8 @@ __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, 
 }
 
 template <class G>
-hipError_t coop_launch(hipStream_t st, IdxArgs ix, const uint32_t* qp, uint64_t num, uint32_t steps,
-                       uint32_t nwords, uint32_t* res)
+hipError_t coop_launch(hipStream_t st, IdxArgs ix, const uint32_t* qp, const uint8_t* ascii, uint32_t m, int maxw,
+                       uint64_t num, uint32_t steps, uint32_t nwords, uint32_t* res)
 {
   using C = CoopCfg<G>;
   if constexpr (!C::OK) {
@@ -182,8 +229,15 @@ hipError_t coop_launch(hipStream_t st, IdxArgs ix, const uint32_t* qp, uint64_t 
     const uint64_t waves = (num + 63) / 64;
     const uint64_t blocks = (waves + C::WPB - 1) / C::WPB;
     const size_t lds = (size_t) C::WPB * C::WAVE_LDS;
-    hipLaunchKernelGGL((coop_kernel<G>), dim3((uint32_t) blocks), dim3(64 * C::WPB), lds, st, ix, qp, num, steps,
-                       nwords, res);
+    if (maxw == 8)
+      hipLaunchKernelGGL((coop_kernel<G, 8>), dim3((uint32_t) blocks), dim3(64 * C::WPB), lds, st, ix, qp, ascii, m,
+                         num, steps, nwords, res);
+    else if (maxw == 16)
+      hipLaunchKernelGGL((coop_kernel<G, 16>), dim3((uint32_t) blocks), dim3(64 * C::WPB), lds, st, ix, qp, ascii, m,
+                         num, steps, nwords, res);
+    else
+      hipLaunchKernelGGL((coop_kernel<G, 0>), dim3((uint32_t) blocks), dim3(64 * C::WPB), lds, st, ix, qp, ascii, m,
+                         num, steps, nwords, res);
     return hipGetLastError();
   }
 }

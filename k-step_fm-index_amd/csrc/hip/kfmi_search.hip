@@ -517,7 +517,7 @@ static bool is_coop(int backend);
 
 static int fused_maxw(int backend, uint32_t nwords)
 {
-  if (is_coop(backend)) return 0;
+  (void) backend;   /* task and coop kernels both pack in-kernel (m <= 256 fits either's LDS staging) */
   const char* e = getenv("KFMI_FUSED");
   if (e && !atoi(e)) return 0;
   return nwords <= 8 ? 8 : (nwords <= 16 ? 16 : 0);
@@ -550,7 +550,7 @@ static hipError_t launch_task(const SearchLaunch& a)
 template <class G>
 static hipError_t launch_coop(const SearchLaunch& a)
 {
-  return coop_launch<G>(a.st, a.ix, a.qp, a.num, a.steps, a.nwords, a.res);
+  return coop_launch<G>(a.st, a.ix, a.qp, a.ascii, a.m, a.maxw, a.num, a.steps, a.nwords, a.res);
 }
 
 template <class G>
