@@ -221,6 +221,8 @@ int32_t build_gpu(const char* text, uint64_t n, uint32_t k, uint32_t d, uint32_t
    * the '$' row 0 for s == n -- and (SA - 1 - s) wraps at most once. */
   if (n == 0 || n + 1 < k || n + 1 > 0xFFFFFFFEull || k < 1 || k > 4 || d == 0 || d % 32)
     return KFMI_E_BAD_ARGUMENT;
+  /* one thread per base: a dispatch holds at most 2^32 - 1 work-items */
+  if (n > 0xFFFFFF00ull) return KFMI_E_NOT_IMPLEMENTED;   /* caller falls back to the host builder */
   BHIP(hipSetDevice(dev));
   hipStream_t st;
   BHIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));

@@ -16,6 +16,7 @@
 #include <string.h>
 #include <chrono>
 #include <mutex>
+#include <new>
 #include <thread>
 #include <vector>
 
@@ -858,7 +859,11 @@ static int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx)
   int32_t err = host_entries_for(f, lay, &owned, &src);
   if (err) return err;
 
-  kfmi_dev_index* di = new kfmi_dev_index();
+  kfmi_dev_index* di = new (std::nothrow) kfmi_dev_index();   /* no C++ exception crosses the C ABI */
+  if (!di) {
+    if (owned) freeIndex((void**) &owned);
+    return KFMI_E_ALLOCATING_FMI;
+  }
   di->device = dev;
   di->backend = backend;
   di->layout = lay;
@@ -1058,7 +1063,8 @@ static int32_t upload_queries(kfmi_qrys_t* q, uint32_t K, int dev, DevCtx* ctx)
 {
   if (q->size == 0 || (q->size % K) != 0) return KFMI_E_BAD_ARGUMENT;   /* B6 */
   if (64ull * q->size > 160ull * 1024) return KFMI_E_BAD_ARGUMENT;       /* pack tile must fit LDS */
-  kfmi_dev_queries* dq = new kfmi_dev_queries();
+  kfmi_dev_queries* dq = new (std::nothrow) kfmi_dev_queries();
+  if (!dq) return KFMI_E_ALLOCATING_MFASTA;
   dq->device = dev;
   dq->num = q->num;
   dq->size = q->size;
@@ -1333,7 +1339,8 @@ extern "C" int32_t kfmi_locate(void* index, void* results, uint32_t max_occ, voi
     if (err) return err;
   }
   const uint64_t num = r->num;
-  kfmi_locations* L = new kfmi_locations();
+  kfmi_locations* L = new (std::nothrow) kfmi_locations();
+  if (!L) return KFMI_E_ALLOCATING_RESULTS;
   L->num = num;
   L->h_off = (uint64_t*) malloc(8 * (num + 1));
   if (!L->h_off) {
