@@ -123,6 +123,16 @@ def make_text(n: int) -> bytes:
     return rng.randbytes(n).translate(synth.TBL)
 
 
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_reference_baseline(idx, reads, ns, k, d, thr, res_gpu):
     """The reference's own CPU searcher (common/searchQueries.c +
     src/fmIndexCPUBaseline.c, compiled from /root/reference sources into
@@ -377,6 +387,13 @@ def main():
                 cpu = port
             else:
                 extra["cpu_port"] = port
+            cpu["cpu_model"] = cpu_model()
+            # single-thread rate of the restatement on a small slice
+            n1 = min(100_000, ns)
+            t = time.perf_counter()
+            oracle.search(img, reads[:n1], nthreads=1)
+            extra["cpu_port_1thread"] = {"value": round(n1 / (time.perf_counter() - t) / 1e6, 4),
+                                         "unit": "Mqueries/s", "cores": 1, "sample": f"first {n1} reads"}
             log(f"cpu baseline {cpu}")
 
     if D.rank == 0:
