@@ -303,14 +303,16 @@ int32_t kfmi_build_index_ex(const char *text, uint64_t n, uint32_t k, uint32_t d
   return kfmi_build_index_cpu_sa(text, n, k, d, sa_rate, index);
 }
 
-/* interface.h:35: K, d from KFMI_K / KFMI_D (the reference: -DK_STEPS, -DNUM_CHUNK). */
+/* interface.h:35: K, d from KFMI_K / KFMI_D (the reference: -DK_STEPS, -DNUM_CHUNK);
+ * KFMI_SA_RATE > 0 also keeps the row-sampled suffix array (locate). */
 int32_t buildIndex(void *reference, void **index)
 {
   kfmi_ref_t *ref = (kfmi_ref_t *) reference;
   const char *ek = getenv("KFMI_K"), *ed = getenv("KFMI_D"), *eg = getenv("KFMI_BUILD_GPU");
+  const char *es = getenv("KFMI_SA_RATE");
   uint32_t k = ek ? (uint32_t) atoi(ek) : 2, d = ed ? (uint32_t) atoi(ed) : 64;
+  uint32_t rate = es ? (uint32_t) atoi(es) : 0;
   int use_gpu = eg ? atoi(eg) : (kfmi_device_count() > 0);
   if (!ref) return KFMI_E_BAD_ARGUMENT;
-  if (use_gpu) return kfmi_build_index_gpu(ref->h_reference, ref->size, k, d, 1, index);
-  return kfmi_build_index_cpu(ref->h_reference, ref->size, k, d, index);
+  return kfmi_build_index_ex(ref->h_reference, ref->size, k, d, rate, use_gpu, index);
 }

@@ -5,8 +5,12 @@
  * searchIndexGPU x iters -> transferGPUtoCPU -> saveResults("<index>.res.gpu").
  * Prints "TIME: <mean seconds per iteration>" like the reference, plus the
  * device-side (HIP event) times of the last iteration.
- * Environment: KFMI_BACKEND (task|coop|task-ac|coop-ac|task-packed|coop-packed),
- * KFMI_DEVICE, KFMI_ITERS (default 5, the reference's `iter`).
+ * Environment: KFMI_BACKEND (task|coop|task-ac|coop-ac|task-packed|coop-packed|
+ * task-mid|coop-mid|task-ac128|coop-ac128), KFMI_DEVICE, KFMI_ITERS (default 5,
+ * the reference's `iter`), KFMI_FTAB.
+ * Locate (extension): KFMI_SA_FILE=<samples written by gfmi> also writes
+ * "<index>.pos.gpu": per query "<n> <p1> ... <pn>" (text positions, suffix
+ * order; at most KFMI_MAX_OCC per query when set).
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -37,6 +41,31 @@ int main(int argc, char *argv[])
     CHECK(kfmi_last_error());
   }
   t1 = sampleTime();
+  if (getenv("KFMI_SA_FILE")) {
+    void *loc = NULL;
+    const char *mo = getenv("KFMI_MAX_OCC");
+    char fn[1100];
+    FILE *fp;
+    uint32_t q;
+    CHECK(kfmi_load_sa(getenv("KFMI_SA_FILE"), index));
+    CHECK(kfmi_locate(index, results, mo ? (uint32_t) strtoul(mo, NULL, 10) : 0u, &loc));
+    snprintf(fn, sizeof fn, "%s.pos.gpu", argv[1]);
+    fp = fopen(fn, "w");
+    if (!fp) { fprintf(stderr, "cannot write %s\n", fn); return EXIT_FAILURE; }
+    {
+      const uint64_t *off = kfmi_locations_offsets(loc);
+      const uint32_t *pos = kfmi_locations_positions(loc);
+      for (q = 0; q < numqueries; q++) {
+        uint64_t i;
+        fprintf(fp, "%llu", (unsigned long long) (off[q + 1] - off[q]));
+        for (i = off[q]; i < off[q + 1]; i++) fprintf(fp, " %u", pos[i]);
+        fputc('\n', fp);
+      }
+    }
+    fclose(fp);
+    printf("LOCATE: %llu positions\n", (unsigned long long) kfmi_locations_total(loc));
+    kfmi_locations_free(&loc);
+  }
   CHECK(transferGPUtoCPU(results));
   CHECK(saveResults(argv[1], results, index));
   CHECK(freeIndexGPU(&index));

@@ -58,3 +58,34 @@ def test_search_driver(tmp_path, backend, tag, res_tag):
     assert f"BACKEND: {backend}" in out and "TIME:" in out
     want = (GOLDEN / "textA" / ent["results"][f"100.{res_tag}"]["file"]).read_bytes()
     assert (tmp_path / "idx.fmi.res.gpu").read_bytes() == want
+
+
+@pytest.mark.gpu
+def test_gfmi_sa_and_search_driver_locate(tmp_path):
+    """CLI locate path (extension): gfmi with KFMI_SA_RATE writes <index>.sa,
+    searchQueries with KFMI_SA_FILE writes <index>.pos.gpu; every position
+    must start an occurrence of its read and the counts must equal R - L."""
+    import numpy as np
+    import util
+    c = manifest()["textA"]
+    shutil.copy(GOLDEN / "textA" / "ref.fa", tmp_path / "ref.fa")
+    n = c["n"]
+    run([BIN / "gfmi", "ref.fa", n], tmp_path, {"KFMI_SA_RATE": "4"})
+    idx = tmp_path / f"ref.fa.{n}.64fmi2steps.fmi"
+    assert (tmp_path / (idx.name + ".sa")).exists()
+    qd = c["queries"]["12"]
+    shutil.copy(GOLDEN / "textA" / qd["file"], tmp_path / "q.qry")
+    out = run([BIN / "searchQueries", idx.name, "q.qry", 12, qd["num"]], tmp_path,
+              {"KFMI_BACKEND": "task-mid", "KFMI_ITERS": "1", "KFMI_SA_FILE": idx.name + ".sa"})
+    assert "LOCATE:" in out
+    text = util.read_fasta_text(GOLDEN / "textA" / "ref.fa")
+    reads = util.read_qry(tmp_path / "q.qry", 12)
+    res = [ln.split() for ln in (tmp_path / (idx.name + ".res.gpu")).read_text().splitlines()[1:]]
+    lines = (tmp_path / (idx.name + ".pos.gpu")).read_text().splitlines()
+    assert len(lines) == len(reads) == len(res)
+    for rd, (L, R), ln in zip(reads, res, lines):
+        f = [int(x) for x in ln.split()]
+        assert f[0] == int(R) - int(L) == len(f) - 1
+        want = bytes(b"ACGT"[util.code_of(ch)] for ch in rd.tobytes()).decode()
+        for p in f[1:]:
+            assert text[p:p + 12] == want
