@@ -529,7 +529,9 @@ static hipError_t launch_task(const SearchLaunch& a)
 {
   if (a.maxw) {
     const uint64_t blocks = (a.num + 255) / 256;
-    const size_t lds = 4 * (size_t) stage_slot_bytes(a.m);
+    /* KFMI_LDS_PAD (experiment): extra LDS per workgroup to cap resident waves */
+    const char* pe = getenv("KFMI_LDS_PAD");
+    const size_t lds = 4 * (size_t) stage_slot_bytes(a.m) + (pe ? (size_t) atoi(pe) : 0);
     if (a.maxw == 8)
       hipLaunchKernelGGL((task_kernel<G, 1, 8>), dim3((uint32_t) blocks), dim3(256), lds, a.st, a.ix, a.qp, a.ascii,
                          a.m, a.num, a.steps, a.nwords, a.res);
