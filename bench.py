@@ -66,6 +66,8 @@ def parse():
     p.add_argument("--sa-rate", type=int, default=32,
                    help="SA sampling rate of the index for the locate leg (0 = no locate)")
     p.add_argument("--locate-steps", type=int, default=3)
+    p.add_argument("--no-config1", dest="config1", action="store_false",
+                   help="skip the 64 Mbase / 2^20-read leg (BASELINE config #1)")
     return p.parse_args()
 
 
@@ -168,6 +170,28 @@ def cpu_reference_baseline(idx, reads, ns, k, d, thr, res_gpu):
                       f"searchQueries.c + fmIndexCPUBaseline.c built from its sources, OMP threads={thr}, "
                       f"5 iterations, TIME {t_iter:.3f} s/iteration",
             "parity_with_gpu": ok}
+
+
+def config1_leg(backend: str, thr: int, steps: int = 5) -> dict:
+    """BASELINE config #1 (64 Mbase recipe text, 2^20 x 100 bp reads): GPU
+    search rate on the md5-pinned inputs and the reference's CPU searcher on
+    the same reads (its 'plumbing' config)."""
+    text, rng = synth.text_64m()
+    idx = K.Index.build(text, k=2, d=64, gpu=True)
+    reads = synth.reads_64m(text, rng)
+    q = K.Queries.from_array(reads)
+    r = K.Results.alloc(reads.shape[0])
+    wall, lf, tot = time_backend(idx, q, r, backend, steps, 2)
+    res = r.array().copy()
+    out = {"backend": backend, "mqps": round(reads.shape[0] * steps / wall / 1e6, 2), "lf_ms": round(lf, 3),
+           "results_md5_pinned": synth.results_md5(res) == synth.MD5["res64"]}
+    ref = cpu_reference_baseline(idx, reads, reads.shape[0], 2, 64, thr, res)
+    if ref:
+        out["cpu_reference"] = {k: ref[k] for k in ("value", "unit", "cores", "parity_with_gpu")}
+    q.close()
+    r.close()
+    idx.close()
+    return out
 
 
 def time_backend(idx, q, r, backend, steps, warmup):
@@ -388,6 +412,12 @@ def main():
             else:
                 extra["cpu_port"] = port
             cpu["cpu_model"] = cpu_model()
+            if a.config1:
+                try:
+                    extra["config1_64mbase"] = config1_leg(a.backend, thr)
+                    log(f"config #1 {extra['config1_64mbase']}")
+                except K.KfmiError as e:
+                    extra["config1_64mbase"] = {"error": str(e)}
             # single-thread rate of the restatement on a small slice
             n1 = min(100_000, ns)
             t = time.perf_counter()

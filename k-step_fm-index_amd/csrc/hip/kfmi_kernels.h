@@ -1,0 +1,306 @@
+/*
+ * kfmi_kernels.h -- the search-side kernels and their launchers, shared by
+ * kfmi_search.hip (host logic, dispatch) and the kfmi_inst_*.hip translation
+ * units that instantiate dispatch_one<K, NB, LAY> for one (K, layout) each, so
+ * the ~700 kernel instantiations compile in parallel.
+ */
+#ifndef KFMI_KERNELS_H_
+#define KFMI_KERNELS_H_
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdlib.h>
+
+#include "kfmi_device.h"
+#include "kfmi_coop.h"
+#include "kfmi_locate.h"
+
+namespace kfmi {
+
+/* ------------------------------------------------------------------------ */
+/* task-per-query kernel: one thread owns QPT queries (both ends each)       */
+/* MAXW == 0: codes come from the pack kernel's words (qp);                 */
+/* MAXW  > 0: the thread reads its own ASCII row once and keeps the codes   */
+/*            in MAXW registers (fused packing, no pack launch, no qp).     */
+/* ------------------------------------------------------------------------ */
+
+template <class G, int QPT, int MAXW>
+__global__ __launch_bounds__(256) void task_kernel(IdxArgs ix, const uint32_t* __restrict__ qp,
+                                                   const uint8_t* __restrict__ ascii, uint32_t m, uint64_t num,
+                                                   uint32_t steps, uint32_t nwords, uint32_t* __restrict__ res)
+{
+  constexpr int SPW = G::SPW;
+  constexpr int CW = MAXW > 0 ? MAXW : 1;
+  static_assert(MAXW == 0 || QPT == 1, "fused packing: one query per thread");
+  const uint64_t base = (uint64_t) blockIdx.x * (256 * QPT) + threadIdx.x;
+  uint32_t cw[QPT][CW];
+  if constexpr (MAXW > 0) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t stage[];
+    stage_query_codes<MAXW>(ascii, num, m, stage, cw[0]);   /* whole block, before any exit */
+  }
+  if (base >= num) return;
+  uint64_t q[QPT];
+  uint32_t L[QPT], R[QPT];
+#pragma unroll
+  for (int i = 0; i < QPT; ++i) {
+    q[i] = base + (uint64_t) i * 256;
+    if (q[i] >= num) q[i] = base;   /* duplicate work for the tail, never stored twice */
+    L[i] = 0;
+    R[i] = ix.bwtsize;
+  }
+  uint32_t skip = 0;
+  if (ix.ftab && steps >= ix.ftab_steps) {   /* wave-uniform: jump start from the ftab */
+    skip = ix.ftab_steps;
+#pragma unroll
+    for (int i = 0; i < QPT; ++i) {
+      uint32_t w0;
+      if constexpr (MAXW > 0) w0 = cw[i][0];
+      else w0 = qp[q[i]];
+      const uint2 lr = ix.ftab[w0 & ix.ftab_mask];
+      L[i] = lr.x;
+      R[i] = lr.y;
+    }
+  }
+  for (uint32_t w = 0; w < nwords; ++w) {
+    uint32_t word[QPT];
+#pragma unroll
+    for (int i = 0; i < QPT; ++i) {
+      if constexpr (MAXW > 0) {
+        word[i] = cw[i][0];
+#pragma unroll
+        for (int k = 0; k + 1 < CW; ++k) cw[i][k] = cw[i][k + 1];
+      } else {
+        word[i] = qp[(uint64_t) w * num + q[i]];
+      }
+    }
+    const uint32_t left = steps - w * SPW;
+#pragma unroll
+    for (int j = 0; j < SPW; ++j) {
+      if ((uint32_t) j >= left) continue;   /* only the last word is partial (wave-uniform) */
+      if (w * SPW + j < skip) continue;      /* steps covered by the ftab (wave-uniform) */
+      uint32_t c[QPT];
+#pragma unroll
+      for (int i = 0; i < QPT; ++i) c[i] = (word[i] >> (2 * G::K * j)) & (uint32_t) (G::NC - 1);
+      if constexpr (G::SMALL) {
+        Blk<G> kl[QPT], kr[QPT];
+        if (w * SPW + j >= ix.nt_from) {   /* wave-uniform: deep steps stream non-temporally */
+#pragma unroll
+          for (int i = 0; i < QPT; ++i) fetch_block<G, true>(ix, L[i] / (uint32_t) G::D, c[i], kl[i]);
+#pragma unroll
+          for (int i = 0; i < QPT; ++i) {
+            const uint32_t br = R[i] / (uint32_t) G::D;
+            if (br != kl[i].b) fetch_block<G, true>(ix, br, c[i], kr[i]);
+            else kr[i] = kl[i];
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < QPT; ++i) fetch_block<G>(ix, L[i] / (uint32_t) G::D, c[i], kl[i]);
+#pragma unroll
+          for (int i = 0; i < QPT; ++i) {
+            const uint32_t br = R[i] / (uint32_t) G::D;
+            if (br != kl[i].b) fetch_block<G>(ix, br, c[i], kr[i]);
+            else kr[i] = kl[i];
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < QPT; ++i) {
+          uint32_t sx[2 * G::K];
+          plane_xor<G::K>(c[i], sx);
+          L[i] = lf_from_block<G>(ix, kl[i], L[i], c[i], sx);
+          R[i] = lf_from_block<G>(ix, kr[i], R[i], c[i], sx);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < QPT; ++i) {
+          uint32_t sx[2 * G::K];
+          plane_xor<G::K>(c[i], sx);
+          L[i] = lf_stream<G>(ix, L[i], c[i], sx);
+          R[i] = lf_stream<G>(ix, R[i], c[i], sx);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < QPT; ++i) {
+    const uint64_t qi = base + (uint64_t) i * 256;
+    if (qi < num) *reinterpret_cast<uint2*>(res + 2 * qi) = make_uint2(L[i], R[i]);
+  }
+}
+
+/* ftab construction: [L, R) of every code stream v of ftab_steps K-steps
+ * (the search's own first steps, from [0, n+1)). */
+template <class G>
+__global__ __launch_bounds__(256) void ftab_build_kernel(IdxArgs ix, uint32_t fsteps, uint64_t n,
+                                                         uint2* __restrict__ out)
+{
+  /* grid-stride: 4^16 entries exceed the 2^32 work-items of one dispatch */
+  for (uint64_t v = (uint64_t) blockIdx.x * 256 + threadIdx.x; v < n; v += (uint64_t) gridDim.x * 256) {
+    uint32_t L = 0, R = ix.bwtsize;
+    for (uint32_t t = 0; t < fsteps; ++t) {
+      const uint32_t c = (uint32_t) (v >> (2 * G::K * t)) & (uint32_t) (G::NC - 1);
+      uint32_t sx[2 * G::K];
+      plane_xor<G::K>(c, sx);
+      L = lf_stream<G>(ix, L, c, sx);
+      R = lf_stream<G>(ix, R, c, sx);
+    }
+    out[v] = make_uint2(L, R);
+  }
+}
+
+/* distinct d-blocks touched per step (1 if L/d == R/d else 2): the
+ * dedup-aware algorithmic traffic of SURVEY 8(d).  Same LF math as the
+ * task kernel; a separate launch so the timed kernels carry no counters. */
+template <class G>
+__global__ __launch_bounds__(256) void count_blocks_kernel(IdxArgs ix, const uint32_t* __restrict__ qp, uint64_t num,
+                                                           uint32_t steps, uint32_t nwords,
+                                                           unsigned long long* __restrict__ total)
+{
+  const uint64_t q = (uint64_t) blockIdx.x * 256 + threadIdx.x;
+  uint32_t cnt = 0;
+  if (q < num) {
+    uint32_t L = 0, R = ix.bwtsize;
+    for (uint32_t t = 0; t < steps; ++t) {
+      const uint32_t word = qp[(uint64_t) (t / G::SPW) * num + q];
+      const uint32_t c = (word >> (2 * G::K * (t % G::SPW))) & (uint32_t) (G::NC - 1);
+      uint32_t sx[2 * G::K];
+      plane_xor<G::K>(c, sx);
+      cnt += (L / (uint32_t) G::D == R / (uint32_t) G::D) ? 1u : 2u;
+      L = lf_stream<G>(ix, L, c, sx);
+      R = lf_stream<G>(ix, R, c, sx);
+    }
+  }
+  /* wave reduction, one atomic per wave */
+  for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+  if ((threadIdx.x & 63) == 0) atomicAdd(total, (unsigned long long) cnt);
+}
+
+/* ------------------------------------------------------------------------ */
+/* dispatch tables                                                          */
+/* ------------------------------------------------------------------------ */
+
+struct SearchLaunch {
+  hipStream_t st;
+  IdxArgs ix;
+  const uint32_t* qp;
+  const uint8_t* ascii;   /* fused packing: ASCII rows of m bases */
+  uint32_t m;
+  int maxw;               /* 0: packed words in qp; 8/16: fused packing */
+  uint64_t num;
+  uint32_t steps, nwords;
+  uint32_t* res;
+  /* locate */
+  const uint32_t* sa;
+  uint32_t sa_log2;
+  const uint64_t* off;
+  const uint32_t* owner;
+  uint64_t total;
+  uint32_t* pos;
+  /* ftab build */
+  uint2* ftab_out;
+  uint32_t ftab_steps;
+  uint64_t ftab_n;
+};
+
+static inline int task_qpt(void)
+{
+  const char* e = getenv("KFMI_QPT");
+  int v = e ? atoi(e) : 1;
+  return v == 2 ? 2 : 1;
+}
+
+template <class G>
+static hipError_t launch_task(const SearchLaunch& a)
+{
+  if (a.maxw) {
+    const uint64_t blocks = (a.num + 255) / 256;
+    /* KFMI_LDS_PAD (experiment): extra LDS per workgroup to cap resident waves */
+    const char* pe = getenv("KFMI_LDS_PAD");
+    const size_t lds = 4 * (size_t) stage_slot_bytes(a.m) + (pe ? (size_t) atoi(pe) : 0);
+    if (a.maxw == 8)
+      hipLaunchKernelGGL((task_kernel<G, 1, 8>), dim3((uint32_t) blocks), dim3(256), lds, a.st, a.ix, a.qp, a.ascii,
+                         a.m, a.num, a.steps, a.nwords, a.res);
+    else
+      hipLaunchKernelGGL((task_kernel<G, 1, 16>), dim3((uint32_t) blocks), dim3(256), lds, a.st, a.ix, a.qp,
+                         a.ascii, a.m, a.num, a.steps, a.nwords, a.res);
+  } else if (task_qpt() == 2) {
+    const uint64_t blocks = (a.num + 511) / 512;
+    hipLaunchKernelGGL((task_kernel<G, 2, 0>), dim3((uint32_t) blocks), dim3(256), 0, a.st, a.ix, a.qp, a.ascii,
+                       a.m, a.num, a.steps, a.nwords, a.res);
+  } else {
+    const uint64_t blocks = (a.num + 255) / 256;
+    hipLaunchKernelGGL((task_kernel<G, 1, 0>), dim3((uint32_t) blocks), dim3(256), 0, a.st, a.ix, a.qp, a.ascii,
+                       a.m, a.num, a.steps, a.nwords, a.res);
+  }
+  return hipGetLastError();
+}
+
+template <class G>
+static hipError_t launch_coop(const SearchLaunch& a)
+{
+  return coop_launch<G>(a.st, a.ix, a.qp, a.ascii, a.m, a.maxw, a.num, a.steps, a.nwords, a.res);
+}
+
+template <class G>
+static hipError_t launch_count(const SearchLaunch& a, unsigned long long* d_total)
+{
+  const uint64_t blocks = (a.num + 255) / 256;
+  hipLaunchKernelGGL((count_blocks_kernel<G>), dim3((uint32_t) blocks), dim3(256), 0, a.st, a.ix, a.qp, a.num,
+                     a.steps, a.nwords, d_total);
+  return hipGetLastError();
+}
+
+
+/* K in {1,2}; d in {32,64,128,192,256,448,960} */
+#define KFMI_FOR_NB(X, K, LAY) \
+  X(K, 1, LAY) X(K, 2, LAY) X(K, 4, LAY) X(K, 6, LAY) X(K, 8, LAY) X(K, 14, LAY) X(K, 30, LAY)
+
+
+/* Locate: enough lanes to fill every CU (8 workgroups of 256 per CU), each
+ * lane walking slot after slot. */
+template <class G>
+static hipError_t launch_locate(const SearchLaunch& a)
+{
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+    cus = 256;
+  uint64_t blocks = (a.total + 255) / 256;
+  if (blocks > (uint64_t) cus * 8) blocks = (uint64_t) cus * 8;
+  hipLaunchKernelGGL((locate_kernel<G>), dim3((uint32_t) blocks), dim3(256), 0, a.st, a.ix, a.sa, a.sa_log2, a.owner,
+                     a.total, a.pos);
+  return hipGetLastError();
+}
+
+template <class G>
+static hipError_t launch_ftab(const SearchLaunch& a)
+{
+  const uint64_t blocks = (a.ftab_n + 255) / 256;
+  hipLaunchKernelGGL((ftab_build_kernel<G>), dim3((uint32_t) (blocks < (1u << 20) ? blocks : (1u << 20))), dim3(256), 0,
+                     a.st, a.ix, a.ftab_steps, a.ftab_n, a.ftab_out);
+  return hipGetLastError();
+}
+
+enum class Op { Task, Coop, Count, Locate, Ftab };
+
+/* Defined here, instantiated once per (K, NB, LAY) in kfmi_inst_*.hip. */
+template <int K, int NB, int LAY>
+hipError_t dispatch_one(Op op, const SearchLaunch& a, unsigned long long* d_total)
+{
+  using G = Geo<K, NB, LAY>;
+  switch (op) {
+    case Op::Task: return launch_task<G>(a);
+    case Op::Coop: return launch_coop<G>(a);
+    case Op::Locate: return launch_locate<G>(a);
+    case Op::Ftab: return launch_ftab<G>(a);
+    default: return launch_count<G>(a, d_total);
+  }
+}
+
+#define KFMI_INSTANTIATE(KK, NBV, LAYV) \
+  template hipError_t dispatch_one<KK, NBV, LAYV>(Op, const SearchLaunch&, unsigned long long*);
+#define KFMI_EXTERN(KK, NBV, LAYV) \
+  extern template hipError_t dispatch_one<KK, NBV, LAYV>(Op, const SearchLaunch&, unsigned long long*);
+
+}  // namespace kfmi
+
+#endif  // KFMI_KERNELS_H_

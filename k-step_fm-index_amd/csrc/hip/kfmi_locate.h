@@ -55,46 +55,6 @@ __device__ __forceinline__ uint32_t lf_row(const IdxArgs& ix, uint32_t X)
   return lf_stream<G>(ix, X, c, sx);
 }
 
-// Positions each query reports: min(R - L, max_occ) (max_occ 0 = all).  The
-// count array has num + 1 slots and the last one is 0, so the exclusive scan's
-// last element is the total.
-__global__ __launch_bounds__(256) void loc_count_kernel(const uint32_t* __restrict__ res, uint64_t num,
-                                                        uint32_t max_occ, uint64_t* __restrict__ cnt)
-{
-  const uint64_t q = (uint64_t) blockIdx.x * 256 + threadIdx.x;
-  if (q > num) return;
-  uint64_t c = 0;
-  if (q < num) {
-    const uint2 lr = *reinterpret_cast<const uint2*>(res + 2 * q);
-    c = lr.y > lr.x ? (uint64_t) (lr.y - lr.x) : 0u;
-    if (max_occ && c > max_occ) c = max_occ;
-  }
-  cnt[q] = c;
-}
-
-// Owner of each output slot without a per-slot search: every query with at
-// least one position writes its id at its first slot (owner[] zeroed first),
-// and an inclusive max-scan spreads it over the query's slots.
-__global__ __launch_bounds__(256) void loc_heads_kernel(const uint64_t* __restrict__ cnt,
-                                                        const uint64_t* __restrict__ off, uint64_t num,
-                                                        uint32_t* __restrict__ owner)
-{
-  const uint64_t q = (uint64_t) blockIdx.x * 256 + threadIdx.x;
-  if (q < num && cnt[q]) owner[off[q]] = (uint32_t) q;
-}
-
-// First row of every output slot, in place over the owner array:
-// rows[i] = L of its query + the slot's rank inside the query.
-__global__ __launch_bounds__(256) void loc_rows_kernel(const uint32_t* __restrict__ res,
-                                                       const uint64_t* __restrict__ off, uint64_t total,
-                                                       uint32_t* __restrict__ own_rows)
-{
-  for (uint64_t i = (uint64_t) blockIdx.x * 256 + threadIdx.x; i < total; i += (uint64_t) gridDim.x * 256) {
-    const uint32_t q = own_rows[i];   /* grid-stride: a batch may hold more than 2^32 positions */
-    own_rows[i] = res[2 * (uint64_t) q] + (uint32_t) (i - off[q]);
-  }
-}
-
 // Each lane walks slot after slot (i, i + stride, ...).  Per iteration a lane
 // either reads its row's sample (sampled row), stops at a '$' row, or takes
 // one LF_K step; the sample load and the step's line load of the other lanes
