@@ -376,11 +376,16 @@ def main():
                     for _ in range(a.e2e_steps):
                         out = K.search_stream(idx, src, out=dst)
                     w = (time.perf_counter() - t) / a.e2e_steps
+                    lt = K.last_timing()
                     e2e[kind] = {"mqps": round(reads.shape[0] / w / 1e6, 2), "ms": round(w * 1e3, 3),
+                                 "host_ms": round(lt["pack_ms"], 3), "wait_ms": round(lt["lf_ms"], 3),
                                  "results_equal": bool(np.array_equal(out, res))}
-                e2e["chunk_queries"] = int(os.environ.get("KFMI_STREAM_CHUNK", 1 << 21))
-                e2e["what"] = "kfmi_search_stream: ASCII reads in host memory -> results in host memory, " \
-                              "chunked H2D / pack+LF / D2H overlapped on 3 HIP streams"
+                host_pack = os.environ.get("KFMI_STREAM_HOSTPACK", "1") != "0"
+                e2e["chunk_queries"] = int(os.environ.get("KFMI_STREAM_CHUNK", (1 << 19) if host_pack else (1 << 16)))
+                e2e["host_pack"] = host_pack
+                e2e["what"] = "kfmi_search_stream: ASCII reads in host memory -> results in host memory; " \
+                              "host 2-bit packing (qpack.c, KFMI_HOST_THREADS) / code-word H2D / LF / D2H " \
+                              "of successive chunks overlapped on 3 HIP streams"
                 extra["end_to_end"] = e2e
                 log(f"end to end {e2e}")
                 del pin, pout

@@ -180,14 +180,25 @@ int32_t kfmi_count_blocks(void *index, void *queries, uint64_t *blocks);
 /* Streamed search from host memory: `num` queries of `size`
  * ASCII bytes at `ascii`, results [L0,R0,L1,R1,...] into `results` (2*num
  * u32).  The index must already be on the device (transferCPUtoGPU(index,
- * NULL, NULL)).  Chunks of `chunk` queries (0: KFMI_STREAM_CHUNK, else 2^21)
- * rotate over 3 HIP streams so that query H2D, packing + LF and result D2H of
- * successive chunks overlap.  Pinned buffers (kfmi_host_alloc) are DMA'd
- * directly; pageable ones are staged through pinned buffers by
- * KFMI_COPY_THREADS host threads (default 8).  Blocking; kfmi_last_timing's
- * total is the wall time of the whole call.  Results equal kfmi_search's. */
+ * NULL, NULL)).  Chunks of `chunk` queries (0: KFMI_STREAM_CHUNK, else 2^19,
+ * or 2^16 without host packing) rotate over 3 HIP streams so that host
+ * packing, H2D, LF and result D2H of successive chunks overlap.  By default
+ * the host packs each chunk to code words (kfmi_pack_queries) and PCIe
+ * carries 4 bytes per 16 bases; KFMI_STREAM_HOSTPACK=0 sends ASCII (pinned:
+ * DMA'd directly; pageable: staged through pinned buffers) and packs on the
+ * device.  Host work runs on KFMI_HOST_THREADS threads (default min(16,
+ * cores)).  Blocking; kfmi_last_timing: total = wall time of the call, pack =
+ * host packing / staging time, lf = time blocked on chunks in flight.
+ * Results equal kfmi_search's. */
 int32_t kfmi_search_stream(void *index, const char *ascii, uint64_t num, uint32_t size,
                            uint32_t *results, uint64_t chunk);
+/* Packs num reads of `size` bases (plain layout q*size, as loadQueries keeps
+ * them, common.c:163-173) into the 2-bit code words the search consumes, on the
+ * host: word-major, word w of read q at words[w * num + q], ceil(size/16) words
+ * per read, the base at reversed index r (base size-1-r) at bits 2r..2r+1 of
+ * the read's bit string (fmIndexCPUBaseline.c:200-226 order; K-independent).
+ * kfmi_search_stream uses it to send 4 bytes per 16 bases over PCIe. */
+int32_t kfmi_pack_queries(const char *ascii, uint64_t num, uint32_t size, uint32_t *words);
 /* Pinned (page-locked) host memory for query/result buffers. */
 int32_t kfmi_host_alloc(uint64_t bytes, void **p);
 int32_t kfmi_host_free(void *p);

@@ -85,6 +85,10 @@ void           kfmi_set_last_error(int32_t e);
 
 /* sampled suffix array (fmi_index.c): (re)allocates h_sa for `rate` */
 int32_t kfmi_sa_alloc(kfmi_fmi_t *f, uint32_t rate);
+
+/* qpack.c: ASCII rows -> word-major 2-bit code words (word w of row q at
+ * out[w * ostride + q]; ceil(m/16) words per row) */
+void kfmi_pack_rows(const uint8_t *ascii, uint64_t n, uint32_t m, uint32_t *out, uint64_t ostride);
 int     kfmi_sa_rate_ok(uint32_t rate);
 
 /* builders with SA sampling (fmi_build.c, kfmi_build.hip) */

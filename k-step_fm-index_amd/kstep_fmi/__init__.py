@@ -99,6 +99,7 @@ def load() -> ctypes.CDLL:
         "kfmi_host_alloc": (i32, [u64, pvp]),
         "kfmi_host_free": (i32, [vp]),
         "kfmi_stream_release": (i32, []),
+        "kfmi_pack_queries": (i32, [vp, u64, u32, vp]),
         "kfmi_build_index_ex": (i32, [vp, u64, u32, u32, u32, i32, pvp]),
         "kfmi_set_ftab": (i32, [u32]),
         "kfmi_index_sa": (i32, [vp, pvp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32)]),
@@ -409,6 +410,16 @@ def pinned_empty(shape, dtype=np.uint8) -> np.ndarray:
     n = int(np.prod(shape)) * dt.itemsize
     owner = _Pinned(max(n, 1))
     return _owned_view(owner.ptr.value, n, dt, owner).reshape(shape)
+
+
+def pack_queries(reads: np.ndarray) -> np.ndarray:
+    """Host 2-bit packing of uint8 [N, m] reads (kfmi_pack_queries): uint32
+    [ceil(m/16), N], word-major, the words the search consumes."""
+    reads = np.ascontiguousarray(reads, dtype=np.uint8)
+    n, m = reads.shape
+    out = np.empty(((m + 15) // 16, n), dtype=np.uint32)
+    _check(load().kfmi_pack_queries(reads.ctypes.data, n, m, out.ctypes.data), "kfmi_pack_queries")
+    return out
 
 
 def search_stream(index: Index, reads: np.ndarray, out: np.ndarray | None = None, chunk: int = 0) -> np.ndarray:

@@ -1,0 +1,16 @@
+#!/bin/bash
+# Round-1 session ZD: host-packed streaming (default) --
+# full GPU suite + smoke + default bench.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-/root/repo}
+OUT=$R/gpurun_out
+mkdir -p $OUT
+export TMPDIR=/tmp
+cd $R
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/gpu_tests_zd.log 2>&1 || { echo tests_failed; tail -40 $OUT/gpu_tests_zd.log; exit 21; }
+tail -1 $OUT/gpu_tests_zd.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke_zd.log 2>&1 || { tail -20 $OUT/smoke_zd.log; exit 22; }
+tail -1 $OUT/smoke_zd.log
+cd /tmp
+timeout -k 10 700 python3 $R/bench.py > $OUT/bench_r01zd.json 2> $OUT/bench_r01zd.log || { tail -20 $OUT/bench_r01zd.log; exit 31; }
+python3 -c "import json; d=json.load(open('$OUT/bench_r01zd.json')); v=d['variants']; print(v.get('end_to_end'), d['value'], d['roofline']['achieved'], d['roofline']['frac'], d['cpu_baseline']['value'], v.get('config1_64mbase'), {k: (x.get('mqps') if isinstance(x, dict) else x) for k, x in v.items()})"

@@ -168,6 +168,22 @@ int main(int argc, char **argv)
     CHECK(loadResults(p, &rl) == 0, "reload results");
     freeResults(&rs); freeResults(&rl);
   }
+  /* 6. host query packing on exactly-sized buffers, every length 1..300 */
+  for (uint32_t mm = 1; mm <= 300; mm++) {
+    const uint32_t nr = 3, nw = (mm + 15) / 16;
+    char *a = malloc((size_t) nr * mm);
+    uint32_t *w = malloc((size_t) nw * nr * 4);
+    for (uint32_t i = 0; i < nr * mm; i++) a[i] = "ACGTNacgt"[(i * 7u + mm) % 9u];
+    CHECK(a && w && kfmi_pack_queries(a, nr, mm, w) == 0, "pack m=%u", mm);
+    /* base 0 of read 1 (reversed index mm-1) sits at bits 2(mm-1) of its string */
+    const uint32_t r = mm - 1, c = base2index((uint32_t) (unsigned char) a[mm]);
+    CHECK(((w[(r / 16) * nr + 1] >> (2 * (r % 16))) & 3u) == c, "pack first base m=%u", mm);
+    CHECK(r % 16 == 15 || (w[(r / 16) * nr + 1] >> (2 * (r % 16) + 2)) == 0, "pack zero tail m=%u", mm);
+    free(a);
+    free(w);
+  }
+  CHECK(kfmi_pack_queries(NULL, 1, 4, NULL) == KFMI_E_BAD_ARGUMENT, "pack null");
+
   freeIndex(&idx); freeIndex(&t101); freeIndex(&t200); freeIndex(&t201);
   printf("%s %d checks, %d failures\n", failures ? "FAILED" : "OK", checks, failures);
   return failures ? 1 : 0;

@@ -1,5 +1,6 @@
 """Streamed search from host memory (kfmi_search_stream): chunked
-H2D / pack + LF / D2H overlap on three HIP streams must return exactly what the
+H2D / pack + LF / D2H overlap on three HIP streams, with the reads packed on the
+host (default) or on the device, must return exactly what the
 resident-batch path (kfmi_search) and the CPU oracle return, for ragged chunk
 sizes and for pinned and pageable host buffers."""
 import numpy as np
@@ -26,10 +27,14 @@ def setup(kfmi_mod):
     return K, idx, reads
 
 
+@pytest.mark.parametrize("hostpack", ["1", "0"])
 @pytest.mark.parametrize("backend", ["task-mid", "coop-mid", "task", "coop-ac", "task-ac128"])
 @pytest.mark.parametrize("chunk", [0, 1_000, 4_099])
-def test_stream_equals_batch_and_oracle(setup, oracle_mod, backend, chunk):
+def test_stream_equals_batch_and_oracle(setup, oracle_mod, backend, chunk, hostpack, monkeypatch):
+    """hostpack 1 (default): code words packed on the host (qpack.c) and sent
+    over PCIe; 0: ASCII sent and packed on the device."""
     K, idx, reads = setup
+    monkeypatch.setenv("KFMI_STREAM_HOSTPACK", hostpack)
     want = K.search_array(idx, reads, backend)
     got = K.search_stream(idx, reads, chunk=chunk)
     assert np.array_equal(got, want)
@@ -38,8 +43,10 @@ def test_stream_equals_batch_and_oracle(setup, oracle_mod, backend, chunk):
         assert np.array_equal(got, ores)
 
 
-def test_stream_pinned_buffers(setup):
+@pytest.mark.parametrize("hostpack", ["1", "0"])
+def test_stream_pinned_buffers(setup, hostpack, monkeypatch):
     K, idx, reads = setup
+    monkeypatch.setenv("KFMI_STREAM_HOSTPACK", hostpack)
     K.set_backend("task-mid")
     K.transfer_to_gpu(idx, None, None)
     want = K.search_array(idx, reads)
@@ -53,8 +60,10 @@ def test_stream_pinned_buffers(setup):
     assert K.last_timing()["total_ms"] > 0
 
 
-def test_stream_k1_and_150bp(kfmi_mod, oracle_mod):
+@pytest.mark.parametrize("hostpack", ["1", "0"])
+def test_stream_k1_and_150bp(kfmi_mod, oracle_mod, hostpack, monkeypatch):
     K = kfmi_mod
+    monkeypatch.setenv("KFMI_STREAM_HOSTPACK", hostpack)
     K.set_device(0)
     rng = np.random.default_rng(5)
     text = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=50_000).tobytes()
