@@ -547,13 +547,8 @@ static int32_t host_entries_for(const kfmi_fmi_t* f, int lay, kfmi_fmi_t** owned
   *owned = nullptr;
   *use = f;
   if (lay == LAY_INTER || lay == LAY_PACKED || lay == LAY_MID) {
-    if (f->tag == 101) return KFMI_SUCCESS;
-    if (f->tag == 100) {
-      int32_t e = kfmi_transform_interleave((void*) f, (void**) owned);
-      if (e) return e;
-      *use = *owned;
-      return KFMI_SUCCESS;
-    }
+    /* tag 101 as is; tag 100 is interleaved on the device (upload_entries) */
+    if (f->tag == 101 || f->tag == 100) return KFMI_SUCCESS;
     return KFMI_INDEX_VER_INTERLEAVE;   /* an AC file cannot feed a plain-counter backend */
   }
   /* AC, AC128 */
@@ -612,6 +607,88 @@ static void free_dev_index(kfmi_dev_index* di)
   delete di;
 }
 
+namespace {
+bool host_pinned(const void* p);
+void par_copy(void* dst, const void* src, uint64_t bytes);
+}  // namespace
+
+/* Large host-to-device copy.  hipMemcpy from pageable memory runs at a few
+ * GB/s; above 256 MB the source is staged through two pinned 64 MB buffers
+ * (filled by the host workers) so that the copy runs at PCIe speed.  Returns
+ * with the copy complete when staged, else queued on `st`. */
+static hipError_t h2d(void* dst, const void* src, uint64_t bytes, hipStream_t st)
+{
+  constexpr uint64_t CH = 64ull << 20;
+  if (bytes < (256ull << 20) || host_pinned(src)) return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st);
+  void* buf[2] = {nullptr, nullptr};
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  hipError_t e = hipSuccess;
+  for (int b = 0; b < 2 && e == hipSuccess; ++b) {
+    e = hipHostMalloc(&buf[b], CH, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ev[b], hipEventDisableTiming);
+  }
+  for (uint64_t off = 0, i = 0; off < bytes && e == hipSuccess; off += CH, ++i) {
+    const int b = (int) (i & 1);
+    if (i >= 2) e = hipEventSynchronize(ev[b]);
+    if (e != hipSuccess) break;
+    const uint64_t len = bytes - off < CH ? bytes - off : CH;
+    par_copy(buf[b], (const uint8_t*) src + off, len);
+    e = hipMemcpyAsync((uint8_t*) dst + off, buf[b], len, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipEventRecord(ev[b], st);
+  }
+  const hipError_t es = hipStreamSynchronize(st);
+  for (int b = 0; b < 2; ++b) {
+    if (ev[b]) (void) hipEventDestroy(ev[b]);
+    if (buf[b]) (void) hipHostFree(buf[b]);
+  }
+  return e != hipSuccess ? e : es;
+}
+
+/* tag-100 -> tag-101 entries (kfmi_transform_interleave's plane order,
+ * transformIndexBitmaps.c) on the device: out word p of an entry is in word
+ * perm[p] of the same entry. */
+constexpr uint32_t KFMI_MAX_ENTRY_WORDS = 160;   /* K <= 2, d <= 960: 2*30*2 + 16 = 136 */
+struct EntryPerm {
+  uint32_t p[KFMI_MAX_ENTRY_WORDS];
+};
+
+__global__ __launch_bounds__(256) void interleave_entries_kernel(const uint32_t* __restrict__ in,
+                                                                 uint32_t* __restrict__ out, uint64_t words,
+                                                                 uint32_t ew, EntryPerm perm)
+{
+  for (uint64_t i = (uint64_t) blockIdx.x * 256 + threadIdx.x; i < words; i += (uint64_t) gridDim.x * 256) {
+    const uint64_t e = i / ew;
+    out[i] = in[e * ew + perm.p[i - e * ew]];
+  }
+}
+
+/* The entries of `src` as tag 101 (plain family) or as stored, into device
+ * memory at dst (`body` bytes). */
+static hipError_t upload_entries(void* dst, const kfmi_fmi_t* src, uint64_t body, hipStream_t st)
+{
+  if (src->tag != 100) return h2d(dst, src->h_index, body, st);
+  const uint32_t ew = src->entry_words, K = src->steps, nb = src->nbitmaps;
+  if (ew > KFMI_MAX_ENTRY_WORDS) return hipErrorInvalidValue;
+  EntryPerm perm;
+  for (uint32_t p = 0; p < ew; ++p) perm.p[p] = p;   /* counters keep their place */
+  for (uint32_t w = 0; w < nb; ++w)
+    for (uint32_t k = 0; k < K; ++k)
+      for (uint32_t t = 0; t < 2; ++t) perm.p[kfmi_plane_index(101, K, nb, k, t, w)] = kfmi_plane_index(100, K, nb, k, t, w);
+  uint32_t* tmp = nullptr;
+  hipError_t e = hipMalloc((void**) &tmp, body ? body : 4);
+  if (e != hipSuccess) return e;
+  e = h2d(tmp, src->h_index, body, st);
+  const uint64_t words = body / 4, blocks = (words + 255) / 256;
+  if (e == hipSuccess && words) {
+    hipLaunchKernelGGL(interleave_entries_kernel, dim3((uint32_t) (blocks < (1u << 20) ? blocks : (1u << 20))),
+                       dim3(256), 0, st, tmp, (uint32_t*) dst, words, ew, perm);
+    e = hipGetLastError();
+  }
+  const hipError_t es = hipStreamSynchronize(st);
+  (void) hipFree(tmp);
+  return e != hipSuccess ? e : es;
+}
+
 /* Device copy of the index's SA samples (locate); none when it has none. */
 static int32_t upload_sa(const kfmi_fmi_t* f, kfmi_dev_index* di, DevCtx* ctx)
 {
@@ -625,7 +702,7 @@ static int32_t upload_sa(const kfmi_fmi_t* f, kfmi_dev_index* di, DevCtx* ctx)
     di->sa = nullptr;
     return KFMI_E_DEVICE_ALLOC;
   }
-  if (hipMemcpyAsync(di->sa, f->h_sa, bytes, hipMemcpyHostToDevice, ctx->st) != hipSuccess ||
+  if (h2d(di->sa, f->h_sa, bytes, ctx->st) != hipSuccess ||
       hipStreamSynchronize(ctx->st) != hipSuccess) {
     (void) hipFree(di->sa);
     di->sa = nullptr;
@@ -681,7 +758,7 @@ static int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx)
     di->ent_bytes = body + 4ull * ew * 2;
     if (hipMalloc((void**) &di->ent, di->ent_bytes) != hipSuccess) return fail(KFMI_E_DEVICE_ALLOC);
     if (lay == LAY_INTER) end_counters(src, pad.data() + 2 * f->nbitmaps * f->steps);
-    if (hipMemcpyAsync(di->ent, src->h_index, body, hipMemcpyHostToDevice, ctx->st) != hipSuccess ||
+    if (upload_entries(di->ent, src, body, ctx->st) != hipSuccess ||
         hipMemcpyAsync((uint8_t*) di->ent + body, pad.data(), 4ull * ew * 2, hipMemcpyHostToDevice, ctx->st) !=
             hipSuccess ||
         hipStreamSynchronize(ctx->st) != hipSuccess)
@@ -699,7 +776,7 @@ static int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx)
       (void) hipFree(tmp);
       return fail(KFMI_E_DEVICE_ALLOC);
     }
-    bool ok = hipMemcpyAsync(tmp, src->h_index, body, hipMemcpyHostToDevice, ctx->st) == hipSuccess &&
+    bool ok = upload_entries(tmp, src, body, ctx->st) == hipSuccess &&
               dispatch_build_ac128(f->steps, f->nbitmaps, tmp, E, nl, di->ent, ctx->st) == hipSuccess &&
               hipStreamSynchronize(ctx->st) == hipSuccess;
     (void) hipFree(tmp);
@@ -730,7 +807,7 @@ static int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx)
       if (d_ext) (void) hipFree(d_ext);
       return fail(KFMI_E_DEVICE_ALLOC);
     }
-    bool ok = hipMemcpyAsync(tmp, src->h_index, body, hipMemcpyHostToDevice, ctx->st) == hipSuccess &&
+    bool ok = upload_entries(tmp, src, body, ctx->st) == hipSuccess &&
               hipMemcpyAsync(d_ext, ext.data(), 8ull * nc, hipMemcpyHostToDevice, ctx->st) == hipSuccess &&
               dispatch_build_mid(f->steps, f->nbitmaps, tmp, E, nl, di->ent, d_ext, d_ext + nc, ctx->st) ==
                   hipSuccess &&
@@ -757,7 +834,7 @@ static int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx)
       return fail(KFMI_E_DEVICE_ALLOC);
     }
     uint32_t over = 0;
-    bool ok = hipMemcpyAsync(tmp, src->h_index, body, hipMemcpyHostToDevice, ctx->st) == hipSuccess &&
+    bool ok = upload_entries(tmp, src, body, ctx->st) == hipSuccess &&
               hipMemcpyAsync((uint8_t*) tmp + body, pad.data(), 4ull * ew, hipMemcpyHostToDevice, ctx->st) ==
                   hipSuccess &&
               hipMemsetAsync(d_over, 0, 4, ctx->st) == hipSuccess &&
@@ -866,7 +943,7 @@ static int32_t upload_queries(kfmi_qrys_t* q, uint32_t K, int dev, DevCtx* ctx)
     free_dev_queries(dq);
     return KFMI_E_DEVICE_ALLOC;
   }
-  if (abytes && (hipMemcpyAsync(dq->ascii, q->h_queries, abytes, hipMemcpyHostToDevice, ctx->st) != hipSuccess ||
+  if (abytes && (h2d(dq->ascii, q->h_queries, abytes, ctx->st) != hipSuccess ||
                  hipStreamSynchronize(ctx->st) != hipSuccess)) {
     free_dev_queries(dq);
     return KFMI_E_KERNEL;
