@@ -1407,13 +1407,15 @@ class HostPool {
     return p;
   }
   int size() const { return (int) th_.size() + 1; }
-  /* fn(i) for i in [0, n) over the workers and the caller; returns when all are done */
+  /* fn(i) for i in [0, n) over the workers and the caller; returns when all are
+   * done.  Calls from several host threads (one per device) take turns. */
   void run(int n, const std::function<void(int)>& fn)
   {
     if (n <= 1 || th_.empty()) {
       for (int i = 0; i < n; ++i) fn(i);
       return;
     }
+    std::lock_guard<std::mutex> turn(run_mu_);
     {
       std::lock_guard<std::mutex> lk(mu_);
       fn_ = &fn;
@@ -1477,7 +1479,7 @@ class HostPool {
     }
   }
   std::vector<std::thread> th_;
-  std::mutex mu_;
+  std::mutex run_mu_, mu_;
   std::condition_variable cv_, done_;
   const std::function<void(int)>* fn_ = nullptr;
   int n_ = 0, next_ = 0, left_ = 0;
