@@ -139,6 +139,21 @@ int32_t     kfmi_search(void *index, void *queries, void *results);
  * (default; KFMI_FTAB sets it process-wide), at most 16, a multiple of K to
  * take effect; per calling thread like the backend. */
 int32_t     kfmi_set_ftab(uint32_t bases);
+/* Device groups (runtime multi-GPU behind the same handles; the reference
+ * picks one GPU at compile time with -DDEVICE, Coop-2Step.cu:256).  With two
+ * or more devices listed -- here or in KFMI_DEVICES=0,1,... -- transferCPUtoGPU
+ * replicates the index on every device and cuts queries and results into
+ * contiguous slices (multiples of 64 reads), searchIndexGPU runs all slices
+ * concurrently (one stream per device) and transferGPUtoCPU gathers them into
+ * h_results; results equal the single-device ones.  A device may be listed
+ * twice (two replicas on one GPU).  n = 0 returns to single-device mode, n = 1
+ * equals kfmi_set_device.  Per calling thread.  kfmi_locate works on group
+ * handles (each device locates its slice); kfmi_count_blocks and
+ * kfmi_search_stream stay single-device (KFMI_E_NOT_IMPLEMENTED / not on
+ * device for group handles). */
+int32_t     kfmi_set_devices(const int32_t *devices, int32_t n);
+/* The device list (returns its length; 0 = single-device mode). */
+int32_t     kfmi_get_devices(int32_t *devices, int32_t cap);
 /* Device-side timing of the last search, from HIP events on the library's
  * stream: total (pack + LF), query packing, and the LF kernel alone (ms). */
 int32_t     kfmi_last_timing(double *ms_total, double *ms_pack, double *ms_lf);

@@ -133,11 +133,14 @@ extern "C" int32_t kfmi_device_count(void)
   return n;
 }
 
+static int group_devices(int* devs);
+
 extern "C" int32_t kfmi_current_device(void)
 {
   if (t_device < 0) {
     const char* e = getenv("KFMI_DEVICE");
-    t_device = e ? atoi(e) : 0;
+    int devs[16];
+    t_device = e ? atoi(e) : (group_devices(devs) == 1 ? devs[0] : 0);
   }
   return t_device;
 }
@@ -713,7 +716,8 @@ static int32_t upload_sa(const kfmi_fmi_t* f, kfmi_dev_index* di, DevCtx* ctx)
   return KFMI_SUCCESS;
 }
 
-static int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx)
+/* Uploads f for `backend` to `dev`: into f->dev, or into *out (group replicas). */
+static int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx, kfmi_dev_index** out = nullptr)
 {
   if (f->steps < 1 || f->steps > 2) return KFMI_E_BAD_ARGUMENT;   /* GPU kernels: K in {1,2} */
   if (!nb_supported(f->nbitmaps)) return KFMI_E_BAD_ARGUMENT;
@@ -859,6 +863,10 @@ static int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx)
       return err;
     }
   }
+  if (out) {
+    *out = di;
+    return KFMI_SUCCESS;
+  }
   if (f->dev) free_dev_index(f->dev);
   f->dev = di;
   return KFMI_SUCCESS;
@@ -882,12 +890,11 @@ static IdxArgs idx_args(const kfmi_dev_index* di)
 /* The ftab of `bases` bases, (re)built on the device from the uploaded layout
  * with the search's own LF steps; sets ix.ftab (null when off or when bases is
  * not a multiple of K). */
-static int32_t use_ftab(kfmi_dev_index* di, DevCtx* ctx, IdxArgs& ix)
+static int32_t use_ftab(kfmi_dev_index* di, hipStream_t st, IdxArgs& ix, uint32_t bases)
 {
   ix.ftab = nullptr;
   ix.ftab_steps = 0;
   ix.ftab_mask = 0;
-  const uint32_t bases = ftab_bases();
   if (!bases || bases % di->K) return KFMI_SUCCESS;
   if (di->ftab_chars != bases) {
     if (di->ftab) (void) hipFree(di->ftab);
@@ -899,13 +906,12 @@ static int32_t use_ftab(kfmi_dev_index* di, DevCtx* ctx, IdxArgs& ix)
       return KFMI_E_DEVICE_ALLOC;
     }
     SearchLaunch a{};
-    a.st = ctx->st;
+    a.st = st;
     a.ix = idx_args(di);
     a.ftab_out = di->ftab;
     a.ftab_steps = bases / di->K;
     a.ftab_n = n;
-    if (dispatch(Op::Ftab, di->K, di->nb, di->layout, a) != hipSuccess ||
-        hipStreamSynchronize(ctx->st) != hipSuccess)
+    if (dispatch(Op::Ftab, di->K, di->nb, di->layout, a) != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
       return KFMI_E_KERNEL;
     di->ftab_chars = bases;
   }
@@ -970,6 +976,279 @@ static hipError_t launch_pack(const kfmi_dev_queries* dq, hipStream_t st)
 }
 
 /* ------------------------------------------------------------------------ */
+/* device groups (SURVEY 8(b) device selection, 8(e) partitioning).  The     */
+/* reference fixes one GPU at compile time (-DDEVICE); KFMI_DEVICES=0,1,...  */
+/* or kfmi_set_devices spreads the same handles over several: the index      */
+/* replicated on every device, the queries cut into contiguous slices        */
+/* (multiples of 64 reads), each device searching its slice on its own       */
+/* stream, results copied back into disjoint slices of h_results.  No        */
+/* exchange between devices on the data path.                               */
+/* ------------------------------------------------------------------------ */
+
+constexpr int KFMI_MAX_GROUP = 16;
+static thread_local int t_ngroup = -1;   /* -1: read KFMI_DEVICES */
+static thread_local int t_group[KFMI_MAX_GROUP];
+
+/* The device list (0 or 1 entry: single-device mode). */
+static int group_devices(int* devs)
+{
+  if (t_ngroup < 0) {
+    t_ngroup = 0;
+    const char* p = getenv("KFMI_DEVICES");
+    while (p && *p && t_ngroup < KFMI_MAX_GROUP) {
+      char* end = nullptr;
+      const long v = strtol(p, &end, 10);
+      if (end == p) break;
+      t_group[t_ngroup++] = (int) v;
+      p = end;
+      while (*p == ',' || *p == ' ') ++p;
+    }
+  }
+  for (int i = 0; i < t_ngroup; ++i) devs[i] = t_group[i];
+  return t_ngroup;
+}
+
+struct GroupIndex {
+  int n = 0, backend = -1;
+  int dev[KFMI_MAX_GROUP] = {};
+  kfmi_dev_index* di[KFMI_MAX_GROUP] = {};
+  hipStream_t st[KFMI_MAX_GROUP] = {};
+  hipEvent_t ev[KFMI_MAX_GROUP][3] = {};
+};
+
+/* queries or results of a group: one contiguous slice per member */
+struct GroupSlices {
+  int n = 0;
+  int dev[KFMI_MAX_GROUP] = {};
+  uint64_t q0[KFMI_MAX_GROUP] = {}, num[KFMI_MAX_GROUP] = {};
+  kfmi_dev_queries* dq[KFMI_MAX_GROUP] = {};
+  uint32_t* d_res[KFMI_MAX_GROUP] = {};
+};
+
+static GroupSlices* group_slices(uint64_t num, const int* devs, int n)
+{
+  GroupSlices* g = new (std::nothrow) GroupSlices();
+  if (!g) return nullptr;
+  g->n = n;
+  uint64_t per = (num + n - 1) / n;
+  per = (per + 63) & ~63ull;
+  for (int i = 0; i < n; ++i) {
+    g->dev[i] = devs[i];
+    const uint64_t a = per * i < num ? per * i : num, b = per * (i + 1) < num ? per * (i + 1) : num;
+    g->q0[i] = a;
+    g->num[i] = b - a;
+  }
+  return g;
+}
+
+static void group_free_index(kfmi_fmi_t* f)
+{
+  GroupIndex* g = (GroupIndex*) f->grp;
+  if (!g) return;
+  for (int i = 0; i < g->n; ++i) {
+    (void) hipSetDevice(g->dev[i]);
+    if (g->st[i]) (void) hipStreamSynchronize(g->st[i]);
+    free_dev_index(g->di[i]);
+    for (int k = 0; k < 3; ++k)
+      if (g->ev[i][k]) (void) hipEventDestroy(g->ev[i][k]);
+    if (g->st[i]) (void) hipStreamDestroy(g->st[i]);
+  }
+  delete g;
+  f->grp = nullptr;
+}
+
+static void free_dev_queries(kfmi_dev_queries* dq);
+
+static void group_free_queries(kfmi_qrys_t* q)
+{
+  GroupSlices* g = (GroupSlices*) q->grp;
+  if (!g) return;
+  for (int i = 0; i < g->n; ++i) free_dev_queries(g->dq[i]);
+  delete g;
+  q->grp = nullptr;
+}
+
+static void group_free_results(kfmi_res_t* r)
+{
+  GroupSlices* g = (GroupSlices*) r->grp;
+  if (!g) return;
+  for (int i = 0; i < g->n; ++i)
+    if (g->d_res[i]) {
+      (void) hipSetDevice(g->dev[i]);
+      (void) hipFree(g->d_res[i]);
+    }
+  delete g;
+  r->grp = nullptr;
+}
+
+static int32_t upload_queries(kfmi_qrys_t* q, uint32_t K, int dev, DevCtx* ctx);
+
+static int32_t group_transfer(kfmi_fmi_t* f, kfmi_qrys_t* q, kfmi_res_t* r, const int* devs, int n)
+{
+  const int backend = kfmi_backend();
+  int32_t err = KFMI_SUCCESS;
+  if (f) {
+    GroupIndex* g = (GroupIndex*) f->grp;
+    bool same = g && g->backend == backend && g->n == n;
+    for (int i = 0; same && i < n; ++i) same = g->dev[i] == devs[i];
+    if (!same) {
+      group_free_index(f);
+      g = new (std::nothrow) GroupIndex();
+      if (!g) return KFMI_E_ALLOCATING_FMI;
+      g->n = n;
+      g->backend = backend;
+      f->grp = g;
+      for (int i = 0; i < n && !err; ++i) {
+        g->dev[i] = devs[i];
+        DevCtx* ctx = nullptr;
+        err = ctx_for(devs[i], &ctx);
+        if (!err) err = upload_index(f, backend, devs[i], ctx, &g->di[i]);
+        if (!err && hipStreamCreateWithFlags(&g->st[i], hipStreamNonBlocking) != hipSuccess) err = KFMI_E_NO_DEVICE;
+        for (int k = 0; k < 3 && !err; ++k)
+          if (hipEventCreate(&g->ev[i][k]) != hipSuccess) err = KFMI_E_NO_DEVICE;
+      }
+      if (err) {
+        group_free_index(f);
+        return err;
+      }
+    }
+    if (f->dev) {   /* one mode per handle: the single-device copy goes */
+      free_dev_index(f->dev);
+      f->dev = nullptr;
+    }
+  }
+  if (q) {
+    if (!f) return KFMI_E_BAD_ARGUMENT;
+    group_free_queries(q);
+    if (q->dev) {
+      free_dev_queries(q->dev);
+      q->dev = nullptr;
+    }
+    GroupSlices* g = group_slices(q->num, devs, n);
+    if (!g) return KFMI_E_ALLOCATING_MFASTA;
+    q->grp = g;
+    for (int i = 0; i < n && !err; ++i) {
+      DevCtx* ctx = nullptr;
+      err = ctx_for(devs[i], &ctx);
+      kfmi_qrys_t sh{};
+      sh.num = g->num[i];
+      sh.size = q->size;
+      sh.h_queries = q->h_queries + g->q0[i] * q->size;
+      if (!err) err = upload_queries(&sh, f->steps, devs[i], ctx);
+      g->dq[i] = sh.dev;
+    }
+    if (err) {
+      group_free_queries(q);
+      return err;
+    }
+  }
+  if (r) {
+    group_free_results(r);
+    if (r->d_results) {
+      (void) hipFree(r->d_results);
+      r->d_results = nullptr;
+    }
+    GroupSlices* g = group_slices(r->num, devs, n);
+    if (!g) return KFMI_E_ALLOCATING_RESULTS;
+    r->grp = g;
+    for (int i = 0; i < n && !err; ++i) {
+      DevCtx* ctx = nullptr;
+      err = ctx_for(devs[i], &ctx);
+      if (!err && hipMalloc((void**) &g->d_res[i], 8ull * (g->num[i] ? g->num[i] : 1)) != hipSuccess) {
+        g->d_res[i] = nullptr;
+        err = KFMI_E_DEVICE_ALLOC;
+      }
+      if (!err && (hipMemsetAsync(g->d_res[i], 0, 8ull * g->num[i], ctx->st) != hipSuccess ||
+                   hipStreamSynchronize(ctx->st) != hipSuccess))
+        err = KFMI_E_KERNEL;
+    }
+    if (err) {
+      group_free_results(r);
+      return err;
+    }
+  }
+  return KFMI_SUCCESS;
+}
+
+static int32_t search_enqueue(kfmi_dev_index* di, kfmi_dev_queries* dq, uint32_t* d_res, hipStream_t st,
+                              hipEvent_t* ev, uint32_t ftab);
+static int32_t search_finish(hipStream_t st, hipEvent_t* ev, double* ms);
+
+/* Every member queues its slice, then all are waited for; the timings are the
+ * slowest member's. */
+static int32_t group_search(kfmi_fmi_t* f, kfmi_qrys_t* q, kfmi_res_t* r)
+{
+  GroupIndex* gi = (GroupIndex*) f->grp;
+  GroupSlices* gq = (GroupSlices*) q->grp;
+  GroupSlices* gr = (GroupSlices*) r->grp;
+  if (!gi || !gq || !gr) return KFMI_E_NOT_ON_DEVICE;   /* handles moved to different modes */
+  if (gq->n != gi->n || gr->n != gi->n) return KFMI_E_BAD_ARGUMENT;
+  for (int i = 0; i < gi->n; ++i)
+    if (gq->dev[i] != gi->dev[i] || gr->dev[i] != gi->dev[i] || gq->num[i] != gr->num[i]) return KFMI_E_BAD_ARGUMENT;
+  const uint32_t ftab = ftab_bases();
+  int32_t err = KFMI_SUCCESS;
+  int queued = 0;
+  for (int i = 0; i < gi->n && !err; ++i) {
+    if (hipSetDevice(gi->dev[i]) != hipSuccess) {
+      err = KFMI_E_NO_DEVICE;
+      break;
+    }
+    err = search_enqueue(gi->di[i], gq->dq[i], gr->d_res[i], gi->st[i], gi->ev[i], ftab);
+    if (!err) ++queued;
+  }
+  double worst[3] = {0, 0, 0};
+  for (int i = 0; i < queued; ++i) {
+    (void) hipSetDevice(gi->dev[i]);
+    double ms[3] = {0, 0, 0};
+    const int32_t e = search_finish(gi->st[i], gi->ev[i], ms);
+    if (e && !err) err = e;
+    for (int k = 0; k < 3; ++k) worst[k] = ms[k] > worst[k] ? ms[k] : worst[k];
+  }
+  for (int k = 0; k < 3; ++k) t_ms[k] = worst[k];
+  return err;
+}
+
+static int32_t group_to_host(kfmi_res_t* r)
+{
+  GroupSlices* g = (GroupSlices*) r->grp;
+  for (int i = 0; i < g->n; ++i) {
+    DevCtx* ctx = nullptr;
+    int32_t err = ctx_for(g->dev[i], &ctx);
+    if (err) return err;
+    if (g->num[i])
+      HIP_OK(hipMemcpyAsync(r->h_results + 2 * g->q0[i], g->d_res[i], 8ull * g->num[i], hipMemcpyDeviceToHost,
+                            ctx->st));
+  }
+  for (int i = 0; i < g->n; ++i) {
+    DevCtx* ctx = nullptr;
+    int32_t err = ctx_for(g->dev[i], &ctx);
+    if (err) return err;
+    HIP_OK(hipStreamSynchronize(ctx->st));
+  }
+  return KFMI_SUCCESS;
+}
+
+extern "C" int32_t kfmi_set_devices(const int32_t* devices, int32_t n)
+{
+  if (n < 0 || n > KFMI_MAX_GROUP || (n && !devices)) return KFMI_E_BAD_ARGUMENT;
+  const int avail = kfmi_device_count();
+  for (int i = 0; i < n; ++i)
+    if (devices[i] < 0 || devices[i] >= avail) return KFMI_E_NO_DEVICE;
+  for (int i = 0; i < n; ++i) t_group[i] = devices[i];
+  t_ngroup = n;
+  if (n == 1) t_device = devices[0];
+  return KFMI_SUCCESS;
+}
+
+extern "C" int32_t kfmi_get_devices(int32_t* devices, int32_t cap)
+{
+  int devs[KFMI_MAX_GROUP];
+  const int n = group_devices(devs);
+  for (int i = 0; i < n && i < cap && devices; ++i) devices[i] = devs[i];
+  return n;
+}
+
+/* ------------------------------------------------------------------------ */
 /* C ABI: the reference's GPU plugin entry points                           */
 /* ------------------------------------------------------------------------ */
 
@@ -981,6 +1260,12 @@ extern "C" int32_t transferCPUtoGPU(void* index, void* queries, void* results)
   kfmi_fmi_t* f = (kfmi_fmi_t*) index;
   kfmi_qrys_t* q = (kfmi_qrys_t*) queries;
   kfmi_res_t* r = (kfmi_res_t*) results;
+  int devs[KFMI_MAX_GROUP];
+  const int ng = group_devices(devs);
+  if (ng > 1) return group_transfer(f, q, r, devs, ng);
+  if (f) group_free_index(f);   /* one mode per handle */
+  if (q) group_free_queries(q);
+  if (r) group_free_results(r);
   const int dev = kfmi_current_device();
   DevCtx* ctx = nullptr;
   int32_t err = ctx_for(dev, &ctx);
@@ -1005,25 +1290,16 @@ extern "C" int32_t transferCPUtoGPU(void* index, void* queries, void* results)
   return KFMI_SUCCESS;
 }
 
-extern "C" int32_t kfmi_search(void* index, void* queries, void* results)
+/* Queues pack (if not fused) + LF of one device batch on `st`, bracketed by
+ * ev[0..2]; search_finish waits and reads the timings. */
+static int32_t search_enqueue(kfmi_dev_index* di, kfmi_dev_queries* dq, uint32_t* d_res, hipStream_t st,
+                              hipEvent_t* ev, uint32_t ftab)
 {
-  kfmi_fmi_t* f = (kfmi_fmi_t*) index;
-  kfmi_qrys_t* q = (kfmi_qrys_t*) queries;
-  kfmi_res_t* r = (kfmi_res_t*) results;
-  if (!f || !q || !r) return KFMI_E_BAD_ARGUMENT;
-  if (!f->dev || !q->dev || !r->d_results) return KFMI_E_NOT_ON_DEVICE;
-  if (q->num != r->num) return KFMI_E_BAD_ARGUMENT;
-  kfmi_dev_index* di = f->dev;
-  kfmi_dev_queries* dq = q->dev;
   if (dq->device != di->device || dq->K != di->K) return KFMI_E_BAD_ARGUMENT;
-  DevCtx* ctx = nullptr;
-  int32_t err = ctx_for(di->device, &ctx);
-  if (err) return err;
-
   SearchLaunch a{};
-  a.st = ctx->st;
+  a.st = st;
   a.ix = idx_args(di);
-  err = use_ftab(di, ctx, a.ix);
+  int32_t err = use_ftab(di, st, a.ix, ftab);
   if (err) return err;
   a.qp = dq->packed;
   a.ascii = dq->ascii;
@@ -1032,24 +1308,47 @@ extern "C" int32_t kfmi_search(void* index, void* queries, void* results)
   a.num = dq->num;
   a.steps = dq->steps;
   a.nwords = dq->nwords;
-  a.res = r->d_results;
-
-  HIP_OK(hipEventRecord(ctx->ev[0], ctx->st));
-  if (!a.maxw) HIP_OK(launch_pack(dq, ctx->st));
-  HIP_OK(hipEventRecord(ctx->ev[1], ctx->st));
+  a.res = d_res;
+  HIP_OK(hipEventRecord(ev[0], st));
+  if (!a.maxw) HIP_OK(launch_pack(dq, st));
+  HIP_OK(hipEventRecord(ev[1], st));
   if (dq->num) {
     const Op op = is_coop(di->backend) ? Op::Coop : Op::Task;
     HIP_OK(dispatch(op, di->K, di->nb, di->layout, a));
   }
-  HIP_OK(hipEventRecord(ctx->ev[2], ctx->st));
-  HIP_OK(hipStreamSynchronize(ctx->st));
-  float ms01 = 0, ms12 = 0;
-  HIP_OK(hipEventElapsedTime(&ms01, ctx->ev[0], ctx->ev[1]));
-  HIP_OK(hipEventElapsedTime(&ms12, ctx->ev[1], ctx->ev[2]));
-  t_ms[0] = ms01 + ms12;
-  t_ms[1] = ms01;
-  t_ms[2] = ms12;
+  HIP_OK(hipEventRecord(ev[2], st));
   return KFMI_SUCCESS;
+}
+
+static int32_t search_finish(hipStream_t st, hipEvent_t* ev, double* ms)
+{
+  HIP_OK(hipStreamSynchronize(st));
+  float ms01 = 0, ms12 = 0;
+  HIP_OK(hipEventElapsedTime(&ms01, ev[0], ev[1]));
+  HIP_OK(hipEventElapsedTime(&ms12, ev[1], ev[2]));
+  ms[0] = ms01 + ms12;
+  ms[1] = ms01;
+  ms[2] = ms12;
+  return KFMI_SUCCESS;
+}
+
+static int32_t group_search(kfmi_fmi_t* f, kfmi_qrys_t* q, kfmi_res_t* r);
+
+extern "C" int32_t kfmi_search(void* index, void* queries, void* results)
+{
+  kfmi_fmi_t* f = (kfmi_fmi_t*) index;
+  kfmi_qrys_t* q = (kfmi_qrys_t*) queries;
+  kfmi_res_t* r = (kfmi_res_t*) results;
+  if (!f || !q || !r) return KFMI_E_BAD_ARGUMENT;
+  if (q->num != r->num) return KFMI_E_BAD_ARGUMENT;
+  if (f->grp || q->grp || r->grp) return group_search(f, q, r);
+  if (!f->dev || !q->dev || !r->d_results) return KFMI_E_NOT_ON_DEVICE;
+  kfmi_dev_index* di = f->dev;
+  DevCtx* ctx = nullptr;
+  int32_t err = ctx_for(di->device, &ctx);
+  if (!err) err = search_enqueue(di, q->dev, r->d_results, ctx->st, ctx->ev, ftab_bases());
+  if (!err) err = search_finish(ctx->st, ctx->ev, t_ms);
+  return err;
 }
 
 /* interface.h:31: synchronous like the reference (cudaThreadSynchronize,
@@ -1067,6 +1366,7 @@ extern "C" int32_t kfmi_count_blocks(void* index, void* queries, uint64_t* block
   kfmi_fmi_t* f = (kfmi_fmi_t*) index;
   kfmi_qrys_t* q = (kfmi_qrys_t*) queries;
   if (!f || !q || !blocks) return KFMI_E_BAD_ARGUMENT;
+  if (f->grp || q->grp) return KFMI_E_NOT_IMPLEMENTED;   /* single-device API */
   if (!f->dev || !q->dev) return KFMI_E_NOT_ON_DEVICE;
   kfmi_dev_index* di = f->dev;
   kfmi_dev_queries* dq = q->dev;
@@ -1102,6 +1402,7 @@ extern "C" int32_t kfmi_count_blocks(void* index, void* queries, uint64_t* block
 extern "C" int32_t transferGPUtoCPU(void* results)
 {
   kfmi_res_t* r = (kfmi_res_t*) results;
+  if (r && r->grp) return group_to_host(r);
   if (!r || !r->d_results) return KFMI_E_NOT_ON_DEVICE;
   DevCtx* ctx = nullptr;
   int32_t err = ctx_for(kfmi_current_device(), &ctx);
@@ -1115,6 +1416,7 @@ extern "C" int32_t transferGPUtoCPU(void* results)
 extern "C" int32_t freeIndexGPU(void** index)
 {
   kfmi_fmi_t* f = index ? (kfmi_fmi_t*) *index : nullptr;
+  if (f) group_free_index(f);
   if (f && f->dev) {
     free_dev_index(f->dev);
     f->dev = nullptr;
@@ -1125,6 +1427,7 @@ extern "C" int32_t freeIndexGPU(void** index)
 extern "C" int32_t freeQueriesGPU(void** queries)
 {
   kfmi_qrys_t* q = queries ? (kfmi_qrys_t*) *queries : nullptr;
+  if (q) group_free_queries(q);
   if (q && q->dev) {
     free_dev_queries(q->dev);
     q->dev = nullptr;
@@ -1135,6 +1438,7 @@ extern "C" int32_t freeQueriesGPU(void** queries)
 extern "C" int32_t freeResultsGPU(void** results)
 {
   kfmi_res_t* r = results ? (kfmi_res_t*) *results : nullptr;
+  if (r) group_free_results(r);
   if (r && r->d_results) {
     (void) hipFree(r->d_results);
     r->d_results = nullptr;
@@ -1145,6 +1449,12 @@ extern "C" int32_t freeResultsGPU(void** results)
 extern "C" uint64_t kfmi_device_index_bytes(void* index)
 {
   kfmi_fmi_t* f = (kfmi_fmi_t*) index;
+  if (f && f->grp) {   /* all replicas of a device group */
+    const GroupIndex* g = (const GroupIndex*) f->grp;
+    uint64_t b = 0;
+    for (int i = 0; i < g->n; ++i) b += g->di[i]->ent_bytes + g->di[i]->sb_bytes + g->di[i]->sa_bytes;
+    return b;
+  }
   if (!f || !f->dev) return 0;
   return f->dev->ent_bytes + f->dev->sb_bytes + f->dev->sa_bytes;
 }
@@ -1186,16 +1496,10 @@ extern "C" const uint32_t* kfmi_locations_positions(void* locations)
   return locations ? ((kfmi_locations*) locations)->h_pos : nullptr;
 }
 
-extern "C" int32_t kfmi_locate(void* index, void* results, uint32_t max_occ, void** locations)
+/* Locate of the `num` results at d_res (device of di) into *locations. */
+static int32_t locate_on(kfmi_fmi_t* f, kfmi_dev_index* di, uint32_t* d_res, uint64_t num, uint32_t max_occ,
+                         kfmi_locations** locations)
 {
-  kfmi_fmi_t* f = (kfmi_fmi_t*) index;
-  kfmi_res_t* r = (kfmi_res_t*) results;
-  if (!locations) return KFMI_E_BAD_ARGUMENT;
-  *locations = nullptr;
-  if (!f || !r) return KFMI_E_BAD_ARGUMENT;
-  if (!f->dev || !r->d_results) return KFMI_E_NOT_ON_DEVICE;
-  if (!f->h_sa || !f->sa_rate) return KFMI_E_BAD_ARGUMENT;   /* index built without SA samples */
-  kfmi_dev_index* di = f->dev;
   DevCtx* ctx = nullptr;
   int32_t err = ctx_for(di->device, &ctx);
   if (err) return err;
@@ -1203,7 +1507,6 @@ extern "C" int32_t kfmi_locate(void* index, void* results, uint32_t max_occ, voi
     err = upload_sa(f, di, ctx);
     if (err) return err;
   }
-  const uint64_t num = r->num;
   kfmi_locations* L = new (std::nothrow) kfmi_locations();
   if (!L) return KFMI_E_ALLOCATING_RESULTS;
   L->num = num;
@@ -1236,7 +1539,7 @@ extern "C" int32_t kfmi_locate(void* index, void* results, uint32_t max_occ, voi
             hipMalloc(&tmp, tb ? tb : 1) == hipSuccess;
   if (!ok) return done(KFMI_E_DEVICE_ALLOC);
   if (hipEventRecord(ctx->ev[0], st) != hipSuccess) return done(KFMI_E_KERNEL);
-  hipLaunchKernelGGL(loc_count_kernel, dim3((uint32_t) ((num + 1 + 255) / 256)), dim3(256), 0, st, r->d_results, num,
+  hipLaunchKernelGGL(loc_count_kernel, dim3((uint32_t) ((num + 1 + 255) / 256)), dim3(256), 0, st, d_res, num,
                      max_occ, d_cnt);
   ok = hipGetLastError() == hipSuccess &&
        rocprim::exclusive_scan(tmp, tb, d_cnt, d_off, (uint64_t) 0, (size_t) (num + 1), rocprim::plus<uint64_t>(),
@@ -1263,13 +1566,13 @@ extern "C" int32_t kfmi_locate(void* index, void* results, uint32_t max_occ, voi
       return done(KFMI_E_KERNEL);
     const uint64_t rb = (total + 255) / 256;
     hipLaunchKernelGGL(loc_rows_kernel, dim3((uint32_t) (rb < (1u << 20) ? rb : (1u << 20))), dim3(256), 0, st,
-                       r->d_results, d_off, total, d_own);   /* owner -> first row of each slot, in place */
+                       d_res, d_off, total, d_own);   /* owner -> first row of each slot, in place */
     if (hipGetLastError() != hipSuccess) return done(KFMI_E_KERNEL);
   }
   SearchLaunch a{};
   a.st = st;
   a.ix = idx_args(di);
-  a.res = r->d_results;
+  a.res = d_res;
   a.num = num;
   a.sa = di->sa;
   a.sa_log2 = di->sa_log2;
@@ -1291,6 +1594,62 @@ extern "C" int32_t kfmi_locate(void* index, void* results, uint32_t max_occ, voi
   t_ms[1] = ms01;
   t_ms[2] = ms12;          /* the locate kernel alone */
   return done(KFMI_SUCCESS);
+}
+
+extern "C" int32_t kfmi_locate(void* index, void* results, uint32_t max_occ, void** locations)
+{
+  kfmi_fmi_t* f = (kfmi_fmi_t*) index;
+  kfmi_res_t* r = (kfmi_res_t*) results;
+  if (!locations) return KFMI_E_BAD_ARGUMENT;
+  *locations = nullptr;
+  if (!f || !r) return KFMI_E_BAD_ARGUMENT;
+  if (!f->h_sa || !f->sa_rate) return KFMI_E_BAD_ARGUMENT;   /* index built without SA samples */
+  if (!f->grp && !r->grp) {
+    if (!f->dev || !r->d_results) return KFMI_E_NOT_ON_DEVICE;
+    return locate_on(f, f->dev, r->d_results, r->num, max_occ, (kfmi_locations**) locations);
+  }
+  /* device group: every member locates its slice, the lists are concatenated */
+  GroupIndex* gi = (GroupIndex*) f->grp;
+  GroupSlices* gr = (GroupSlices*) r->grp;
+  if (!gi || !gr) return KFMI_E_NOT_ON_DEVICE;
+  if (gr->n != gi->n) return KFMI_E_BAD_ARGUMENT;
+  kfmi_locations* part[KFMI_MAX_GROUP] = {};
+  int32_t err = KFMI_SUCCESS;
+  double ms[3] = {0, 0, 0};
+  uint64_t total = 0;
+  for (int i = 0; i < gi->n && !err; ++i) {
+    if (gr->dev[i] != gi->dev[i]) err = KFMI_E_BAD_ARGUMENT;
+    if (!err) err = locate_on(f, gi->di[i], gr->d_res[i], gr->num[i], max_occ, &part[i]);
+    if (!err) {
+      total += part[i]->total;
+      for (int k = 0; k < 3; ++k) ms[k] += t_ms[k];
+    }
+  }
+  kfmi_locations* L = err ? nullptr : new (std::nothrow) kfmi_locations();
+  if (!err && !L) err = KFMI_E_ALLOCATING_RESULTS;
+  if (!err) {
+    L->num = r->num;
+    L->total = total;
+    L->h_off = (uint64_t*) malloc(8 * (r->num + 1));
+    L->h_pos = (uint32_t*) malloc(4 * total + 4);
+    if (!L->h_off || !L->h_pos) err = KFMI_E_ALLOCATING_RESULTS;
+  }
+  if (!err) {
+    uint64_t base = 0;
+    for (int i = 0; i < gi->n; ++i) {
+      for (uint64_t j = 0; j < gr->num[i]; ++j) L->h_off[gr->q0[i] + j] = base + part[i]->h_off[j];
+      if (part[i]->total) memcpy(L->h_pos + base, part[i]->h_pos, 4 * part[i]->total);
+      base += part[i]->total;
+    }
+    L->h_off[r->num] = total;
+    *locations = L;
+    for (int k = 0; k < 3; ++k) t_ms[k] = ms[k];
+  } else if (L) {
+    kfmi_locations_free((void**) &L);
+  }
+  for (int i = 0; i < gi->n; ++i)
+    if (part[i]) kfmi_locations_free((void**) &part[i]);
+  return err;
 }
 
 /* ------------------------------------------------------------------------ */
@@ -1578,7 +1937,7 @@ extern "C" int32_t kfmi_search_stream(void* index, const char* ascii, uint64_t n
   const auto t0 = std::chrono::steady_clock::now();
   const Op op = is_coop(di->backend) ? Op::Coop : Op::Task;
   IdxArgs ix = idx_args(di);
-  err = use_ftab(di, ctx, ix);
+  err = use_ftab(di, ctx->st, ix, ftab_bases());
   if (err) return err;
   int32_t status = KFMI_SUCCESS;
   using clk = std::chrono::steady_clock;

@@ -171,7 +171,7 @@ int32_t freeQueries(void **queries)
 {
   kfmi_qrys_t *q = queries ? (kfmi_qrys_t *) *queries : NULL;
   if (!q) return KFMI_SUCCESS;
-  if (q->dev) freeQueriesGPU(queries);
+  if (q->dev || q->grp) freeQueriesGPU(queries);
   free(q->h_queries);
   free(q);
   *queries = NULL;
@@ -205,7 +205,7 @@ int32_t freeResults(void **results)
 {
   kfmi_res_t *r = results ? (kfmi_res_t *) *results : NULL;
   if (!r) return KFMI_SUCCESS;
-  if (r->d_results) freeResultsGPU(results);
+  if (r->d_results || r->grp) freeResultsGPU(results);
   free(r->h_results);
   free(r);
   *results = NULL;

@@ -205,7 +205,7 @@ int32_t freeIndex(void **index)
 {
   kfmi_fmi_t *f = index ? (kfmi_fmi_t *) *index : NULL;
   if (!f) return KFMI_SUCCESS;
-  if (f->dev) freeIndexGPU(index);
+  if (f->dev || f->grp) freeIndexGPU(index);
   free(f->h_sa);
   free(f->image);
   free(f);

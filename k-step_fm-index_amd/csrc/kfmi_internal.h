@@ -45,6 +45,7 @@ typedef struct {
   uint32_t  sa_gen;
   uint64_t  sa_count;
   uint32_t *h_sa;
+  void     *grp;           /* replicas on a device group (KFMI_DEVICES, kfmi_set_devices) */
 } kfmi_fmi_t;
 
 typedef struct {
@@ -52,12 +53,14 @@ typedef struct {
   uint32_t size;
   char    *h_queries;      /* num*size ASCII, query q at q*size (plain layout) */
   struct kfmi_dev_queries *dev;
+  void    *grp;            /* per-device slices on a device group */
 } kfmi_qrys_t;
 
 typedef struct {
   uint64_t  num;
   uint32_t *h_results;     /* 2*num: [L0,R0,L1,R1,...] */
   uint32_t *d_results;     /* device copy (hipMalloc), NULL until transfer */
+  void     *grp;           /* per-device slices on a device group */
 } kfmi_res_t;
 
 typedef struct {

@@ -100,6 +100,8 @@ def load() -> ctypes.CDLL:
         "kfmi_host_free": (i32, [vp]),
         "kfmi_stream_release": (i32, []),
         "kfmi_pack_queries": (i32, [vp, u64, u32, vp]),
+        "kfmi_set_devices": (i32, [ctypes.POINTER(ctypes.c_int32), i32]),
+        "kfmi_get_devices": (i32, [ctypes.POINTER(ctypes.c_int32), i32]),
         "kfmi_build_index_ex": (i32, [vp, u64, u32, u32, u32, i32, pvp]),
         "kfmi_set_ftab": (i32, [u32]),
         "kfmi_index_sa": (i32, [vp, pvp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32)]),
@@ -145,6 +147,20 @@ def set_ftab(bases: int) -> None:
 
 def set_device(dev: int) -> None:
     _check(load().kfmi_set_device(int(dev)), f"set_device({dev})")
+
+
+def set_devices(devs) -> None:
+    """Device group for the transfer/search/transfer trio (kfmi_set_devices):
+    index replicated, queries sliced; [] returns to single-device mode."""
+    devs = [int(d) for d in devs]
+    arr = (ctypes.c_int32 * max(len(devs), 1))(*devs)
+    _check(load().kfmi_set_devices(arr, len(devs)), f"set_devices({devs})")
+
+
+def get_devices() -> list:
+    arr = (ctypes.c_int32 * 16)()
+    n = load().kfmi_get_devices(arr, 16)
+    return [arr[i] for i in range(n)]
 
 
 def device_count() -> int:

@@ -1,0 +1,123 @@
+"""Device groups (kfmi_set_devices / KFMI_DEVICES): runtime multi-GPU behind
+the reference's handles (SURVEY 8(b) device selection, 8(e) query slicing).
+The index is replicated per member, queries and results are cut into
+contiguous 64-read slices; results and locate output must equal the
+single-device ones bit for bit.  On a one-GPU box the group lists device 0
+several times (independent replicas and streams on one card), which runs
+every line of the group path."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import util
+
+
+def test_device_list_from_env_and_validation(kfmi_mod):
+    code = ("import sys; sys.path[:0] = {paths!r}; import kstep_fmi as K; "
+            "print(K.get_devices())").format(paths=[str(util.REPO), str(util.PKG)])
+    env = dict(os.environ, KFMI_DEVICES="0, 1,2")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert out.stdout.strip() == "[0, 1, 2]", out.stderr
+    K = kfmi_mod
+    K.set_devices([])
+    assert K.get_devices() == []
+    with pytest.raises(K.KfmiError):
+        K.set_devices([K.device_count() + 3])
+    with pytest.raises(K.KfmiError):
+        K.set_devices(list(range(17)))
+
+
+@pytest.fixture(scope="module")
+def setup(kfmi_mod):
+    K = kfmi_mod
+    if K.device_count() < 1:
+        pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
+    K.set_devices([])
+    K.set_device(0)
+    rng = np.random.default_rng(41)
+    text = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=200_001).tobytes()
+    idx = K.Index.build(text, k=2, d=64, gpu=True, sa_rate=4)
+    t = np.frombuffer(text, np.uint8)
+    reads = np.concatenate([t[rng.integers(0, len(text) - 100, size=3_000)[:, None] + np.arange(100)],
+                            rng.choice(np.frombuffer(b"ACGTN", np.uint8), size=(333, 100))])
+    return K, idx, reads
+
+
+def run_trio(K, idx, reads):
+    q = K.Queries.from_array(reads)
+    r = K.Results.alloc(reads.shape[0])
+    K.transfer_to_gpu(idx, q, r)
+    K.search(idx, q, r)
+    K.transfer_to_cpu(r)
+    return q, r, r.array().copy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("backend", ["task-mid", "coop-mid", "task", "coop-ac", "task-ac128"])
+@pytest.mark.parametrize("group", [[0, 0], [0, 0, 0]])
+@pytest.mark.parametrize("num", [3_333, 130, 64, 1, 0])
+def test_group_equals_single_device(setup, backend, group, num):
+    K, idx, reads = setup
+    sub = np.ascontiguousarray(reads[:num])
+    K.set_backend(backend)
+    K.set_devices([])
+    q, r, want = run_trio(K, idx, sub)
+    q.close(); r.close()
+    try:
+        K.set_devices(group)
+        q, r, got = run_trio(K, idx, sub)
+        assert np.array_equal(got, want)
+        assert K.last_timing()["total_ms"] >= 0
+        q.close(); r.close()
+    finally:
+        K.set_devices([])
+        idx.free_gpu()
+
+
+@pytest.mark.gpu
+def test_group_locate_and_mode_switch(setup):
+    K, idx, reads = setup
+    K.set_backend("task-mid")
+    K.set_devices([])
+    q, r, want = run_trio(K, idx, reads)
+    loc1 = K.locate(idx, r)
+    single_bytes = idx.device_bytes()
+    q.close(); r.close()
+    try:
+        K.set_devices([0, 0, 0])
+        q, r, got = run_trio(K, idx, reads)
+        assert np.array_equal(got, want)
+        loc3 = K.locate(idx, r)
+        assert np.array_equal(loc3.offsets(), loc1.offsets())
+        assert np.array_equal(loc3.positions(), loc1.positions())
+        assert idx.device_bytes() == 3 * single_bytes > 0   # three replicas
+        # the same handles back in single-device mode
+        K.set_devices([])
+        K.transfer_to_gpu(idx, q, r)
+        K.search(idx, q, r)
+        K.transfer_to_cpu(r)
+        assert np.array_equal(r.array(), want)
+        q.close(); r.close()
+    finally:
+        K.set_devices([])
+        idx.free_gpu()
+
+
+@pytest.mark.gpu
+def test_group_search_driver(tmp_path):
+    """The reference's searchQueries flow, unmodified, over a group of three."""
+    import shutil
+    c = util.manifest()["textA"]
+    ent = c["indexes"]["k2_d64"]
+    shutil.copy(util.GOLDEN / "textA" / ent["files"]["101"]["file"], tmp_path / "idx.fmi")
+    qd = c["queries"]["100"]
+    shutil.copy(util.GOLDEN / "textA" / qd["file"], tmp_path / "q.qry")
+    env = dict(os.environ, KFMI_BACKEND="task-mid", KFMI_DEVICES="0,0,0", KFMI_ITERS="2")
+    p = subprocess.run([str(util.PKG / "bin" / "searchQueries"), "idx.fmi", "q.qry", "100", str(qd["num"])],
+                       cwd=tmp_path, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout + p.stderr
+    want = (util.GOLDEN / "textA" / ent["results"]["100.100"]["file"]).read_bytes()
+    assert (tmp_path / "idx.fmi.res.gpu").read_bytes() == want
