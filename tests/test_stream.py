@@ -91,3 +91,23 @@ def test_stream_errors(setup):
         K.search_stream(fresh, reads[:10])
     assert e.value.code == 34
     K.load().kfmi_stream_release()
+
+
+@pytest.mark.parametrize("hostpack", ["1", "0"])
+@pytest.mark.parametrize("m", [2, 4, 16, 32, 34, 254, 256, 300, 1000])
+def test_stream_read_lengths(kfmi_mod, hostpack, m, monkeypatch):
+    """Every word-count class of the host packer (ceil(m/16) words, partial
+    last word) and of the fused/unfused device paths."""
+    K = kfmi_mod
+    monkeypatch.setenv("KFMI_STREAM_HOSTPACK", hostpack)
+    K.set_device(0)
+    rng = np.random.default_rng(m)
+    text = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=20_000).tobytes()
+    idx = K.Index.build(text, k=2, d=64, gpu=True)
+    t = np.frombuffer(text, np.uint8)
+    reads = np.concatenate([t[rng.integers(0, len(text) - m, size=700)[:, None] + np.arange(m)],
+                            rng.choice(np.frombuffer(b"ACGTNacgt", np.uint8), size=(77, m))])
+    want = K.search_array(idx, reads, "task-mid")
+    got = K.search_stream(idx, reads, chunk=256)
+    assert np.array_equal(got, want)
+    K.load().kfmi_stream_release()
