@@ -1,0 +1,128 @@
+/*
+ * kfmi_runtime.h -- host-side runtime shared by the library's translation
+ * units: kfmi_search.hip (backends, devices, uploads, the reference's entry
+ * points), kfmi_group.hip (device groups), kfmi_locate.hip (locate) and
+ * kfmi_stream.hip (streamed search, host worker pool).
+ */
+#ifndef KFMI_RUNTIME_H_
+#define KFMI_RUNTIME_H_
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <mutex>
+
+#include "../kfmi_internal.h"
+#include "kfmi_kernels.h"
+
+#define HIP_OK(x)                                                                   \
+  do {                                                                              \
+    hipError_t _e = (x);                                                            \
+    if (_e != hipSuccess) {                                                         \
+      fprintf(stderr, "kstepfmi: %s failed: %s (%s:%d)\n", #x, hipGetErrorString(_e), \
+              __FILE__, __LINE__);                                                  \
+      return KFMI_E_KERNEL;                                                         \
+    }                                                                               \
+  } while (0)
+
+/* ------------------------------------------------------------------------ */
+/* device-side handles                                                      */
+/* ------------------------------------------------------------------------ */
+
+struct kfmi_dev_index {
+  int device = -1;
+  int backend = -1;
+  int layout = -1;
+  uint32_t K = 0, d = 0, nb = 0, bwtsize = 0, nentries = 0;
+  kfmi::DollarArgs dl{};
+  uint32_t* ent = nullptr;     /* device entries */
+  uint64_t ent_bytes = 0;
+  uint32_t* sb = nullptr;      /* packed: superblock counters */
+  uint64_t sb_bytes = 0;
+  uint32_t* sa = nullptr;      /* locate: row-sampled suffix array */
+  uint64_t sa_bytes = 0;
+  uint32_t sa_log2 = 0, sa_gen = 0;
+  uint2* ftab = nullptr;       /* jump-start table of ftab_chars bases (0 = none) */
+  uint32_t ftab_chars = 0;
+};
+
+struct kfmi_dev_queries {
+  int device = -1;
+  uint8_t* ascii = nullptr;    /* num*size bytes, plain layout */
+  uint32_t* packed = nullptr;  /* nwords x num u32 codes */
+  uint64_t num = 0;
+  uint32_t size = 0, K = 0, steps = 0, nwords = 0;
+};
+
+namespace kfmi {
+
+/* One non-blocking stream and a set of timing events per device. */
+struct DevCtx {
+  bool init = false;
+  hipStream_t st = nullptr;
+  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+};
+extern std::mutex g_ctx_mu;   /* guards g_ctx; also one streamed search per device at a time */
+int32_t ctx_for(int dev, DevCtx** out);   /* selects `dev`, creates its stream and events once */
+
+/* per calling thread (kfmi_search.hip) */
+extern thread_local int t_device;
+extern thread_local int32_t t_last_error;
+extern thread_local double t_ms[3];   /* kfmi_last_timing: total, pack, lf (ms) */
+uint32_t ftab_bases(void);
+
+/* backends and kernel dispatch (kfmi_search.hip) */
+bool is_coop(int backend);
+int fused_maxw(int backend, uint32_t nwords);
+hipError_t dispatch(Op op, uint32_t K, uint32_t nb, int lay, const SearchLaunch& a,
+                    unsigned long long* d_total = nullptr);
+IdxArgs idx_args(const kfmi_dev_index* di);
+int32_t use_ftab(kfmi_dev_index* di, hipStream_t st, IdxArgs& ix, uint32_t bases);
+hipError_t launch_pack(const kfmi_dev_queries* dq, hipStream_t st);
+
+/* uploads (kfmi_search.hip) */
+int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx, kfmi_dev_index** out = nullptr);
+int32_t upload_sa(const kfmi_fmi_t* f, kfmi_dev_index* di, DevCtx* ctx);
+int32_t upload_queries(kfmi_qrys_t* q, uint32_t K, int dev, DevCtx* ctx);
+void free_dev_index(kfmi_dev_index* di);
+void free_dev_queries(kfmi_dev_queries* dq);
+hipError_t h2d(void* dst, const void* src, uint64_t bytes, hipStream_t st);
+
+/* one device batch: queue pack + LF bracketed by ev[0..2], then wait (kfmi_search.hip) */
+int32_t search_enqueue(kfmi_dev_index* di, kfmi_dev_queries* dq, uint32_t* d_res, hipStream_t st, hipEvent_t* ev,
+                       uint32_t ftab);
+int32_t search_finish(hipStream_t st, hipEvent_t* ev, double* ms);
+
+/* host memory helpers (kfmi_stream.hip) */
+bool host_pinned(const void* p);
+void par_copy(void* dst, const void* src, uint64_t bytes);
+
+/* device groups (kfmi_group.hip) */
+constexpr int KFMI_MAX_GROUP = 16;
+struct GroupIndex {
+  int n = 0, backend = -1;
+  int dev[KFMI_MAX_GROUP] = {};
+  kfmi_dev_index* di[KFMI_MAX_GROUP] = {};
+  hipStream_t st[KFMI_MAX_GROUP] = {};
+  hipEvent_t ev[KFMI_MAX_GROUP][3] = {};
+};
+
+/* queries or results of a group: one contiguous slice per member */
+struct GroupSlices {
+  int n = 0;
+  int dev[KFMI_MAX_GROUP] = {};
+  uint64_t q0[KFMI_MAX_GROUP] = {}, num[KFMI_MAX_GROUP] = {};
+  kfmi_dev_queries* dq[KFMI_MAX_GROUP] = {};
+  uint32_t* d_res[KFMI_MAX_GROUP] = {};
+};
+int group_devices(int* devs);   /* the KFMI_DEVICES / kfmi_set_devices list */
+int32_t group_transfer(kfmi_fmi_t* f, kfmi_qrys_t* q, kfmi_res_t* r, const int* devs, int n);
+int32_t group_search(kfmi_fmi_t* f, kfmi_qrys_t* q, kfmi_res_t* r);
+int32_t group_to_host(kfmi_res_t* r);
+void group_free_index(kfmi_fmi_t* f);
+void group_free_queries(kfmi_qrys_t* q);
+void group_free_results(kfmi_res_t* r);
+
+}  // namespace kfmi
+
+#endif  // KFMI_RUNTIME_H_

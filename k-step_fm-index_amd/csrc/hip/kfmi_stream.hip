@@ -1,0 +1,371 @@
+/*
+ * kfmi_stream.hip -- streamed search from host memory and
+ * the host worker pool shared with the staged uploads.
+ */
+#include <stdlib.h>
+#include <string.h>
+#include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "kfmi_runtime.h"
+
+namespace kfmi {
+
+/* ------------------------------------------------------------------------ */
+/* streamed search from host memory: query H2D, packing, LF  */
+/* and result D2H of successive chunks overlap on NSLOT HIP streams.  By    */
+/* default the host packs each chunk to 2-bit code words (qpack.c) while    */
+/* the GPU works on the previous ones, so PCIe carries 4 bytes per 16 bases */
+/* (KFMI_STREAM_HOSTPACK=0: ASCII H2D and packing on the device).  Pinned   */
+/* ASCII is DMA'd directly; pageable goes through pinned staging.           */
+/* ------------------------------------------------------------------------ */
+
+constexpr int NSLOT = 3;
+
+struct StreamSlot {
+  hipStream_t st = nullptr;
+  hipEvent_t done = nullptr;
+  kfmi_dev_queries dq;         /* device ascii + packed of one chunk */
+  uint32_t* d_res = nullptr;
+  uint8_t* h_in = nullptr;     /* pinned staging */
+  uint32_t* h_out = nullptr;
+  uint32_t* h_pk = nullptr;    /* pinned host-packed code words */
+  uint64_t cap_q = 0, cap_in = 0, cap_words = 0;
+  uint64_t q0 = 0, n = 0;
+  bool busy = false;
+};
+
+struct StreamPool {
+  bool init = false;
+  StreamSlot slot[NSLOT];
+};
+static StreamPool g_pool[64];
+
+static void pool_free(int dev)
+{
+  StreamPool& p = g_pool[dev];
+  if (!p.init) return;
+  (void) hipSetDevice(dev);
+  for (StreamSlot& s : p.slot) {
+    if (s.st) (void) hipStreamSynchronize(s.st);
+    if (s.dq.ascii) (void) hipFree(s.dq.ascii);
+    if (s.dq.packed) (void) hipFree(s.dq.packed);
+    if (s.d_res) (void) hipFree(s.d_res);
+    if (s.h_in) (void) hipHostFree(s.h_in);
+    if (s.h_out) (void) hipHostFree(s.h_out);
+    if (s.h_pk) (void) hipHostFree(s.h_pk);
+    if (s.done) (void) hipEventDestroy(s.done);
+    if (s.st) (void) hipStreamDestroy(s.st);
+    s = StreamSlot();
+  }
+  p.init = false;
+}
+
+/* Grows slot buffers to hold `cq` queries of `size` bytes packed in `words` words. */
+static int32_t slot_reserve(StreamSlot& s, uint64_t cq, uint32_t size, uint32_t words, bool stage_in, bool stage_out,
+                     bool host_pack)
+{
+  if (!s.st) {
+    if (hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess)
+      return KFMI_E_NO_DEVICE;
+  }
+  const uint64_t in = cq * size + 16;
+  if (in > s.cap_in) {
+    if (s.dq.ascii) (void) hipFree(s.dq.ascii);
+    if (s.h_in) { (void) hipHostFree(s.h_in); s.h_in = nullptr; }
+    s.dq.ascii = nullptr;
+    s.cap_in = 0;
+    if (hipMalloc((void**) &s.dq.ascii, in) != hipSuccess) return KFMI_E_DEVICE_ALLOC;
+    s.cap_in = in;
+  }
+  if (stage_in && !s.h_in && hipHostMalloc((void**) &s.h_in, s.cap_in, hipHostMallocDefault) != hipSuccess)
+    return KFMI_E_ALLOCATING_MFASTA;
+  if (cq > s.cap_q || (uint64_t) words * cq > s.cap_words) {
+    if (s.dq.packed) (void) hipFree(s.dq.packed);
+    if (s.d_res) (void) hipFree(s.d_res);
+    if (s.h_out) { (void) hipHostFree(s.h_out); s.h_out = nullptr; }
+    if (s.h_pk) { (void) hipHostFree(s.h_pk); s.h_pk = nullptr; }
+    s.dq.packed = nullptr;
+    s.d_res = nullptr;
+    s.cap_q = s.cap_words = 0;
+    if (hipMalloc((void**) &s.dq.packed, 4ull * words * cq) != hipSuccess ||
+        hipMalloc((void**) &s.d_res, 8ull * cq) != hipSuccess)
+      return KFMI_E_DEVICE_ALLOC;
+    s.cap_q = cq;
+    s.cap_words = (uint64_t) words * cq;
+  }
+  if (stage_out && !s.h_out && hipHostMalloc((void**) &s.h_out, 8ull * s.cap_q, hipHostMallocDefault) != hipSuccess)
+    return KFMI_E_ALLOCATING_RESULTS;
+  if (host_pack && !s.h_pk && hipHostMalloc((void**) &s.h_pk, 4ull * s.cap_words, hipHostMallocDefault) != hipSuccess)
+    return KFMI_E_ALLOCATING_MFASTA;
+  return KFMI_SUCCESS;
+}
+
+bool host_pinned(const void* p)
+{
+  hipPointerAttribute_t at;
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void) hipGetLastError();
+    return false;
+  }
+  return at.type == hipMemoryTypeHost;
+}
+
+/* Persistent host workers for the streamed search (a chunk every few hundred
+ * microseconds: spawning threads per chunk would cost as much as the work).
+ * KFMI_HOST_THREADS (default min(16, cores)) threads including the caller. */
+class HostPool {
+ public:
+  static HostPool& get()
+  {
+    static HostPool p;
+    return p;
+  }
+  int size() const { return (int) th_.size() + 1; }
+  /* fn(i) for i in [0, n) over the workers and the caller; returns when all are
+   * done.  Calls from several host threads (one per device) take turns. */
+  void run(int n, const std::function<void(int)>& fn)
+  {
+    if (n <= 1 || th_.empty()) {
+      for (int i = 0; i < n; ++i) fn(i);
+      return;
+    }
+    std::lock_guard<std::mutex> turn(run_mu_);
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      fn_ = &fn;
+      n_ = n;
+      next_ = 0;
+      left_ = n;
+      ++gen_;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> lk(mu_);
+    done_.wait(lk, [&] { return left_ == 0; });
+    fn_ = nullptr;
+  }
+
+ private:
+  HostPool()
+  {
+    const char* e = getenv("KFMI_HOST_THREADS");
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    int v = e ? atoi(e) : (int) std::min(16u, hw);
+    v = std::max(1, std::min(v, 64));
+    for (int i = 0; i + 1 < v; ++i) th_.emplace_back([this] { loop(); });
+  }
+  ~HostPool()
+  {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  void loop()
+  {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+      }
+      work();
+    }
+  }
+  void work()
+  {
+    for (;;) {
+      const std::function<void(int)>* f;
+      int i;
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (!fn_ || next_ >= n_) return;
+        i = next_++;
+        f = fn_;
+      }
+      (*f)(i);
+      std::lock_guard<std::mutex> lk(mu_);
+      if (--left_ == 0) done_.notify_all();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex run_mu_, mu_;
+  std::condition_variable cv_, done_;
+  const std::function<void(int)>* fn_ = nullptr;
+  int n_ = 0, next_ = 0, left_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
+/* memcpy split over the host workers (pageable <-> pinned staging) */
+void par_copy(void* dst, const void* src, uint64_t bytes)
+{
+  HostPool& hp = HostPool::get();
+  const int nt = hp.size();
+  if (nt == 1 || bytes < (8u << 20)) {
+    memcpy(dst, src, bytes);
+    return;
+  }
+  const uint64_t part = ((bytes + nt - 1) / nt + 4095) & ~4095ull;
+  hp.run(nt, [&](int t) {
+    const uint64_t b = part * t;
+    if (b >= bytes) return;
+    const uint64_t len = bytes - b < part ? bytes - b : part;
+    memcpy((uint8_t*) dst + b, (const uint8_t*) src + b, len);
+  });
+}
+
+/* ASCII rows -> word-major code words of one chunk, over the host workers */
+static void par_pack(const char* src, uint64_t n, uint32_t size, uint32_t* out)
+{
+  HostPool& hp = HostPool::get();
+  const int parts = n < 4096 ? 1 : hp.size();
+  hp.run(parts, [&](int t) {
+    const uint64_t r0 = n * t / parts, r1 = n * (t + 1) / parts;
+    kfmi_pack_rows((const uint8_t*) src + r0 * size, r1 - r0, size, out + r0, n);
+  });
+}
+
+extern "C" int32_t kfmi_host_alloc(uint64_t bytes, void** p)
+{
+  if (!p) return KFMI_E_BAD_ARGUMENT;
+  *p = nullptr;
+  if (hipSetDevice(kfmi_current_device()) != hipSuccess) return KFMI_E_NO_DEVICE;
+  if (hipHostMalloc(p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return KFMI_E_ALLOCATING_MFASTA;
+  return KFMI_SUCCESS;
+}
+
+extern "C" int32_t kfmi_host_free(void* p)
+{
+  if (p && hipHostFree(p) != hipSuccess) return KFMI_E_BAD_ARGUMENT;
+  return KFMI_SUCCESS;
+}
+
+extern "C" int32_t kfmi_stream_release(void)
+{
+  const int dev = kfmi_current_device();
+  if (dev < 0 || dev >= 64) return KFMI_E_NO_DEVICE;
+  std::lock_guard<std::mutex> lk(g_ctx_mu);
+  pool_free(dev);
+  return KFMI_SUCCESS;
+}
+
+extern "C" int32_t kfmi_search_stream(void* index, const char* ascii, uint64_t num, uint32_t size,
+                                      uint32_t* results, uint64_t chunk)
+{
+  kfmi_fmi_t* f = (kfmi_fmi_t*) index;
+  if (!f || (!ascii && num) || (!results && num)) return KFMI_E_BAD_ARGUMENT;
+  if (!f->dev) return KFMI_E_NOT_ON_DEVICE;
+  kfmi_dev_index* di = f->dev;
+  const uint32_t K = di->K;
+  if (size == 0 || size % K || 64ull * size > 160ull * 1024) return KFMI_E_BAD_ARGUMENT;
+  DevCtx* ctx = nullptr;
+  int32_t err = ctx_for(di->device, &ctx);
+  if (err) return err;
+  if (num == 0) return KFMI_SUCCESS;
+  const char* hp = getenv("KFMI_STREAM_HOSTPACK");
+  const bool host_pack = !hp || atoi(hp) != 0;
+  const uint64_t def_chunk = host_pack ? (1ull << 19) : (1ull << 16);   /* profiles/r01/e2e_sweep*.jsonl */
+  if (chunk == 0) {
+    const char* e = getenv("KFMI_STREAM_CHUNK");
+    chunk = e ? strtoull(e, nullptr, 10) : def_chunk;
+  }
+  if (chunk == 0) chunk = def_chunk;
+  if (chunk > num) chunk = num;
+  const uint32_t steps = size / K, spw = 32 / (2 * K), nwords = (steps + spw - 1) / spw;
+  const bool pin_in = host_pinned(ascii), pin_out = host_pinned(results);
+
+  std::lock_guard<std::mutex> lk(g_ctx_mu);   /* one streamed search per device at a time */
+  StreamPool& pool = g_pool[di->device];
+  pool.init = true;
+  for (StreamSlot& s : pool.slot) {
+    err = slot_reserve(s, chunk, size, nwords, !pin_in && !host_pack, !pin_out, host_pack);
+    if (err) return err;
+    s.busy = false;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  const Op op = is_coop(di->backend) ? Op::Coop : Op::Task;
+  IdxArgs ix = idx_args(di);
+  err = use_ftab(di, ctx->st, ix, ftab_bases());
+  if (err) return err;
+  int32_t status = KFMI_SUCCESS;
+  using clk = std::chrono::steady_clock;
+  double host_ms = 0, wait_ms = 0;   /* host packing/staging; blocked on the GPU */
+  auto since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
+  auto retire = [&](StreamSlot& s) {
+    if (!s.busy) return;
+    const auto tw = clk::now();
+    const bool ok = hipEventSynchronize(s.done) == hipSuccess;
+    wait_ms += since(tw);
+    if (!ok) status = KFMI_E_KERNEL;
+    else if (!pin_out) par_copy(results + 2 * s.q0, s.h_out, 8ull * s.n);
+    s.busy = false;
+  };
+  const uint64_t nchunks = (num + chunk - 1) / chunk;
+  for (uint64_t i = 0; i < nchunks && status == KFMI_SUCCESS; ++i) {
+    StreamSlot& s = pool.slot[i % NSLOT];
+    retire(s);
+    if (status) break;
+    s.q0 = i * chunk;
+    s.n = num - s.q0 < chunk ? num - s.q0 : chunk;
+    const char* src = ascii + s.q0 * size;
+    const uint64_t bytes = s.n * size;
+    const void* hsrc = src;
+    const auto th = clk::now();
+    if (host_pack) par_pack(src, s.n, size, s.h_pk);
+    else if (!pin_in) {
+      par_copy(s.h_in, src, bytes);
+      hsrc = s.h_in;
+    }
+    host_ms += since(th);
+    s.dq.device = di->device;
+    s.dq.num = s.n;
+    s.dq.size = size;
+    s.dq.K = K;
+    s.dq.steps = steps;
+    s.dq.nwords = nwords;
+    SearchLaunch a;
+    a.st = s.st;
+    a.ix = ix;
+    a.qp = s.dq.packed;
+    a.ascii = s.dq.ascii;
+    a.m = size;
+    a.maxw = host_pack ? 0 : fused_maxw(di->backend, nwords);
+    a.num = s.n;
+    a.steps = steps;
+    a.nwords = nwords;
+    a.res = s.d_res;
+    void* hdst = pin_out ? (void*) (results + 2 * s.q0) : (void*) s.h_out;
+    const bool up_ok = host_pack
+                           ? hipMemcpyAsync(s.dq.packed, s.h_pk, 4ull * nwords * s.n, hipMemcpyHostToDevice, s.st) ==
+                                 hipSuccess
+                           : (hipMemcpyAsync(s.dq.ascii, hsrc, bytes, hipMemcpyHostToDevice, s.st) == hipSuccess &&
+                              (a.maxw || launch_pack(&s.dq, s.st) == hipSuccess));
+    if (!up_ok || dispatch(op, K, di->nb, di->layout, a) != hipSuccess ||
+        hipMemcpyAsync(hdst, s.d_res, 8ull * s.n, hipMemcpyDeviceToHost, s.st) != hipSuccess ||
+        hipEventRecord(s.done, s.st) != hipSuccess) {
+      status = KFMI_E_KERNEL;
+      break;
+    }
+    s.busy = true;
+  }
+  for (StreamSlot& s : pool.slot) retire(s);
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  t_ms[0] = ms;
+  t_ms[1] = host_ms;   /* host packing or staging copies */
+  t_ms[2] = wait_ms;   /* blocked on chunks in flight */
+  return status;
+}
+
+}  // namespace kfmi
