@@ -4,7 +4,7 @@ backward search (3 Gbase synthetic reference, 10M x 100 bp reads, K=2, d=64)
 on N MI355X, one process per GPU, plus the achieved HBM fraction of the LF
 kernel and the CPU oracle timed on the host cores.
 
-  python bench.py --gpus 1 --steps 10 --warmup 3
+  python bench.py --gpus 1 --steps 10 --warmup 20
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
       --master-port P bench.py --gpus N
 
@@ -44,7 +44,9 @@ def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
-    p.add_argument("--warmup", type=int, default=3)
+    # right after the upload the LF kernel needs ~10 steps to reach its steady
+    # rate (9.9 -> 9.55 ms, profiles/r01/idle_probe.jsonl); 20 warmup steps = 0.2 s
+    p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--backend", default="task-mid")
     p.add_argument("--ref-size", type=int, default=3_000_000_000)
     p.add_argument("--queries", type=int, default=10_000_000)
@@ -181,7 +183,7 @@ def config1_leg(backend: str, thr: int, steps: int = 5) -> dict:
     reads = synth.reads_64m(text, rng)
     q = K.Queries.from_array(reads)
     r = K.Results.alloc(reads.shape[0])
-    wall, lf, tot = time_backend(idx, q, r, backend, steps, 2)
+    wall, lf, tot = time_backend(idx, q, r, backend, steps, 20)
     res = r.array().copy()
     out = {"backend": backend, "mqps": round(reads.shape[0] * steps / wall / 1e6, 2), "lf_ms": round(lf, 3),
            "results_md5_pinned": synth.results_md5(res) == synth.MD5["res64"]}
@@ -352,7 +354,7 @@ def main():
         # ---- other backends (same index, same reads) ------------------------
         for b in [x for x in a.variants.split(",") if x and x != a.backend]:
             try:
-                wall, lf, tot = time_backend(idx, q, r, b, a.variant_steps, 1)
+                wall, lf, tot = time_backend(idx, q, r, b, a.variant_steps, 10)
                 ok = bool(np.array_equal(r.array(), res))
                 extra[b] = {"mqps": round(reads.shape[0] * a.variant_steps / wall / 1e6, 2),
                             "lf_ms": round(lf, 3), "step_ms": round(tot, 3), "results_equal": ok,
