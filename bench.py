@@ -56,7 +56,10 @@ def parse():
     p.add_argument("--d", type=int, default=64)
     p.add_argument("--cpu-sample", type=int, default=2_000_000,
                    help="queries of the CPU-oracle baseline sample (0 = skip)")
-    p.add_argument("--cpu-threads", type=int, default=0)
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="threads of the CPU baseline (0: every core in this process's affinity mask)")
+    p.add_argument("--parity-sample", type=int, default=100_000,
+                   help="reads per rank checked against the CPU oracle after the timed region (0 = skip)")
     p.add_argument("--cpu-port-only", action="store_true",
                    help="time only our restatement, not the reference's CPU binary (oracle/_ref)")
     p.add_argument("--variants", default="task,coop,task-ac,coop-ac,task-ac128,coop-ac128,task-packed,coop-packed,"
@@ -105,6 +108,14 @@ class Dist:
         self.pg.all_reduce(t, op=self.pg.ReduceOp.SUM)
         return float(t.item())
 
+    def gather(self, obj) -> list:
+        """Every rank's `obj` (JSON-able), in rank order, on every rank."""
+        if not self.pg:
+            return [obj]
+        out = [None] * self.world
+        self.pg.all_gather_object(out, obj)
+        return out
+
     def close(self):
         if self.pg:
             self.pg.destroy_process_group()
@@ -125,6 +136,41 @@ def make_text(n: int) -> bytes:
     import random
     rng = random.Random(n)
     return rng.randbytes(n).translate(synth.TBL)
+
+
+def cpu_threads() -> int:
+    """Every core this process may run on (its affinity mask), SURVEY 8(d)."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
+
+
+def cpu_quota() -> float | None:
+    """CPUs granted by the cgroup (cpu.max quota / period), None when unlimited."""
+    for fn in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(fn).read().split()[:2]
+            if q != "max":
+                return round(int(q) / int(per), 2)
+        except (OSError, ValueError):
+            pass
+    return None
+
+
+def aggregate_ranks(rows: list) -> dict:
+    """Whole-job view of the per-rank rows (rank, device, lf_ms, step_ms,
+    queries, parity_ok, ...): min/max LF time over ranks and the AND of every
+    rank's oracle-sample parity."""
+    lf = [r["lf_ms"] for r in rows]
+    st = [r["step_ms"] for r in rows]
+    oks = [r.get("parity_ok") for r in rows]
+    return {"n_ranks": len(rows),
+            "lf_ms_min": round(min(lf), 4), "lf_ms_max": round(max(lf), 4),
+            "step_ms_min": round(min(st), 4), "step_ms_max": round(max(st), 4),
+            "queries": int(sum(r["queries"] for r in rows)),
+            "parity_ok_all": None if any(o is None for o in oks) else bool(all(oks)),
+            "ranks": rows}
 
 
 def cpu_model() -> str:
@@ -291,6 +337,21 @@ def main():
     if pinned and a.qlen == 100 and a.queries == 10_000_000 and D.rank == 0 and not a.no_md5:
         results_md5_ok = synth.results_md5(res) == synth.MD5["res3g.q10M"]
         log(f"results md5 pinned-ok={results_md5_ok}")
+    # every rank: an evenly spread sample of its own results against the CPU
+    # oracle (oracle/fmi_oracle.c, test infrastructure; never on the timed path),
+    # with the semantics of the backend (AltCounters for the *-ac backends)
+    parity_ok, ns_par = None, min(a.parity_sample, reads.shape[0])
+    if ns_par > 0:
+        from oracle import oracle
+        t = time.perf_counter()
+        sel = np.linspace(0, reads.shape[0] - 1, ns_par).astype(np.int64)
+        ac = a.backend in ("task-ac", "coop-ac", "task-ac128", "coop-ac128")
+        img_idx = idx.alt_counters()[0] if ac else idx
+        want, _ = oracle.search(img_idx.image(), reads[sel], nthreads=max(1, cpu_threads() // D.world))
+        parity_ok = bool(np.array_equal(want.reshape(-1, 2), res.reshape(-1, 2)[sel]))
+        if ac:
+            img_idx.close()
+        log(f"rank {D.rank}: oracle sample {ns_par} reads parity_ok={parity_ok} ({time.perf_counter() - t:.1f}s)")
 
     # ---- roofline: algorithmic bytes of the LF kernel ------------------------
     blocks = K.count_blocks(idx, q)
@@ -310,7 +371,7 @@ def main():
     # (scripts/traffic_from_pmc.py: TCC_EA0_RDREQ x line bytes, gfx950-corrected)
     traffic, traffic_src, rdreq = None, None, None
     tj = Path(a.traffic_json)
-    if tj.exists():
+    if tj.exists() and D.world == 1:   # a one-GPU PMC profile says nothing about N > 1 runs
         try:
             tr = json.loads(tj.read_text())
             if (tr.get("backend") == a.backend and tr.get("queries") == a.queries and tr.get("ref_size") == a.ref_size
@@ -319,6 +380,13 @@ def main():
                 rdreq = tr.get("rdreq_per_launch")
         except Exception:
             traffic = None
+
+    rank_rows = D.gather({"rank": D.rank, "device": dev, "queries": int(reads.shape[0]),
+                          "lf_ms": round(float(np.mean(lf_ms)), 4), "step_ms": round(float(np.mean(tot_ms)), 4),
+                          "elapsed_s": round(elapsed, 4), "distinct_blocks": int(blocks),
+                          "parity_ok": parity_ok, "parity_sample": int(ns_par),
+                          "results_md5_pinned": results_md5_ok})
+    ranks = aggregate_ranks(rank_rows)
 
     extra = {}
     cpu = None
@@ -363,6 +431,27 @@ def main():
             except K.KfmiError as e:
                 extra[b] = {"error": str(e)}
             idx.free_gpu()
+        # ---- device-group replication (kfmi_set_devices): the layout is built
+        # once and fanned out device-to-device; here one card listed n times ----
+        try:
+            K.set_backend(a.backend)
+            reps = {}
+            for nrep in (1, 2, 4):
+                K.set_devices([dev] * nrep if nrep > 1 else [])
+                idx.free_gpu()
+                t = time.perf_counter()
+                K.transfer_to_gpu(idx, None, None)
+                reps[str(nrep)] = round(time.perf_counter() - t, 3)
+            K.set_devices([])
+            idx.free_gpu()
+            extra["group_replication"] = {"setup_s_by_replicas": reps,
+                                          "what": "transferCPUtoGPU(index) for a device group of n replicas "
+                                                  "on this card: host upload + relayout on the first, "
+                                                  "hipMemcpyPeerAsync to the others"}
+            log(f"group replication {extra['group_replication']}")
+        except K.KfmiError as e:
+            K.set_devices([])
+            extra["group_replication"] = {"error": str(e)}
         # ---- end to end from host memory: streamed H2D + search + D2H ------
         if a.e2e_steps > 0:
             try:
@@ -394,44 +483,48 @@ def main():
                 K.load().kfmi_stream_release()
             except K.KfmiError as e:
                 extra["end_to_end"] = {"error": str(e)}
-        # ---- CPU baseline: the oracle restatement on the host cores ---------
-        if a.cpu_sample > 0:
-            from oracle import oracle
-            thr = a.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-            ns = min(a.cpu_sample, reads.shape[0])
-            img = idx.image()
-            t = time.perf_counter()
-            cres, _ = oracle.search(img, reads[:ns], nthreads=thr)
-            cpu_s = time.perf_counter() - t
-            port = {"value": round(ns / cpu_s / 1e6, 4), "unit": "Mqueries/s", "cores": thr, "kind": "port",
-                    "sample": f"first {ns} of the same 10M reads, 1 pass, oracle/fmi_oracle.c "
-                              f"(restatement of fmIndexCPUBaseline.c), OMP threads={thr}, {cpu_s:.2f}s",
-                    "parity_with_gpu": bool(np.array_equal(cres, res[:2 * ns]))}
-            log(f"cpu baseline (port) {port}")
-            cpu = None
-            if not a.cpu_port_only:
-                try:
-                    cpu = cpu_reference_baseline(idx, reads, ns, a.k, a.d, thr, res)
-                except Exception as e:          # the reference binary is a baseline, never the product
-                    log(f"reference cpu baseline unavailable: {e}")
-            if cpu is None:
-                cpu = port
-            else:
-                extra["cpu_port"] = port
-            cpu["cpu_model"] = cpu_model()
-            if a.config1:
-                try:
-                    extra["config1_64mbase"] = config1_leg(a.backend, thr)
-                    log(f"config #1 {extra['config1_64mbase']}")
-                except K.KfmiError as e:
-                    extra["config1_64mbase"] = {"error": str(e)}
-            # single-thread rate of the restatement on a small slice
-            n1 = min(100_000, ns)
-            t = time.perf_counter()
-            oracle.search(img, reads[:n1], nthreads=1)
-            extra["cpu_port_1thread"] = {"value": round(n1 / (time.perf_counter() - t) / 1e6, 4),
-                                         "unit": "Mqueries/s", "cores": 1, "sample": f"first {n1} reads"}
-            log(f"cpu baseline {cpu}")
+    # ---- CPU baseline on rank 0 at any N: the reference's CPU searcher and the
+    # restatement on every core of the affinity mask (other ranks wait) --------
+    if D.rank == 0 and a.cpu_sample > 0:
+        from oracle import oracle
+        thr = a.cpu_threads or cpu_threads()
+        ns = min(a.cpu_sample, reads.shape[0])
+        img = idx.image()
+        t = time.perf_counter()
+        cres, _ = oracle.search(img, reads[:ns], nthreads=thr)
+        cpu_s = time.perf_counter() - t
+        port = {"value": round(ns / cpu_s / 1e6, 4), "unit": "Mqueries/s", "cores": thr, "kind": "port",
+                "sample": f"first {ns} of the same 10M reads, 1 pass, oracle/fmi_oracle.c "
+                          f"(restatement of fmIndexCPUBaseline.c), OMP threads={thr}, {cpu_s:.2f}s",
+                "parity_with_gpu": bool(np.array_equal(cres, res[:2 * ns]))}
+        log(f"cpu baseline (port) {port}")
+        cpu = None
+        if not a.cpu_port_only:
+            try:
+                cpu = cpu_reference_baseline(idx, reads, ns, a.k, a.d, thr, res)
+            except Exception as e:          # the reference binary is a baseline, never the product
+                log(f"reference cpu baseline unavailable: {e}")
+        if cpu is None:
+            cpu = port
+        else:
+            extra["cpu_port"] = port
+        cpu["cpu_model"] = cpu_model()
+        cpu["affinity_cores"] = cpu_threads()
+        cpu["os_cpu_count"] = os.cpu_count()
+        cpu["cgroup_cpu_quota"] = cpu_quota()
+        if a.config1 and D.world == 1:
+            try:
+                extra["config1_64mbase"] = config1_leg(a.backend, thr)
+                log(f"config #1 {extra['config1_64mbase']}")
+            except K.KfmiError as e:
+                extra["config1_64mbase"] = {"error": str(e)}
+        # single-thread rate of the restatement on a small slice
+        n1 = min(100_000, ns)
+        t = time.perf_counter()
+        oracle.search(img, reads[:n1], nthreads=1)
+        extra["cpu_port_1thread"] = {"value": round(n1 / (time.perf_counter() - t) / 1e6, 4),
+                                     "unit": "Mqueries/s", "cores": 1, "sample": f"first {n1} reads"}
+        log(f"cpu baseline {cpu}")
 
     if D.rank == 0:
         line = {
@@ -469,12 +562,15 @@ def main():
                          "line_requests_G_per_s": round(rdreq / (lf_avg_ms / 1e3) / 1e9, 2) if rdreq else None,
                          "line_request_ceiling_G_per_s": PROBE_CEILING_GLINES},
             "cpu_baseline": cpu,
-            "parity": {"index_md5_pinned": index_md5_ok, "results_md5_pinned": results_md5_ok},
+            "parity": {"index_md5_pinned": index_md5_ok, "results_md5_pinned": results_md5_ok,
+                       "oracle_sample_ok": ranks["parity_ok_all"], "oracle_sample_per_rank": int(ns_par)},
+            "ranks": ranks,
             "setup_s": {"gpu_index_build": round(build_s, 2), "h2d": round(upload_s, 2), "d2h": round(d2h_s, 3)},
             "device_index_bytes": dev_index_bytes,
             "variants": extra,
         }
         print(json.dumps(line), flush=True)
+    D.barrier()          # every rank leaves together (rank 0 ran the CPU baseline)
     D.close()
 
 

@@ -4,6 +4,8 @@
  */
 #include <stdlib.h>
 #include <new>
+#include <thread>
+#include <vector>
 
 #include "kfmi_runtime.h"
 
@@ -95,6 +97,61 @@ void group_free_results(kfmi_res_t* r)
   r->grp = nullptr;
 }
 
+/* A replica of `src` on device `dev`: same geometry, device buffers copied
+ * device-to-device on `st` (hipMemcpyPeerAsync: over xGMI between GPUs, a
+ * local copy when `dev` is src's own device).  Returns with the copies queued. */
+static int32_t replicate_index(const kfmi_dev_index* src, int dev, hipStream_t st, kfmi_dev_index** out)
+{
+  kfmi_dev_index* di = new (std::nothrow) kfmi_dev_index();
+  if (!di) return KFMI_E_ALLOCATING_FMI;
+  di->device = dev;
+  di->backend = src->backend;
+  di->layout = src->layout;
+  di->K = src->K;
+  di->d = src->d;
+  di->nb = src->nb;
+  di->bwtsize = src->bwtsize;
+  di->nentries = src->nentries;
+  di->dl = src->dl;
+  di->ent_bytes = src->ent_bytes;
+  di->sb_bytes = src->sb_bytes;
+  di->sa_bytes = src->sa_bytes;
+  di->sa_log2 = src->sa_log2;
+  di->sa_gen = src->sa_gen;
+  struct Buf { uint32_t* const* from; uint32_t** to; uint64_t bytes; };
+  const Buf bufs[3] = {{&src->ent, &di->ent, src->ent_bytes}, {&src->sb, &di->sb, src->sb_bytes},
+                       {&src->sa, &di->sa, src->sa ? src->sa_bytes + 4 : 0}};
+  for (const Buf& b : bufs) {
+    if (!*b.from || !b.bytes) continue;
+    if (hipMalloc((void**) b.to, b.bytes) != hipSuccess) {
+      *b.to = nullptr;
+      free_dev_index(di);
+      return KFMI_E_DEVICE_ALLOC;
+    }
+    if (hipMemcpyPeerAsync(*b.to, dev, *b.from, src->device, b.bytes, st) != hipSuccess) {
+      free_dev_index(di);
+      return KFMI_E_KERNEL;
+    }
+  }
+  *out = di;
+  return KFMI_SUCCESS;
+}
+
+/* fn(i) for every member i on its own host thread (hipSetDevice is per thread),
+ * first error wins. */
+template <class F>
+static int32_t each_member(int n, F fn)
+{
+  std::vector<int32_t> errs(n, KFMI_SUCCESS);
+  std::vector<std::thread> th;
+  th.reserve(n);
+  for (int i = 0; i < n; ++i) th.emplace_back([&, i] { errs[i] = fn(i); });
+  for (auto& t : th) t.join();
+  for (int32_t e : errs)
+    if (e) return e;
+  return KFMI_SUCCESS;
+}
+
 int32_t group_transfer(kfmi_fmi_t* f, kfmi_qrys_t* q, kfmi_res_t* r, const int* devs, int n)
 {
   const int backend = kfmi_backend();
@@ -110,15 +167,32 @@ int32_t group_transfer(kfmi_fmi_t* f, kfmi_qrys_t* q, kfmi_res_t* r, const int* 
       g->n = n;
       g->backend = backend;
       f->grp = g;
+      /* the layout is built once, on the first member (host -> device upload and
+       * the relayout kernels), then fanned out device-to-device to the others,
+       * every copy queued on its destination's stream before any is waited for
+       * (one-time replication over xGMI, no host round trip) */
       for (int i = 0; i < n && !err; ++i) {
         g->dev[i] = devs[i];
         DevCtx* ctx = nullptr;
         err = ctx_for(devs[i], &ctx);
-        if (!err) err = upload_index(f, backend, devs[i], ctx, &g->di[i]);
         if (!err && hipStreamCreateWithFlags(&g->st[i], hipStreamNonBlocking) != hipSuccess) err = KFMI_E_NO_DEVICE;
         for (int k = 0; k < 3 && !err; ++k)
           if (hipEventCreate(&g->ev[i][k]) != hipSuccess) err = KFMI_E_NO_DEVICE;
+        if (!err && i == 0) err = upload_index(f, backend, devs[0], ctx, &g->di[0]);
       }
+      for (int i = 1; i < n && !err; ++i) {
+        int can = 0;
+        (void) hipSetDevice(devs[i]);
+        if (devs[i] != devs[0] && hipDeviceCanAccessPeer(&can, devs[i], devs[0]) == hipSuccess && can &&
+            hipDeviceEnablePeerAccess(devs[0], 0) != hipSuccess)
+          (void) hipGetLastError();   /* already enabled: fine; else the copy is staged by the runtime */
+        err = replicate_index(g->di[0], devs[i], g->st[i], &g->di[i]);
+      }
+      for (int i = 1; i < n; ++i)
+        if (g->st[i]) {
+          (void) hipSetDevice(devs[i]);
+          if (hipStreamSynchronize(g->st[i]) != hipSuccess && !err) err = KFMI_E_KERNEL;
+        }
       if (err) {
         group_free_index(f);
         return err;
@@ -139,16 +213,18 @@ int32_t group_transfer(kfmi_fmi_t* f, kfmi_qrys_t* q, kfmi_res_t* r, const int* 
     GroupSlices* g = group_slices(q->num, devs, n);
     if (!g) return KFMI_E_ALLOCATING_MFASTA;
     q->grp = g;
-    for (int i = 0; i < n && !err; ++i) {
+    /* every slice over its own device's PCIe link at the same time */
+    err = each_member(n, [&](int i) {
       DevCtx* ctx = nullptr;
-      err = ctx_for(devs[i], &ctx);
+      int32_t e = ctx_for(devs[i], &ctx);
       kfmi_qrys_t sh{};
       sh.num = g->num[i];
       sh.size = q->size;
       sh.h_queries = q->h_queries + g->q0[i] * q->size;
-      if (!err) err = upload_queries(&sh, f->steps, devs[i], ctx);
+      if (!e) e = upload_queries(&sh, f->steps, devs[i], ctx);
       g->dq[i] = sh.dev;
-    }
+      return e;
+    });
     if (err) {
       group_free_queries(q);
       return err;

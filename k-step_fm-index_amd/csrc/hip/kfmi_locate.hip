@@ -100,6 +100,8 @@ static int32_t locate_on(kfmi_fmi_t* f, kfmi_dev_index* di, uint32_t* d_res, uin
   DevCtx* ctx = nullptr;
   int32_t err = ctx_for(di->device, &ctx);
   if (err) return err;
+  hipEvent_t* ev = thread_events(di->device);
+  if (!ev) return KFMI_E_NO_DEVICE;
   if (!di->sa || di->sa_gen != f->sa_gen) {
     err = upload_sa(f, di, ctx);
     if (err) return err;
@@ -135,7 +137,7 @@ static int32_t locate_on(kfmi_fmi_t* f, kfmi_dev_index* di, uint32_t* d_res, uin
                                     rocprim::plus<uint64_t>(), st) == hipSuccess &&
             hipMalloc(&tmp, tb ? tb : 1) == hipSuccess;
   if (!ok) return done(KFMI_E_DEVICE_ALLOC);
-  if (hipEventRecord(ctx->ev[0], st) != hipSuccess) return done(KFMI_E_KERNEL);
+  if (hipEventRecord(ev[0], st) != hipSuccess) return done(KFMI_E_KERNEL);
   hipLaunchKernelGGL(loc_count_kernel, dim3((uint32_t) ((num + 1 + 255) / 256)), dim3(256), 0, st, d_res, num,
                      max_occ, d_cnt);
   ok = hipGetLastError() == hipSuccess &&
@@ -177,16 +179,16 @@ static int32_t locate_on(kfmi_fmi_t* f, kfmi_dev_index* di, uint32_t* d_res, uin
   a.owner = d_own;
   a.total = total;
   a.pos = d_pos;
-  ok = hipEventRecord(ctx->ev[1], st) == hipSuccess &&
+  ok = hipEventRecord(ev[1], st) == hipSuccess &&
        (total == 0 || dispatch(Op::Locate, di->K, di->nb, di->layout, a) == hipSuccess) &&
-       hipEventRecord(ctx->ev[2], st) == hipSuccess &&
+       hipEventRecord(ev[2], st) == hipSuccess &&
        hipMemcpyAsync(L->h_off, d_off, 8 * (num + 1), hipMemcpyDeviceToHost, st) == hipSuccess &&
        (total == 0 || hipMemcpyAsync(L->h_pos, d_pos, 4 * total, hipMemcpyDeviceToHost, st) == hipSuccess) &&
        hipStreamSynchronize(st) == hipSuccess;
   if (!ok) return done(KFMI_E_KERNEL);
   float ms01 = 0, ms12 = 0;
-  (void) hipEventElapsedTime(&ms01, ctx->ev[0], ctx->ev[1]);
-  (void) hipEventElapsedTime(&ms12, ctx->ev[1], ctx->ev[2]);
+  (void) hipEventElapsedTime(&ms01, ev[0], ev[1]);
+  (void) hipEventElapsedTime(&ms12, ev[1], ev[2]);
   t_ms[0] = ms01 + ms12;   /* scan + walk (the host read of the total sits between) */
   t_ms[1] = ms01;
   t_ms[2] = ms12;          /* the locate kernel alone */
@@ -203,6 +205,7 @@ extern "C" int32_t kfmi_locate(void* index, void* results, uint32_t max_occ, voi
   if (!f->h_sa || !f->sa_rate) return KFMI_E_BAD_ARGUMENT;   /* index built without SA samples */
   if (!f->grp && !r->grp) {
     if (!f->dev || !r->d_results) return KFMI_E_NOT_ON_DEVICE;
+    if (r->d_device != f->dev->device) return KFMI_E_BAD_ARGUMENT;
     return locate_on(f, f->dev, r->d_results, r->num, max_occ, (kfmi_locations**) locations);
   }
   /* device group: every member locates its slice, the lists are concatenated */

@@ -42,8 +42,11 @@ struct kfmi_dev_index {
   uint32_t* sa = nullptr;      /* locate: row-sampled suffix array */
   uint64_t sa_bytes = 0;
   uint32_t sa_log2 = 0, sa_gen = 0;
-  uint2* ftab = nullptr;       /* jump-start table of ftab_chars bases (0 = none) */
-  uint32_t ftab_chars = 0;
+  /* jump-start tables, one per base count (built on first use, then immutable
+   * until the index leaves the device, so concurrent searches with different
+   * kfmi_set_ftab values never free a table another kernel reads) */
+  uint2* ftab[17] = {};
+  std::mutex ftab_mu;
 };
 
 struct kfmi_dev_queries {
@@ -56,14 +59,15 @@ struct kfmi_dev_queries {
 
 namespace kfmi {
 
-/* One non-blocking stream and a set of timing events per device. */
+/* One non-blocking stream per device, shared by the threads that use it (their
+ * work is serialised on it).  Timing events are per calling thread. */
 struct DevCtx {
   bool init = false;
   hipStream_t st = nullptr;
-  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
 };
-extern std::mutex g_ctx_mu;   /* guards g_ctx; also one streamed search per device at a time */
-int32_t ctx_for(int dev, DevCtx** out);   /* selects `dev`, creates its stream and events once */
+int32_t ctx_for(int dev, DevCtx** out);   /* selects `dev`, creates its stream once */
+/* The calling thread's three timing events on device `dev` (current device). */
+hipEvent_t* thread_events(int dev);
 
 /* per calling thread (kfmi_search.hip) */
 extern thread_local int t_device;

@@ -134,22 +134,36 @@ extern "C" int32_t kfmi_last_timing(double* ms_total, double* ms_pack, double* m
 }
 
 static DevCtx g_ctx[64];
-std::mutex g_ctx_mu;
+static std::mutex g_ctx_mu;   /* guards the one-time creation of g_ctx[dev] only */
 
 int32_t ctx_for(int dev, DevCtx** out)
 {
   if (dev < 0 || dev >= 64) return KFMI_E_NO_DEVICE;
-  std::lock_guard<std::mutex> lk(g_ctx_mu);
-  DevCtx& c = g_ctx[dev];
   if (hipSetDevice(dev) != hipSuccess) return KFMI_E_NO_DEVICE;
-  if (!c.init) {
-    if (hipStreamCreateWithFlags(&c.st, hipStreamNonBlocking) != hipSuccess) return KFMI_E_NO_DEVICE;
-    for (int i = 0; i < 3; ++i)
-      if (hipEventCreate(&c.ev[i]) != hipSuccess) return KFMI_E_NO_DEVICE;
-    c.init = true;
+  DevCtx& c = g_ctx[dev];
+  {
+    std::lock_guard<std::mutex> lk(g_ctx_mu);
+    if (!c.init) {
+      if (hipStreamCreateWithFlags(&c.st, hipStreamNonBlocking) != hipSuccess) return KFMI_E_NO_DEVICE;
+      c.init = true;
+    }
   }
   *out = &c;
   return KFMI_SUCCESS;
+}
+
+/* Per thread and device, so that concurrent searches on one device do not
+ * overwrite each other's timing (never destroyed: a handful per thread). */
+hipEvent_t* thread_events(int dev)
+{
+  static thread_local hipEvent_t ev[64][3];
+  if (dev < 0 || dev >= 64) return nullptr;
+  for (int i = 0; i < 3; ++i)
+    if (!ev[dev][i] && hipEventCreate(&ev[dev][i]) != hipSuccess) {
+      ev[dev][i] = nullptr;
+      return nullptr;
+    }
+  return ev[dev];
 }
 
 /* ------------------------------------------------------------------------ */
@@ -517,7 +531,8 @@ void free_dev_index(kfmi_dev_index* di)
   if (di->ent) (void) hipFree(di->ent);
   if (di->sb) (void) hipFree(di->sb);
   if (di->sa) (void) hipFree(di->sa);
-  if (di->ftab) (void) hipFree(di->ftab);
+  for (uint2* t : di->ftab)
+    if (t) (void) hipFree(t);
   delete di;
 }
 
@@ -813,27 +828,27 @@ int32_t use_ftab(kfmi_dev_index* di, hipStream_t st, IdxArgs& ix, uint32_t bases
   ix.ftab = nullptr;
   ix.ftab_steps = 0;
   ix.ftab_mask = 0;
-  if (!bases || bases % di->K) return KFMI_SUCCESS;
-  if (di->ftab_chars != bases) {
-    if (di->ftab) (void) hipFree(di->ftab);
-    di->ftab = nullptr;
-    di->ftab_chars = 0;
-    const uint64_t n = 1ull << (2 * bases);
-    if (hipMalloc((void**) &di->ftab, 8 * n) != hipSuccess) {
-      di->ftab = nullptr;
-      return KFMI_E_DEVICE_ALLOC;
+  if (!bases || bases % di->K || bases > 16) return KFMI_SUCCESS;
+  {
+    std::lock_guard<std::mutex> lk(di->ftab_mu);
+    if (!di->ftab[bases]) {
+      const uint64_t n = 1ull << (2 * bases);
+      uint2* t = nullptr;
+      if (hipMalloc((void**) &t, 8 * n) != hipSuccess) return KFMI_E_DEVICE_ALLOC;
+      SearchLaunch a{};
+      a.st = st;
+      a.ix = idx_args(di);
+      a.ftab_out = t;
+      a.ftab_steps = bases / di->K;
+      a.ftab_n = n;
+      if (dispatch(Op::Ftab, di->K, di->nb, di->layout, a) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
+        (void) hipFree(t);
+        return KFMI_E_KERNEL;
+      }
+      di->ftab[bases] = t;   /* published complete; never replaced */
     }
-    SearchLaunch a{};
-    a.st = st;
-    a.ix = idx_args(di);
-    a.ftab_out = di->ftab;
-    a.ftab_steps = bases / di->K;
-    a.ftab_n = n;
-    if (dispatch(Op::Ftab, di->K, di->nb, di->layout, a) != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
-      return KFMI_E_KERNEL;
-    di->ftab_chars = bases;
   }
-  ix.ftab = di->ftab;
+  ix.ftab = di->ftab[bases];
   ix.ftab_steps = bases / di->K;
   ix.ftab_mask = bases >= 16 ? 0xFFFFFFFFu : (1u << (2 * bases)) - 1u;
   return KFMI_SUCCESS;
@@ -926,8 +941,14 @@ extern "C" int32_t transferCPUtoGPU(void* index, void* queries, void* results)
     if (err) return err;
   }
   if (r) {
-    if (r->d_results) { (void) hipFree(r->d_results); r->d_results = nullptr; }
+    if (r->d_results) {
+      (void) hipSetDevice(r->d_device);
+      (void) hipFree(r->d_results);
+      r->d_results = nullptr;
+      (void) hipSetDevice(dev);
+    }
     if (hipMalloc((void**) &r->d_results, 8ull * (r->num ? r->num : 1)) != hipSuccess) return KFMI_E_DEVICE_ALLOC;
+    r->d_device = dev;
     if (hipMemsetAsync(r->d_results, 0, 8ull * r->num, ctx->st) != hipSuccess ||
         hipStreamSynchronize(ctx->st) != hipSuccess)
       return KFMI_E_KERNEL;
@@ -987,10 +1008,13 @@ extern "C" int32_t kfmi_search(void* index, void* queries, void* results)
   if (f->grp || q->grp || r->grp) return group_search(f, q, r);
   if (!f->dev || !q->dev || !r->d_results) return KFMI_E_NOT_ON_DEVICE;
   kfmi_dev_index* di = f->dev;
+  if (r->d_device != di->device) return KFMI_E_BAD_ARGUMENT;   /* handles transferred to different devices */
   DevCtx* ctx = nullptr;
   int32_t err = ctx_for(di->device, &ctx);
-  if (!err) err = search_enqueue(di, q->dev, r->d_results, ctx->st, ctx->ev, ftab_bases());
-  if (!err) err = search_finish(ctx->st, ctx->ev, t_ms);
+  hipEvent_t* ev = err ? nullptr : thread_events(di->device);
+  if (!err && !ev) err = KFMI_E_NO_DEVICE;
+  if (!err) err = search_enqueue(di, q->dev, r->d_results, ctx->st, ev, ftab_bases());
+  if (!err) err = search_finish(ctx->st, ev, t_ms);
   return err;
 }
 
@@ -1048,7 +1072,7 @@ extern "C" int32_t transferGPUtoCPU(void* results)
   if (r && r->grp) return group_to_host(r);
   if (!r || !r->d_results) return KFMI_E_NOT_ON_DEVICE;
   DevCtx* ctx = nullptr;
-  int32_t err = ctx_for(kfmi_current_device(), &ctx);
+  int32_t err = ctx_for(r->d_device, &ctx);   /* the device the results live on, not the caller's current one */
   if (err) return err;
   HIP_OK(hipMemcpyAsync(r->h_results, r->d_results, 8ull * r->num, hipMemcpyDeviceToHost, ctx->st));
   HIP_OK(hipStreamSynchronize(ctx->st));
@@ -1083,6 +1107,7 @@ extern "C" int32_t freeResultsGPU(void** results)
   kfmi_res_t* r = results ? (kfmi_res_t*) *results : nullptr;
   if (r) group_free_results(r);
   if (r && r->d_results) {
+    (void) hipSetDevice(r->d_device);
     (void) hipFree(r->d_results);
     r->d_results = nullptr;
   }

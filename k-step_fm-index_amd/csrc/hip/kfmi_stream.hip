@@ -45,6 +45,9 @@ struct StreamPool {
   StreamSlot slot[NSLOT];
 };
 static StreamPool g_pool[64];
+/* one streamed search per device at a time; searches on different devices (one
+ * host thread each) and every other entry point run concurrently with it */
+static std::mutex g_pool_mu[64];
 
 static void pool_free(int dev)
 {
@@ -252,12 +255,14 @@ extern "C" int32_t kfmi_host_free(void* p)
   return KFMI_SUCCESS;
 }
 
+/* Frees the pools of every device (not only the caller's current one: the
+ * pools belong to the devices the searched indexes live on). */
 extern "C" int32_t kfmi_stream_release(void)
 {
-  const int dev = kfmi_current_device();
-  if (dev < 0 || dev >= 64) return KFMI_E_NO_DEVICE;
-  std::lock_guard<std::mutex> lk(g_ctx_mu);
-  pool_free(dev);
+  for (int dev = 0; dev < 64; ++dev) {
+    std::lock_guard<std::mutex> lk(g_pool_mu[dev]);
+    pool_free(dev);
+  }
   return KFMI_SUCCESS;
 }
 
@@ -286,7 +291,7 @@ extern "C" int32_t kfmi_search_stream(void* index, const char* ascii, uint64_t n
   const uint32_t steps = size / K, spw = 32 / (2 * K), nwords = (steps + spw - 1) / spw;
   const bool pin_in = host_pinned(ascii), pin_out = host_pinned(results);
 
-  std::lock_guard<std::mutex> lk(g_ctx_mu);   /* one streamed search per device at a time */
+  std::lock_guard<std::mutex> lk(g_pool_mu[di->device]);
   StreamPool& pool = g_pool[di->device];
   pool.init = true;
   for (StreamSlot& s : pool.slot) {

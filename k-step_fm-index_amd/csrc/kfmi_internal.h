@@ -60,6 +60,7 @@ typedef struct {
   uint64_t  num;
   uint32_t *h_results;     /* 2*num: [L0,R0,L1,R1,...] */
   uint32_t *d_results;     /* device copy (hipMalloc), NULL until transfer */
+  int32_t   d_device;      /* device holding d_results (valid while d_results != NULL) */
   void     *grp;           /* per-device slices on a device group */
 } kfmi_res_t;
 

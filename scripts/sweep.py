@@ -38,8 +38,9 @@ def main():
     p.add_argument("--backends", default="task-packed,task,task-ac,coop,coop-ac,coop-packed")
     p.add_argument("--env", default="", help="semicolon list of VAR=v1,v2 knobs swept for every backend")
     p.add_argument("--steps", type=int, default=5)
-    p.add_argument("--sort-suffix", type=int, default=0,
-                   help="experiment: order reads by their last N bases (backward-search order)")
+    p.add_argument("--sort-suffix", default="0",
+                   help="experiment: comma list of N; order reads by their last N bases (backward-search "
+                        "order, N <= 32), one pass over the backends per N")
     a = p.parse_args()
 
     K.load()
@@ -51,51 +52,66 @@ def main():
     t = time.perf_counter()
     idx = K.Index.build(text, k=a.k, d=a.d, gpu=True)
     log(f"build {time.perf_counter() - t:.1f}s")
-    reads = synth.gather_reads(text, synth.read_starts(len(text), a.queries, a.qlen, 10), a.qlen)
-    if a.sort_suffix:
-        cols = [reads[:, a.qlen - 1 - j] for j in range(a.sort_suffix)]
-        order = np.lexsort(cols[::-1])            # primary key: the last base
-        reads = np.ascontiguousarray(reads[order])
-        log(f"reads ordered by their last {a.sort_suffix} bases")
+    reads0 = synth.gather_reads(text, synth.read_starts(len(text), a.queries, a.qlen, 10), a.qlen)
     log("reads ready")
-    q = K.Queries.from_array(reads)
-    r = K.Results.alloc(reads.shape[0])
     knobs = [{}]
     for spec in [s for s in a.env.split(";") if s]:
         var, vals = spec.split("=")
         knobs = [dict(k, **{var: v}) for k in knobs for v in vals.split(",")]
     ref = None
-    for b in a.backends.split(","):
-        for kn in knobs:
-            for var, v in kn.items():
-                os.environ[var] = v
-            try:
-                K.set_backend(b)
-                K.transfer_to_gpu(idx, q, r)
-                K.search(idx, q, r)
-                lf, tot = [], []
-                t0 = time.perf_counter()
-                for _ in range(a.steps):
+    for ss in [int(x) for x in a.sort_suffix.split(",")]:
+        inv = None
+        reads = reads0
+        if ss:
+            # key: code of base m-1 most significant, then m-2, ... (the order the
+            # backward search consumes them), so reads sharing their last j bases
+            # are contiguous for every j <= ss
+            codes = ((reads0 >> 1) & 3).astype(np.uint64)     # A0 C1 G3 T2: a bijection, fine for grouping
+            key = np.zeros(reads0.shape[0], dtype=np.uint64)
+            for j in range(ss):
+                key = (key << np.uint64(2)) | codes[:, a.qlen - 1 - j]
+            order = np.argsort(key, kind="stable")
+            reads = np.ascontiguousarray(reads0[order])
+            inv = np.empty_like(order)
+            inv[order] = np.arange(order.size)
+            log(f"reads ordered by their last {ss} bases")
+        q = K.Queries.from_array(reads)
+        r = K.Results.alloc(reads.shape[0])
+        for b in a.backends.split(","):
+            for kn in knobs:
+                for var, v in kn.items():
+                    os.environ[var] = v
+                try:
+                    K.set_backend(b)
+                    K.transfer_to_gpu(idx, q, r)
                     K.search(idx, q, r)
-                    tm = K.last_timing()
-                    lf.append(tm["lf_ms"])
-                    tot.append(tm["total_ms"])
-                wall = (time.perf_counter() - t0) / a.steps
-                K.transfer_to_cpu(r)
-                res = r.array().copy()
-                if ref is None:
-                    ref = res
-                out = {"backend": b, "knobs": kn, "lf_ms": round(float(np.median(lf)), 3),
-                       "lf_ms_min": round(float(np.min(lf)), 3), "step_ms": round(float(np.median(tot)), 3),
-                       "wall_ms": round(wall * 1e3, 3), "mqps": round(reads.shape[0] / wall / 1e6, 1),
-                       "equal": bool(np.array_equal(res, ref)), "dev_bytes": idx.device_bytes()}
-            except K.KfmiError as e:
-                out = {"backend": b, "knobs": kn, "error": str(e)}
-            print(json.dumps(out), flush=True)
-            log(out)
-            for var in kn:
-                os.environ.pop(var, None)
-        idx.free_gpu()
+                    lf, tot = [], []
+                    t0 = time.perf_counter()
+                    for _ in range(a.steps):
+                        K.search(idx, q, r)
+                        tm = K.last_timing()
+                        lf.append(tm["lf_ms"])
+                        tot.append(tm["total_ms"])
+                    wall = (time.perf_counter() - t0) / a.steps
+                    K.transfer_to_cpu(r)
+                    res = r.array().copy()
+                    if inv is not None:
+                        res = res.reshape(-1, 2)[inv].reshape(-1)
+                    if ref is None:
+                        ref = res
+                    out = {"backend": b, "knobs": kn, "sort_suffix": ss, "lf_ms": round(float(np.median(lf)), 3),
+                           "lf_ms_min": round(float(np.min(lf)), 3), "step_ms": round(float(np.median(tot)), 3),
+                           "wall_ms": round(wall * 1e3, 3), "mqps": round(reads.shape[0] / wall / 1e6, 1),
+                           "equal": bool(np.array_equal(res, ref)), "dev_bytes": idx.device_bytes()}
+                except K.KfmiError as e:
+                    out = {"backend": b, "knobs": kn, "sort_suffix": ss, "error": str(e)}
+                print(json.dumps(out), flush=True)
+                log(out)
+                for var in kn:
+                    os.environ.pop(var, None)
+            idx.free_gpu()
+        q.close()
+        r.close()
 
 
 if __name__ == "__main__":

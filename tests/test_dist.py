@@ -28,8 +28,13 @@ WORKER = textwrap.dedent(r"""
     el = time.perf_counter() - t0
     el_max = D.max(el)
     total = D.sum(float(reads.shape[0]))
+    # per-rank rows as bench.py gathers them (rank 1 reports a failed parity sample)
+    rows = D.gather({"rank": D.rank, "device": D.local, "queries": int(reads.shape[0]),
+                     "lf_ms": 9.0 + D.rank, "step_ms": 9.5 + D.rank, "elapsed_s": el,
+                     "parity_ok": D.rank == 0, "parity_sample": 100})
+    agg = bench.aggregate_ranks(rows)
     out = json.dumps({"rank": D.rank, "world": D.world, "local": D.local, "el": el, "el_max": el_max,
-                      "total": total, "first": reads[0].tobytes().decode(), "start0": int(st[0])})
+                      "total": total, "first": reads[0].tobytes().decode(), "start0": int(st[0]), "agg": agg})
     with open("rank%%d.json" %% D.rank, "w") as f:
         f.write(out)
     D.close()
@@ -60,3 +65,22 @@ def test_two_rank_gloo_bench_plumbing(tmp_path):
         assert abs(r["el_max"] - max(x["el"] for x in rows)) < 1e-9
     # disjoint, deterministic shards: rank r uses read seed 10 + r
     assert rows[0]["start0"] != rows[1]["start0"]
+    # per-rank aggregation (bench.py "ranks"): same view on every rank
+    for r in rows:
+        agg = r["agg"]
+        assert agg == rows[0]["agg"]
+        assert agg["n_ranks"] == 2 and agg["queries"] == 2000
+        assert agg["lf_ms_min"] == 9.0 and agg["lf_ms_max"] == 10.0
+        assert agg["step_ms_min"] == 9.5 and agg["step_ms_max"] == 10.5
+        assert [x["rank"] for x in agg["ranks"]] == [0, 1]
+        assert agg["parity_ok_all"] is False                  # one failed rank fails the job
+
+
+def test_aggregate_ranks_single_and_cpu_threads():
+    import bench
+    agg = bench.aggregate_ranks([{"rank": 0, "device": 0, "queries": 10, "lf_ms": 1.5, "step_ms": 1.6,
+                                  "parity_ok": True}])
+    assert agg["parity_ok_all"] is True and agg["lf_ms_min"] == agg["lf_ms_max"] == 1.5
+    agg = bench.aggregate_ranks([{"rank": 0, "queries": 1, "lf_ms": 1, "step_ms": 1, "parity_ok": None}])
+    assert agg["parity_ok_all"] is None                       # sample skipped: no claim
+    assert bench.cpu_threads() == len(os.sched_getaffinity(0))

@@ -1,0 +1,105 @@
+"""GPU parity at the configs' own scale (BASELINE configs #2-#5): the 3 Gbase
+recipe text indexed on the device, searched by every
+backend through the C ABI.
+
+Pins (produced by the reference's own binaries,
+/root/reference/src/genFMindex.c:457-543 and fmIndexCPUBaseline.c:157-292):
+  * the GPU-built tag-100 index image           md5 38f85a87...
+  * the q1M reads (random.Random(1))            md5 973c43bb...
+  * every backend's q1M results file            md5 96148f99...
+  * the q10M reads (random.Random(10))          md5 6a87831e...
+  * the q10M results file (one backend's md5, every other backend equal)
+                                                md5 cfa6bc65...
+The 150 bp leg (config #5's read length) has no reference vector at this
+scale: 200K sampled + 50K random/N/lowercase reads are checked against the C
+restatement (oracle/fmi_oracle.c), plain and AltCounters semantics.
+
+The text has n+1 = 3,000,000,001 rows, so every LF here crosses 2^31.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+import util
+from test_gpu_parity import ALT, PLAIN
+
+pytestmark = pytest.mark.gpu
+
+N3G = 3_000_000_000
+
+
+@pytest.fixture(scope="module")
+def gpu(kfmi_mod):
+    if kfmi_mod.device_count() < 1:
+        pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
+    kfmi_mod.set_device(0)
+    return kfmi_mod
+
+
+@pytest.fixture(scope="module")
+def g3(gpu):
+    from kstep_fmi import synth
+    text = synth.text_3g(N3G)
+    idx = gpu.Index.build(text, k=2, d=64, gpu=True)
+    yield text, idx
+    idx.free_gpu()
+    idx.close()
+
+
+@pytest.fixture(scope="module")
+def reads(g3, oracle_mod):
+    """q1M, q10M (md5-pinned) and the 150 bp leg with its oracle results."""
+    from kstep_fmi import synth
+    text, idx = g3
+    q1m = synth.gather_reads(text, synth.read_starts(N3G, 1_000_000, 100, seed=1), 100)
+    q10m = synth.gather_reads(text, synth.read_starts(N3G, 10_000_000, 100, seed=10), 100)
+    rng = np.random.default_rng(150)
+    t = np.frombuffer(text, dtype=np.uint8)
+    st = rng.integers(0, N3G - 150, size=200_000)
+    q150 = np.concatenate([t[st[:, None] + np.arange(150)[None, :]],
+                           rng.choice(np.frombuffer(b"ACGTNacgt", dtype=np.uint8), size=(50_000, 150))])
+    want150, _ = oracle_mod.search(idx.image(), q150)
+    i200, i201 = idx.alt_counters()
+    i201.close()
+    want150ac, _ = oracle_mod.search(i200.image(), q150)
+    i200.close()
+    return {"q1m": q1m, "q10m": q10m, "q150": q150, "want150": want150, "want150ac": want150ac, "res10m": {}}
+
+
+def test_3g_index_md5_pinned(g3):
+    """GPU builder output == the reference builder's 3 Gbase tag-100 file."""
+    from kstep_fmi import synth
+    _, idx = g3
+    h = idx.header()
+    assert h["bwtsize"] == N3G + 1 and h["bwtsize"] > 2 ** 31
+    assert hashlib.md5(idx.image().tobytes()).hexdigest() == synth.MD5["ref3g.k2d64.fmi"]
+
+
+def test_3g_reads_md5_pinned(reads):
+    from kstep_fmi import synth
+    assert synth.qry_md5(reads["q1m"]) == synth.MD5["q1M.qry"]
+    assert synth.qry_md5(reads["q10m"]) == synth.MD5["q10M.qry"]
+
+
+@pytest.mark.parametrize("backend", ("task-mid",) + tuple(b for b in PLAIN + ALT if b != "task-mid"))
+def test_3g_backend_full_scale(gpu, g3, reads, backend, tmp_path):
+    from kstep_fmi import synth
+    _, idx = g3
+    # q1M: every backend's own results file md5 (configs #2-#4 read count 1M)
+    res = gpu.search_array(idx, reads["q1m"], backend)
+    assert int(res.max()) > 2 ** 31                       # rows past 2^31 are exercised
+    assert util.results_md5(gpu, res, tmp_path) == synth.MD5["res3g.q1M"], backend
+    # q10M: the headline batch; md5 once, then bit-equality with it
+    res = gpu.search_array(idx, reads["q10m"], backend)
+    ref = reads["res10m"]
+    if not ref:
+        assert util.results_md5(gpu, res, tmp_path) == synth.MD5["res3g.q10M"], backend
+        ref["res"] = res
+    else:
+        assert np.array_equal(res, ref["res"]), backend
+    # 150 bp (config #5's read length): oracle restatement, plain or AC semantics
+    want = reads["want150ac"] if backend in ALT else reads["want150"]
+    got = gpu.search_array(idx, reads["q150"], backend)
+    assert np.array_equal(got, want), (backend, int(np.flatnonzero(got != want)[0]))
+    idx.free_gpu()

@@ -121,3 +121,37 @@ def test_group_search_driver(tmp_path):
     assert p.returncode == 0, p.stdout + p.stderr
     want = (util.GOLDEN / "textA" / ent["results"]["100.100"]["file"]).read_bytes()
     assert (tmp_path / "idx.fmi.res.gpu").read_bytes() == want
+
+
+@pytest.mark.gpu
+def test_group_replication_setup_time(kfmi_mod):
+    """A group's index replicas are built once (host upload + relayout on the
+    first member) and fanned out device-to-device, so three replicas on one
+    card cost well under twice the single-device setup (64 Mbase, MID128)."""
+    import time
+    K = kfmi_mod
+    rng = np.random.default_rng(7)
+    text = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=1 << 26).tobytes()
+    idx = K.Index.build(text, k=2, d=64, gpu=True)
+    K.set_backend("task-mid")
+
+    def setup_s(group):
+        best = 1e9
+        for _ in range(3):
+            K.set_devices(group)
+            idx.free_gpu()
+            t = time.perf_counter()
+            K.transfer_to_gpu(idx, None, None)
+            best = min(best, time.perf_counter() - t)
+        return best
+
+    try:
+        one = setup_s([])
+        three = setup_s([0, 0, 0])
+        assert idx.device_bytes() > 0
+        print(f"setup single {one * 1e3:.1f} ms, group of 3 on one card {three * 1e3:.1f} ms")
+        assert three < 2 * one, (one, three)
+    finally:
+        K.set_devices([])
+        idx.free_gpu()
+        idx.close()

@@ -52,6 +52,25 @@ def golden_cases():
                            GOLDEN / case / r["file"])
 
 
+def results_md5(kfmi, res: np.ndarray, tmpdir) -> str:
+    """md5 of the reference results file for res = [L0,R0,...], written by the
+    library's writeResults (common.c:201-220 format, byte-identical to the
+    reference's per tests/test_dropin.py) -- fast at 10M queries."""
+    import ctypes
+    import hashlib
+    res = np.ascontiguousarray(res, dtype=np.uint32)
+    fn = Path(tmpdir) / "res.txt"
+    err = kfmi.load().writeResults(str(fn).encode(), res.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                                   res.size // 2)
+    assert err == 0, err
+    h = hashlib.md5()
+    with open(fn, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 24), b""):
+            h.update(blk)
+    fn.unlink()
+    return h.hexdigest()
+
+
 def code_of(x: int) -> int:
     """base2index (genFMindex.c:71-84)."""
     b1 = x & 4
