@@ -187,6 +187,10 @@ uint64_t  kfmi_results_num(void *results);
 int32_t kfmi_build_index_cpu(const char *text, uint64_t n, uint32_t k, uint32_t d, void **index);
 int32_t kfmi_build_index_gpu(const char *text, uint64_t n, uint32_t k, uint32_t d,
                              int32_t want_host_image, void **index);
+/* Diagnostics of the last GPU build in this process: sorted positions whose
+ * 32-base key tied with their predecessor, and the prefix-doubling rounds the
+ * device spent resolving them (0 when there were none). */
+int32_t kfmi_build_stats(uint64_t *ties, uint32_t *rounds);
 
 /* Dedup-aware algorithmic traffic of the last search: sum over queries and
  * steps of distinct d-blocks touched (1 if L/d == R/d else 2), SURVEY 8(d). */

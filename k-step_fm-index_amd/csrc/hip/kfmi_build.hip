@@ -21,6 +21,8 @@
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
+#include <rocprim/device/device_select.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -83,16 +85,104 @@ __global__ __launch_bounds__(256) void k_keys(const uint32_t* __restrict__ packe
   vals[i] = (uint32_t) i;
 }
 
+/* number of sorted positions j >= 1 whose 32-base key equals key j-1 (one
+ * atomic per wave) */
 __global__ __launch_bounds__(256) void k_ties(const uint64_t* __restrict__ keys, uint64_t n,
-                                              uint32_t* __restrict__ list, uint32_t cap,
                                               unsigned long long* __restrict__ count)
 {
   const uint64_t i = (uint64_t) blockIdx.x * 256 + threadIdx.x + 1;
-  if (i >= n) return;
-  if (keys[i] == keys[i - 1]) {
-    const unsigned long long slot = atomicAdd(count, 1ull);
-    if (slot < cap) list[slot] = (uint32_t) i;
-  }
+  const bool tie = i < n && keys[i] == keys[i - 1];
+  const uint64_t b = __ballot(tie);
+  if ((threadIdx.x & 63) == 0 && b) atomicAdd(count, (unsigned long long) __popcll(b));
+}
+
+/* ---- tie resolution by prefix doubling (Manber-Myers / Larsson-Sadakane on
+ * the device).  After the 32-base radix sort, positions j with equal keys form
+ * groups; rank[i] = group start (a position in SA order) of suffix i.  Round h
+ * (h = 32, 64, ...) re-sorts every non-singleton group by the rank of suffix
+ * i + h, which holds the order of chars h..2h-1.  Suffixes whose $ falls inside
+ * the first h chars (i + h >= n) take n - 1 - i: below every real rank (those
+ * are shifted by h) and shortest first -- '$' sorts lowest, and a padded key
+ * only ties with a longer suffix that has A where this one ends. */
+__device__ __forceinline__ uint64_t dbl_key(const uint32_t* __restrict__ rank, uint64_t n, uint64_t h, uint32_t i)
+{
+  return (uint64_t) i + h < n ? (uint64_t) rank[i + h] + h : n - 1 - (uint64_t) i;
+}
+
+/* head value (j if j starts a key group, else 0) for the max-scan of group starts */
+__global__ __launch_bounds__(256) void k_head_values(const uint64_t* __restrict__ keys, uint64_t n,
+                                                     uint32_t* __restrict__ hv)
+{
+  const uint64_t j = (uint64_t) blockIdx.x * 256 + threadIdx.x;
+  if (j >= n) return;
+  hv[j] = (j == 0 || keys[j] != keys[j - 1]) ? (uint32_t) j : 0u;
+}
+
+/* rank[sa[j]] = gs[j]; active[j] = j lies in a group of two or more */
+__global__ __launch_bounds__(256) void k_rank_init(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ sa,
+                                                   const uint32_t* __restrict__ gs, uint64_t n,
+                                                   uint32_t* __restrict__ rank, uint8_t* __restrict__ active)
+{
+  const uint64_t j = (uint64_t) blockIdx.x * 256 + threadIdx.x;
+  if (j >= n) return;
+  rank[sa[j]] = gs[j];
+  const bool head = j == 0 || keys[j] != keys[j - 1];
+  const bool last = j + 1 == n || keys[j + 1] != keys[j];
+  active[j] = (head && last) ? 0 : 1;
+}
+
+/* round h, step 1: the doubling key and suffix of every active position */
+__global__ __launch_bounds__(256) void k_dbl_keys(const uint32_t* __restrict__ act, uint64_t m,
+                                                  const uint32_t* __restrict__ sa, const uint32_t* __restrict__ rank,
+                                                  uint64_t n, uint64_t h, uint64_t* __restrict__ key2,
+                                                  uint32_t* __restrict__ suf)
+{
+  const uint64_t k = (uint64_t) blockIdx.x * 256 + threadIdx.x;
+  if (k >= m) return;
+  const uint32_t i = sa[act[k]];
+  key2[k] = dbl_key(rank, n, h, i);
+  suf[k] = i;
+}
+
+/* step 2: the current group of every suffix (primary key of the stable pass) */
+__global__ __launch_bounds__(256) void k_dbl_groups(const uint32_t* __restrict__ suf, uint64_t m,
+                                                    const uint32_t* __restrict__ rank, uint32_t* __restrict__ grp)
+{
+  const uint64_t k = (uint64_t) blockIdx.x * 256 + threadIdx.x;
+  if (k >= m) return;
+  grp[k] = rank[suf[k]];
+}
+
+/* step 3: write the re-sorted suffixes back into their groups' SA slots (the
+ * active positions are in SA order and every group is contiguous there), and
+ * mark where a new (group, key) run starts */
+__global__ __launch_bounds__(256) void k_dbl_apply(const uint32_t* __restrict__ act, uint64_t m,
+                                                   const uint32_t* __restrict__ suf, const uint32_t* __restrict__ grp,
+                                                   const uint32_t* __restrict__ rank, uint64_t n, uint64_t h,
+                                                   uint32_t* __restrict__ sa, uint32_t* __restrict__ hv,
+                                                   uint8_t* __restrict__ head)
+{
+  const uint64_t k = (uint64_t) blockIdx.x * 256 + threadIdx.x;
+  if (k >= m) return;
+  const uint32_t i = suf[k];
+  sa[act[k]] = i;
+  bool hd = k == 0 || grp[k] != grp[k - 1];
+  if (!hd) hd = dbl_key(rank, n, h, i) != dbl_key(rank, n, h, suf[k - 1]);
+  head[k] = hd ? 1 : 0;
+  hv[k] = hd ? act[k] : 0u;
+}
+
+/* step 4 (after the max-scan of hv into ngs): new ranks, and which positions
+ * stay active (runs of two or more) */
+__global__ __launch_bounds__(256) void k_dbl_rank(const uint32_t* __restrict__ suf, const uint32_t* __restrict__ ngs,
+                                                  const uint8_t* __restrict__ head, uint64_t m,
+                                                  uint32_t* __restrict__ rank, uint8_t* __restrict__ active)
+{
+  const uint64_t k = (uint64_t) blockIdx.x * 256 + threadIdx.x;
+  if (k >= m) return;
+  rank[suf[k]] = ngs[k];
+  const bool last = k + 1 == m || head[k + 1];
+  active[k] = (head[k] && last) ? 0 : 1;
 }
 
 __global__ __launch_bounds__(256) void k_dollar(const uint32_t* __restrict__ sa, uint64_t n, uint32_t k,
@@ -202,18 +292,111 @@ struct DevBuf {
   void release() { if (p) (void) hipFree(p); p = nullptr; }
 };
 
-/* '$'-aware full suffix comparison on the host text (the tie breaker). */
-struct SuffixLess {
-  const char* t;
-  uint64_t n;
-  bool operator()(uint32_t a, uint32_t b) const
+unsigned long long g_last_ties = 0;   /* diagnostics of the last build (kfmi_build_stats) */
+uint32_t g_last_tie_rounds = 0;
+
+/* Sorts every group of equal 32-base keys in `sa` (length n, sorted by the
+ * keys in `keys`) into true suffix order; see k_dbl_key. */
+int32_t resolve_ties(const uint64_t* keys, uint32_t* sa, uint64_t n, hipStream_t st, uint32_t* rounds)
+{
+  const dim3 gn((uint32_t) ((n + 255) / 256)), blk(256);
+  DevBuf rank, gs, hv0, act, flags, cnt;
+  BHIP(rank.alloc(4 * n));
+  BHIP(gs.alloc(4 * n));
+  BHIP(hv0.alloc(4 * n));
+  BHIP(act.alloc(4 * n));
+  BHIP(flags.alloc(n));
+  BHIP(cnt.alloc(8));
+  /* group starts, ranks, the active positions */
   {
-    const uint64_t la = n - a, lb = n - b, l = std::min(la, lb);
-    const int c = memcmp(t + a, t + b, l);
-    if (c) return c < 0;
-    return la < lb;   /* the shorter suffix hits '$' first */
+    hipLaunchKernelGGL(k_head_values, gn, blk, 0, st, keys, n, hv0.as<uint32_t>());
+    BHIP(hipGetLastError());
+    size_t tb = 0;
+    BHIP(rocprim::inclusive_scan(nullptr, tb, hv0.as<uint32_t>(), gs.as<uint32_t>(), (size_t) n,
+                                 rocprim::maximum<uint32_t>(), st));
+    DevBuf tmp;
+    BHIP(tmp.alloc(tb));
+    BHIP(rocprim::inclusive_scan(tmp.p, tb, hv0.as<uint32_t>(), gs.as<uint32_t>(), (size_t) n,
+                                 rocprim::maximum<uint32_t>(), st));
+    hipLaunchKernelGGL(k_rank_init, gn, blk, 0, st, keys, sa, gs.as<uint32_t>(), n, rank.as<uint32_t>(),
+                       flags.as<uint8_t>());
+    BHIP(hipGetLastError());
   }
-};
+  auto compact = [&](const uint32_t* in, bool counting, uint64_t len, uint32_t* outp, uint64_t* m) -> hipError_t {
+    size_t tb = 0;
+    rocprim::counting_iterator<uint32_t> ci(0);
+    hipError_t e = counting ? rocprim::select(nullptr, tb, ci, flags.as<uint8_t>(), outp,
+                                              cnt.as<unsigned long long>(), (size_t) len, st)
+                            : rocprim::select(nullptr, tb, in, flags.as<uint8_t>(), outp,
+                                              cnt.as<unsigned long long>(), (size_t) len, st);
+    if (e != hipSuccess) return e;
+    DevBuf tmp;
+    if ((e = tmp.alloc(tb)) != hipSuccess) return e;
+    e = counting ? rocprim::select(tmp.p, tb, ci, flags.as<uint8_t>(), outp, cnt.as<unsigned long long>(),
+                                   (size_t) len, st)
+                 : rocprim::select(tmp.p, tb, in, flags.as<uint8_t>(), outp, cnt.as<unsigned long long>(),
+                                   (size_t) len, st);
+    unsigned long long c = 0;
+    if (e == hipSuccess) e = hipMemcpyAsync(&c, cnt.p, 8, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    *m = c;
+    return e;
+  };
+  uint64_t m = 0;
+  BHIP(compact(nullptr, true, n, act.as<uint32_t>(), &m));
+  gs.release();
+  hv0.release();
+  uint32_t r = 0;
+  for (uint64_t h = 32; m > 0; h *= 2, ++r) {
+    if (h > 2 * n + 64) return KFMI_E_BUILDING_BWT;   /* cannot happen: all suffixes differ by then */
+    const dim3 gm((uint32_t) ((m + 255) / 256));
+    DevBuf k2a, k2b, sfa, sfb, ga, gb, hv, ngs, head, nact, tmp;
+    BHIP(k2a.alloc(8 * m)); BHIP(k2b.alloc(8 * m));
+    BHIP(sfa.alloc(4 * m)); BHIP(sfb.alloc(4 * m));
+    BHIP(ga.alloc(4 * m)); BHIP(gb.alloc(4 * m));
+    hipLaunchKernelGGL(k_dbl_keys, gm, blk, 0, st, act.as<uint32_t>(), m, sa, rank.as<uint32_t>(), n, h,
+                       k2a.as<uint64_t>(), sfa.as<uint32_t>());
+    BHIP(hipGetLastError());
+    /* LSD: by the doubling key, then stably by the group */
+    unsigned kbits = 1;
+    while (kbits < 64 && (n + h) >> kbits) ++kbits;
+    size_t tb = 0, tb2 = 0;
+    BHIP(rocprim::radix_sort_pairs(nullptr, tb, k2a.as<uint64_t>(), k2b.as<uint64_t>(), sfa.as<uint32_t>(),
+                                   sfb.as<uint32_t>(), (size_t) m, 0, kbits, st));
+    BHIP(rocprim::radix_sort_pairs(nullptr, tb2, ga.as<uint32_t>(), gb.as<uint32_t>(), sfb.as<uint32_t>(),
+                                   sfa.as<uint32_t>(), (size_t) m, 0, 32, st));
+    BHIP(tmp.alloc(tb > tb2 ? tb : tb2));
+    BHIP(rocprim::radix_sort_pairs(tmp.p, tb, k2a.as<uint64_t>(), k2b.as<uint64_t>(), sfa.as<uint32_t>(),
+                                   sfb.as<uint32_t>(), (size_t) m, 0, kbits, st));
+    k2a.release(); k2b.release();
+    hipLaunchKernelGGL(k_dbl_groups, gm, blk, 0, st, sfb.as<uint32_t>(), m, rank.as<uint32_t>(), ga.as<uint32_t>());
+    BHIP(hipGetLastError());
+    BHIP(rocprim::radix_sort_pairs(tmp.p, tb2, ga.as<uint32_t>(), gb.as<uint32_t>(), sfb.as<uint32_t>(),
+                                   sfa.as<uint32_t>(), (size_t) m, 0, 32, st));
+    tmp.release(); ga.release(); sfb.release();
+    BHIP(hv.alloc(4 * m)); BHIP(head.alloc(m));
+    hipLaunchKernelGGL(k_dbl_apply, gm, blk, 0, st, act.as<uint32_t>(), m, sfa.as<uint32_t>(), gb.as<uint32_t>(),
+                       rank.as<uint32_t>(), n, h, sa, hv.as<uint32_t>(), head.as<uint8_t>());
+    BHIP(hipGetLastError());
+    BHIP(ngs.alloc(4 * m));
+    BHIP(rocprim::inclusive_scan(nullptr, tb, hv.as<uint32_t>(), ngs.as<uint32_t>(), (size_t) m,
+                                 rocprim::maximum<uint32_t>(), st));
+    BHIP(tmp.alloc(tb));
+    BHIP(rocprim::inclusive_scan(tmp.p, tb, hv.as<uint32_t>(), ngs.as<uint32_t>(), (size_t) m,
+                                 rocprim::maximum<uint32_t>(), st));
+    hipLaunchKernelGGL(k_dbl_rank, gm, blk, 0, st, sfa.as<uint32_t>(), ngs.as<uint32_t>(), head.as<uint8_t>(), m,
+                       rank.as<uint32_t>(), flags.as<uint8_t>());
+    BHIP(hipGetLastError());
+    BHIP(nact.alloc(4 * m));
+    uint64_t m2 = 0;
+    BHIP(compact(act.as<uint32_t>(), false, m, nact.as<uint32_t>(), &m2));
+    BHIP(hipMemcpyAsync(act.p, nact.p, 4 * m2, hipMemcpyDeviceToDevice, st));
+    m = m2;
+  }
+  BHIP(hipStreamSynchronize(st));
+  *rounds = r;
+  return KFMI_SUCCESS;
+}
 
 int32_t build_gpu(const char* text, uint64_t n, uint32_t k, uint32_t d, uint32_t sa_rate, int dev, kfmi_fmi_t** out)
 {
@@ -271,36 +454,23 @@ int32_t build_gpu(const char* text, uint64_t n, uint32_t k, uint32_t d, uint32_t
     if (vb.current() != sa.as<uint32_t>())
       BHIP(hipMemcpyAsync(sa.p, vb.current(), n * 4, hipMemcpyDeviceToDevice, st));
 
-    /* 4. ties */
-    const uint32_t cap = 1u << 24;
-    DevBuf list, cntb;
-    BHIP(list.alloc((size_t) cap * 4));
+    /* 4. ties: equal 32-base keys (repeats, or suffixes ending within 32 bases
+     * of the end), resolved on the device by prefix doubling */
+    DevBuf cntb;
     BHIP(cntb.alloc(8));
     BHIP(hipMemsetAsync(cntb.p, 0, 8, st));
     if (n > 1)
       hipLaunchKernelGGL(k_ties, dim3((uint32_t) ((n - 1 + 255) / 256)), dim3(256), 0, st, kb.current(), n,
-                         list.as<uint32_t>(), cap, cntb.as<unsigned long long>());
+                         cntb.as<unsigned long long>());
     BHIP(hipGetLastError());
     unsigned long long nties = 0;
     BHIP(hipMemcpyAsync(&nties, cntb.p, 8, hipMemcpyDeviceToHost, st));
     BHIP(hipStreamSynchronize(st));
-    if (nties > cap) return KFMI_E_NOT_IMPLEMENTED;   /* too repetitive: caller uses the host builder */
+    g_last_ties = nties;
+    g_last_tie_rounds = 0;
     if (nties) {
-      std::vector<uint32_t> idx(nties);
-      BHIP(hipMemcpy(idx.data(), list.p, nties * 4, hipMemcpyDeviceToHost));
-      std::sort(idx.begin(), idx.end());
-      SuffixLess less{text, n};
-      size_t i = 0;
-      while (i < idx.size()) {
-        size_t j = i;
-        while (j + 1 < idx.size() && idx[j + 1] == idx[j] + 1) ++j;
-        const uint64_t lo = idx[i] - 1, hi = idx[j];   /* run of equal keys [lo, hi] */
-        std::vector<uint32_t> grp(hi - lo + 1);
-        BHIP(hipMemcpy(grp.data(), sa.as<uint32_t>() + lo, grp.size() * 4, hipMemcpyDeviceToHost));
-        std::sort(grp.begin(), grp.end(), less);
-        BHIP(hipMemcpy(sa.as<uint32_t>() + lo, grp.data(), grp.size() * 4, hipMemcpyHostToDevice));
-        i = j + 1;
-      }
+      int32_t e = resolve_ties(kb.current(), sa.as<uint32_t>(), n, st, &g_last_tie_rounds);
+      if (e) return e;
     }
   }
 
@@ -436,10 +606,18 @@ extern "C" int32_t kfmi_build_index_gpu_sa(const char* text, uint64_t n, uint32_
   if (kfmi_device_count() < 1) return KFMI_E_NO_DEVICE;
   int32_t e = build_gpu(text, n, k, d, sa_rate, kfmi_current_device(), (kfmi_fmi_t**) index);
   if (e == KFMI_E_NOT_IMPLEMENTED) {
-    fprintf(stderr, "kstepfmi build: text too repetitive for the GPU tie breaker, using the host builder\n");
+    fprintf(stderr, "kstepfmi build: text of %llu bases exceeds one dispatch per base (2^32 - 256), "
+                    "using the host builder\n", (unsigned long long) n);
     return kfmi_build_index_cpu_sa(text, n, k, d, sa_rate, index);
   }
   return e;
+}
+
+extern "C" int32_t kfmi_build_stats(uint64_t* ties, uint32_t* rounds)
+{
+  if (ties) *ties = g_last_ties;
+  if (rounds) *rounds = g_last_tie_rounds;
+  return KFMI_SUCCESS;
 }
 
 extern "C" int32_t kfmi_build_index_gpu(const char* text, uint64_t n, uint32_t k, uint32_t d,

@@ -8,10 +8,14 @@
  * the plain layout `q*size` (common.c:163-173 without -DINTERLEAVING_QUERIES).
  */
 #define _GNU_SOURCE
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
 #include <time.h>
+#include <unistd.h>
 #include "../kfmi_internal.h"
 
 /* common.c:28-33 (monotonic instead of CLOCK_REALTIME) */
@@ -116,15 +120,140 @@ int32_t freeReference(void **reference, void **index)
  * exactly `sizequery` characters (common.c:167-173 copies strlen-1 bytes per
  * line; a line of another length is an error here instead of silently
  * shifting every following read).  Reads beyond `numqueries` are ignored;
- * fewer reads than `numqueries` is an error. */
-int32_t loadQueries(const char *fn, uint32_t sizequery, uint32_t numqueries, void **queries)
+ * fewer reads than `numqueries` is an error.
+ *
+ * The reference reads line by line with fgets on one thread into 32-bit
+ * offsets (common.c:132-199, :163, :167).  Here a regular file is mapped and
+ * parsed by KFMI_HOST_THREADS threads (default min(16, cores)) in two passes
+ * over contiguous byte ranges: count the read lines of each range (and note the
+ * first malformed one), then -- after a prefix sum gives every range its first
+ * read number -- copy each read to q * size.  Same semantics as the
+ * line-by-line loop (load_queries_stream, kept for pipes and KFMI_LOAD_MMAP=0). */
+
+static int32_t load_queries_stream(FILE *fp, kfmi_qrys_t *q, uint64_t numqueries, uint32_t sizequery)
 {
-  kfmi_qrys_t *q;
-  FILE *fp;
   char *line = NULL;
   size_t cap = 0;
   ssize_t len;
   uint64_t i = 0;
+  while (i < numqueries && (len = getline(&line, &cap, fp)) > 0) {
+    if (line[0] == '>') continue;
+    while (len > 0 && (line[len - 1] == '\n' || line[len - 1] == '\r')) len--;
+    if ((uint64_t) len != sizequery) { free(line); return KFMI_E_READING_MFASTA_FILE; }
+    memcpy(q->h_queries + i * sizequery, line, sizequery);
+    i++;
+  }
+  free(line);
+  return i == numqueries ? KFMI_SUCCESS : KFMI_E_READING_MFASTA_FILE;
+}
+
+typedef struct {
+  const char *base;
+  uint64_t size, b, e;      /* lines whose first byte lies in [b, e) */
+  uint32_t m;
+  int pass;                 /* 1: count, 2: copy */
+  uint64_t nseq;            /* pass 1: read lines in the range */
+  uint64_t first_bad;       /* pass 1: range ordinal of the first malformed read line, or UINT64_MAX */
+  uint64_t first;           /* pass 2: global number of the range's first read */
+  uint64_t limit;           /* numqueries */
+  char *out;
+} lq_range;
+
+/* first line start at or after x */
+static uint64_t line_start(const char *base, uint64_t size, uint64_t x)
+{
+  const char *nl;
+  if (x == 0) return 0;
+  if (x >= size) return size;
+  nl = (const char *) memchr(base + x - 1, '\n', size - (x - 1));
+  return nl ? (uint64_t) (nl - base) + 1 : size;
+}
+
+static void *lq_worker(void *arg)
+{
+  lq_range *r = (lq_range *) arg;
+  const char *base = r->base;
+  uint64_t pos = line_start(base, r->size, r->b), end = line_start(base, r->size, r->e), k = 0;
+  r->nseq = 0;
+  if (r->pass == 1) r->first_bad = UINT64_MAX;
+  while (pos < end) {
+    const char *ls = base + pos;
+    const char *nl = (const char *) memchr(ls, '\n', r->size - pos);
+    uint64_t len = nl ? (uint64_t) (nl - ls) : r->size - pos;
+    const uint64_t next = pos + len + (nl ? 1 : 0);
+    if (ls[0] != '>') {
+      while (len > 0 && ls[len - 1] == '\r') len--;
+      if (r->pass == 1) {
+        if (len != r->m && r->first_bad == UINT64_MAX) r->first_bad = k;
+      } else {
+        const uint64_t g = r->first + k;
+        if (g >= r->limit) break;
+        memcpy(r->out + g * r->m, ls, r->m);
+      }
+      k++;
+    }
+    pos = next;
+  }
+  r->nseq = k;
+  return NULL;
+}
+
+static int host_threads(void)
+{
+  const char *e = getenv("KFMI_HOST_THREADS");
+  long n = sysconf(_SC_NPROCESSORS_ONLN);
+  int v = e ? atoi(e) : (int) (n > 16 ? 16 : (n < 1 ? 1 : n));
+  return v < 1 ? 1 : (v > 64 ? 64 : v);
+}
+
+static int32_t load_queries_mapped(const char *base, uint64_t size, kfmi_qrys_t *q, uint64_t numqueries,
+                                   uint32_t sizequery)
+{
+  int nt = host_threads(), t;
+  lq_range r[64];
+  pthread_t th[64];
+  uint64_t acc = 0;
+  if (size < (4u << 20)) nt = 1;
+  for (t = 0; t < nt; t++) {
+    r[t].base = base;
+    r[t].size = size;
+    r[t].b = size * (uint64_t) t / (uint64_t) nt;
+    r[t].e = size * (uint64_t) (t + 1) / (uint64_t) nt;
+    r[t].m = sizequery;
+    r[t].limit = numqueries;
+    r[t].out = q->h_queries;
+  }
+  for (int pass = 1; pass <= 2; pass++) {
+    for (t = 0; t < nt; t++) r[t].pass = pass;
+    for (t = 1; t < nt; t++)
+      if (pthread_create(&th[t], NULL, lq_worker, &r[t])) {
+        for (int u = 1; u < t; u++) pthread_join(th[u], NULL);
+        return KFMI_E_ALLOCATING_MFASTA;
+      }
+    lq_worker(&r[0]);
+    for (t = 1; t < nt; t++) pthread_join(th[t], NULL);
+    if (pass == 1) {
+      /* a malformed read line before the numqueries-th read is what the line
+       * loop would stop at; too few reads is an error as well */
+      for (t = 0; t < nt; t++) {
+        if (r[t].first_bad != UINT64_MAX && acc + r[t].first_bad < numqueries) return KFMI_E_READING_MFASTA_FILE;
+        r[t].first = acc;
+        acc += r[t].nseq;
+      }
+      if (acc < numqueries) return KFMI_E_READING_MFASTA_FILE;
+    }
+  }
+  return KFMI_SUCCESS;
+}
+
+int32_t loadQueries(const char *fn, uint32_t sizequery, uint32_t numqueries, void **queries)
+{
+  kfmi_qrys_t *q;
+  FILE *fp;
+  struct stat sb;
+  const char *mm = getenv("KFMI_LOAD_MMAP");
+  int32_t err = KFMI_E_READING_MFASTA_FILE;
+  int done = 0;
   if (sizequery == 0) return KFMI_E_BAD_ARGUMENT;
   fp = fopen(fn, "rb");
   if (!fp) return KFMI_E_OPENING_MFASTA_FILE;
@@ -134,19 +263,18 @@ int32_t loadQueries(const char *fn, uint32_t sizequery, uint32_t numqueries, voi
   q->size = sizequery;
   q->h_queries = (char *) malloc((size_t) numqueries * sizequery + 1);
   if (!q->h_queries) { free(q); fclose(fp); return KFMI_E_ALLOCATING_MFASTA; }
-  while (i < numqueries && (len = getline(&line, &cap, fp)) > 0) {
-    if (line[0] == '>') continue;
-    while (len > 0 && (line[len - 1] == '\n' || line[len - 1] == '\r')) len--;
-    if ((uint64_t) len != sizequery) {
-      free(line); free(q->h_queries); free(q); fclose(fp);
-      return KFMI_E_READING_MFASTA_FILE;
+  if ((!mm || atoi(mm)) && fstat(fileno(fp), &sb) == 0 && S_ISREG(sb.st_mode) && sb.st_size > 0) {
+    void *base = mmap(NULL, (size_t) sb.st_size, PROT_READ, MAP_PRIVATE, fileno(fp), 0);
+    if (base != MAP_FAILED) {
+      (void) madvise(base, (size_t) sb.st_size, MADV_WILLNEED);
+      err = load_queries_mapped((const char *) base, (uint64_t) sb.st_size, q, numqueries, sizequery);
+      munmap(base, (size_t) sb.st_size);
+      done = 1;
     }
-    memcpy(q->h_queries + i * sizequery, line, sizequery);
-    i++;
   }
-  free(line);
+  if (!done) err = load_queries_stream(fp, q, numqueries, sizequery);
   fclose(fp);
-  if (i != numqueries) { free(q->h_queries); free(q); return KFMI_E_READING_MFASTA_FILE; }
+  if (err) { free(q->h_queries); free(q); return err; }
   *queries = q;
   return KFMI_SUCCESS;
 }

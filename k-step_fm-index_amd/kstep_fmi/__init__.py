@@ -93,6 +93,7 @@ def load() -> ctypes.CDLL:
         "kfmi_results_num": (u64, [vp]),
         "kfmi_build_index_cpu": (i32, [vp, u64, u32, u32, pvp]),
         "kfmi_build_index_gpu": (i32, [vp, u64, u32, u32, i32, pvp]),
+        "kfmi_build_stats": (i32, [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32)]),
         "kfmi_count_blocks": (i32, [vp, vp, ctypes.POINTER(ctypes.c_uint64)]),
         "kfmi_device_index_bytes": (u64, [vp]),
         "kfmi_search_stream": (i32, [vp, vp, u64, u32, vp, u64]),
@@ -161,6 +162,13 @@ def get_devices() -> list:
     arr = (ctypes.c_int32 * 16)()
     n = load().kfmi_get_devices(arr, 16)
     return [arr[i] for i in range(n)]
+
+
+def build_stats() -> dict:
+    """Tie diagnostics of the last GPU index build (kfmi_build_stats)."""
+    t, r = ctypes.c_uint64(), ctypes.c_uint32()
+    _check(load().kfmi_build_stats(ctypes.byref(t), ctypes.byref(r)), "build_stats")
+    return {"ties": int(t.value), "rounds": int(r.value)}
 
 
 def device_count() -> int:

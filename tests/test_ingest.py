@@ -1,0 +1,94 @@
+"""Query ingest: the multi-threaded mapped loadQueries against
+the line-by-line loop it replaces (reference common/common.c:132-199
+semantics, kept as the KFMI_LOAD_MMAP=0 path) on the golden query files, a
+1M-read file and the malformed-input cases."""
+import os
+
+import numpy as np
+import pytest
+
+import util
+
+
+def load(K, path, m, n):
+    q = K.Queries.load(path, m, n)
+    L = K.load()
+    import ctypes
+
+    class Q(ctypes.Structure):
+        _fields_ = [("num", ctypes.c_uint64), ("size", ctypes.c_uint32), ("h", ctypes.c_void_p)]
+    qs = Q.from_address(q.ptr.value)
+    out = np.ctypeslib.as_array((ctypes.c_uint8 * (qs.num * qs.size)).from_address(qs.h)).reshape(qs.num, qs.size)
+    out = out.copy()
+    q.close()
+    del L
+    return out
+
+
+def both(K, path, m, n, monkeypatch):
+    """(mapped parallel result or error code, line-loop result or error code)"""
+    res = []
+    for mm in ("1", "0"):
+        monkeypatch.setenv("KFMI_LOAD_MMAP", mm)
+        try:
+            res.append(load(K, path, m, n))
+        except K.KfmiError as e:
+            res.append(e.code)
+    monkeypatch.delenv("KFMI_LOAD_MMAP")
+    return res
+
+
+def test_golden_query_files_equal(kfmi_mod, monkeypatch):
+    seen = 0
+    for case, c in sorted(util.manifest().items()):
+        for m, qd in sorted(c["queries"].items()):
+            m = int(m)
+            path = util.GOLDEN / case / qd["file"]
+            a, b = both(kfmi_mod, path, m, qd["num"], monkeypatch)
+            assert isinstance(a, np.ndarray) and np.array_equal(a, b), (case, m)
+            assert np.array_equal(a, util.read_qry(path, m))
+            seen += 1
+    assert seen
+
+
+@pytest.mark.parametrize("threads", ["1", "3", "8"])
+def test_million_reads_file(kfmi_mod, tmp_path, monkeypatch, threads):
+    """1M x 100 bp reads with ragged headers and CRLF lines, parsed over several
+    byte ranges (a range boundary falls inside headers and reads)."""
+    rng = np.random.default_rng(int(threads))
+    n, m = 1_000_000, 100
+    reads = rng.choice(np.frombuffer(b"ACGTNacgt", np.uint8), size=(n, m))
+    path = tmp_path / "q.fa"
+    with open(path, "wb") as f:
+        for i in range(0, n, 100_000):
+            blk = reads[i:i + 100_000]
+            f.write(b"".join(b">r%d%s\n%s%s\n" % (i + j, b" x" * (j % 7), blk[j].tobytes(), b"\r" * (j % 3 == 0))
+                             for j in range(blk.shape[0])))
+    monkeypatch.setenv("KFMI_HOST_THREADS", threads)
+    a, b = both(kfmi_mod, path, m, n, monkeypatch)
+    assert np.array_equal(a, reads) and np.array_equal(b, reads)
+    # the first 777 reads only: everything after them is ignored
+    a, b = both(kfmi_mod, path, m, 777, monkeypatch)
+    assert np.array_equal(a, reads[:777]) and np.array_equal(b, reads[:777])
+
+
+@pytest.mark.parametrize("body,n,ok", [
+    (b">a\nACGT\n>b\nTTTT\n", 2, True),
+    (b">a\nACGT\n>b\nTTTT", 2, True),                 # no final newline
+    (b"ACGT\nTTTT\nGGGG\n", 3, True),                  # no headers at all
+    (b">a\nACGT\n>b\nTTTT\n", 3, False),              # too few reads
+    (b">a\nACGT\n>b\nTTT\n", 2, False),               # short read before the limit
+    (b">a\nACGT\n>b\nTTTT\n>c\nTT\n", 2, True),        # malformed read after the limit: ignored
+    (b">a\nACGT\n\n>b\nTTTT\n", 2, False),             # empty line counts as a (bad) read
+    (b">a\r\nACGT\r\n>b\r\nTTTT\r\n", 2, True),        # CRLF
+    (b">\n>\nACGT\n", 1, True),                        # bare headers
+])
+def test_edge_cases_equal(kfmi_mod, tmp_path, monkeypatch, body, n, ok):
+    for pad in (0, 5_000_000):       # small files parse on one thread, large ones in ranges
+        path = tmp_path / "e.fa"
+        path.write_bytes(b">pad\n" * (pad // 5) + body if pad else body)
+        a, b = both(kfmi_mod, path, 4, n, monkeypatch)
+        if ok:
+            assert isinstance(a, np.ndarray) and np.array_equal(a, b), (body, pad)
+        else:
+            assert a == b == 12, (body, pad, a, b)     # KFMI_E_READING_MFASTA_FILE
