@@ -53,6 +53,11 @@ struct kfmi_dev_queries {
   int device = -1;
   uint8_t* ascii = nullptr;    /* num*size bytes, plain layout */
   uint32_t* packed = nullptr;  /* nwords x num u32 codes */
+  /* in-call reorder (KFMI_REORDER=1): keys/reads double buffers, row-major
+   * code words, rocPRIM temporary storage; allocated on first use */
+  uint32_t* ro_buf = nullptr;
+  void* ro_tmp = nullptr;
+  size_t ro_tmp_bytes = 0;
   uint64_t num = 0;
   uint32_t size = 0, K = 0, steps = 0, nwords = 0;
 };

@@ -26,6 +26,7 @@
 #include "kfmi_coop.h"
 #include "kfmi_locate.h"
 #include "kfmi_runtime.h"
+#include <rocprim/device/device_radix_sort.hpp>
 
 namespace kfmi {
 
@@ -860,6 +861,8 @@ void free_dev_queries(kfmi_dev_queries* dq)
   if (dq->device >= 0) (void) hipSetDevice(dq->device);
   if (dq->ascii) (void) hipFree(dq->ascii);
   if (dq->packed) (void) hipFree(dq->packed);
+  if (dq->ro_buf) (void) hipFree(dq->ro_buf);
+  if (dq->ro_tmp) (void) hipFree(dq->ro_tmp);
   delete dq;
 }
 
@@ -956,8 +959,51 @@ extern "C" int32_t transferCPUtoGPU(void* index, void* queries, void* results)
   return KFMI_SUCCESS;
 }
 
+/* KFMI_REORDER=1: search a task backend's batch in suffix order (DESIGN.md
+ * 5c).  Needs fused packing with 8 code words (m <= 128), no ftab, < 2^32 reads. */
+static bool reorder_wanted(const kfmi_dev_index* di, const kfmi_dev_queries* dq, int maxw, bool ftab)
+{
+  const char* e = getenv("KFMI_REORDER");
+  return e && atoi(e) && !is_coop(di->backend) && maxw == 8 && !ftab && dq->num > 0 &&
+         dq->num < 0xFFFFFFFFull;
+}
+
+/* keys, reads (2 buffers each of num u32) and 8 code words per read */
+static int32_t reorder_queue(kfmi_dev_queries* dq, hipStream_t st, const uint32_t** perm, const uint32_t** pk)
+{
+  const uint64_t n = dq->num;
+  if (!dq->ro_buf) {
+    if (hipMalloc((void**) &dq->ro_buf, 4ull * n * (4 + 8)) != hipSuccess) {
+      dq->ro_buf = nullptr;
+      return KFMI_E_DEVICE_ALLOC;
+    }
+    size_t tb = 0;
+    uint32_t* b = dq->ro_buf;
+    if (rocprim::radix_sort_pairs(nullptr, tb, b, b + n, b + 2 * n, b + 3 * n, (size_t) n, 0, 32, st) != hipSuccess ||
+        hipMalloc(&dq->ro_tmp, tb ? tb : 1) != hipSuccess)
+      return KFMI_E_DEVICE_ALLOC;
+    dq->ro_tmp_bytes = tb;
+  }
+  uint32_t* keys = dq->ro_buf;
+  uint32_t* keys2 = keys + n;
+  uint32_t* vals = keys + 2 * n;
+  uint32_t* vals2 = keys + 3 * n;
+  uint32_t* words = keys + 4 * n;
+  const size_t lds = 4 * (size_t) stage_slot_bytes(dq->size);
+  hipLaunchKernelGGL(reorder_keys_kernel<8>, dim3((uint32_t) ((n + 255) / 256)), dim3(256), lds, st, dq->ascii,
+                     dq->size, n, keys, vals, words);
+  HIP_OK(hipGetLastError());
+  const unsigned bits = dq->size >= 16 ? 32u : 2u * dq->size;
+  size_t tb = dq->ro_tmp_bytes;
+  HIP_OK(rocprim::radix_sort_pairs(dq->ro_tmp, tb, keys, keys2, vals, vals2, (size_t) n, 0, bits, st));
+  *perm = vals2;
+  *pk = words;
+  return KFMI_SUCCESS;
+}
+
 /* Queues pack (if not fused) + LF of one device batch on `st`, bracketed by
- * ev[0..2]; search_finish waits and reads the timings. */
+ * ev[0..2]; search_finish waits and reads the timings.  With the reorder,
+ * the key/sort launches sit between ev[0] and ev[1] (reported as pack). */
 int32_t search_enqueue(kfmi_dev_index* di, kfmi_dev_queries* dq, uint32_t* d_res, hipStream_t st,
                               hipEvent_t* ev, uint32_t ftab)
 {
@@ -975,11 +1021,16 @@ int32_t search_enqueue(kfmi_dev_index* di, kfmi_dev_queries* dq, uint32_t* d_res
   a.steps = dq->steps;
   a.nwords = dq->nwords;
   a.res = d_res;
+  const bool reorder = reorder_wanted(di, dq, a.maxw, a.ix.ftab != nullptr);
   HIP_OK(hipEventRecord(ev[0], st));
   if (!a.maxw) HIP_OK(launch_pack(dq, st));
+  if (reorder) {
+    err = reorder_queue(dq, st, &a.perm, &a.pk);
+    if (err) return err;
+  }
   HIP_OK(hipEventRecord(ev[1], st));
   if (dq->num) {
-    const Op op = is_coop(di->backend) ? Op::Coop : Op::Task;
+    const Op op = reorder ? Op::TaskSorted : (is_coop(di->backend) ? Op::Coop : Op::Task);
     HIP_OK(dispatch(op, di->K, di->nb, di->layout, a));
   }
   HIP_OK(hipEventRecord(ev[2], st));
