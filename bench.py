@@ -558,13 +558,15 @@ def main():
                     lt = K.last_timing()
                     e2e[kind] = {"mqps": round(reads.shape[0] / w / 1e6, 2), "ms": round(w * 1e3, 3),
                                  "host_ms": round(lt["pack_ms"], 3), "wait_ms": round(lt["lf_ms"], 3),
+                                 "hostpacked_fraction": round(K.load().kfmi_stream_hostpacked_fraction(), 3),
                                  "results_equal": bool(np.array_equal(out, res))}
-                host_pack = os.environ.get("KFMI_STREAM_HOSTPACK", "1") != "0"
-                e2e["chunk_queries"] = int(os.environ.get("KFMI_STREAM_CHUNK", (1 << 19) if host_pack else (1 << 16)))
-                e2e["host_pack"] = host_pack
+                hp_mode = os.environ.get("KFMI_STREAM_HOSTPACK", "2")
+                e2e["chunk_queries"] = int(os.environ.get("KFMI_STREAM_CHUNK", (1 << 16) if hp_mode == "0" else (1 << 19)))
+                e2e["host_pack"] = {"0": "never", "1": "always", "3": "alternate"}.get(hp_mode, "adaptive")
                 e2e["what"] = "kfmi_search_stream: ASCII reads in host memory -> results in host memory; " \
-                              "host 2-bit packing (qpack.c, KFMI_HOST_THREADS) / code-word H2D / LF / D2H " \
-                              "of successive chunks overlapped on 3 HIP streams"
+                              "per chunk host 2-bit packing (qpack.c, KFMI_HOST_THREADS) + code-word H2D, or " \
+                              "ASCII H2D + device packing, chosen from measured rates; LF / D2H of successive " \
+                              "chunks overlapped on 3 HIP streams"
                 extra["end_to_end"] = e2e
                 log(f"end to end {e2e}")
                 del pin, pout

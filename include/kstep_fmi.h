@@ -200,12 +200,14 @@ int32_t kfmi_count_blocks(void *index, void *queries, uint64_t *blocks);
  * ASCII bytes at `ascii`, results [L0,R0,L1,R1,...] into `results` (2*num
  * u32).  The index must already be on the device (transferCPUtoGPU(index,
  * NULL, NULL)).  Chunks of `chunk` queries (0: KFMI_STREAM_CHUNK, else 2^19,
- * or 2^16 without host packing) rotate over 3 HIP streams so that host
- * packing, H2D, LF and result D2H of successive chunks overlap.  By default
- * the host packs each chunk to code words (kfmi_pack_queries) and PCIe
- * carries 4 bytes per 16 bases; KFMI_STREAM_HOSTPACK=0 sends ASCII (pinned:
- * DMA'd directly; pageable: staged through pinned buffers) and packs on the
- * device.  Host work runs on KFMI_HOST_THREADS threads (default min(16,
+ * or 2^16 when every chunk goes as ASCII) rotate over 3 HIP streams so that
+ * host packing, H2D, LF and result D2H of successive chunks overlap.  Each
+ * chunk either is packed by the host to code words (kfmi_pack_queries; PCIe
+ * carries 4 bytes per 16 bases) or goes as ASCII (pinned: DMA'd directly;
+ * pageable: staged through pinned buffers) and is packed on the device.  By
+ * default the choice is made per chunk from the measured host-packing and
+ * link rates (whichever finishes first); KFMI_STREAM_HOSTPACK=1 packs every
+ * chunk on the host, =0 sends every chunk as ASCII.  Host work runs on KFMI_HOST_THREADS threads (default min(16,
  * cores)).  Blocking; kfmi_last_timing: total = wall time of the call, pack =
  * host packing / staging time, lf = time blocked on chunks in flight.
  * Results equal kfmi_search's. */
@@ -223,6 +225,9 @@ int32_t kfmi_host_alloc(uint64_t bytes, void **p);
 int32_t kfmi_host_free(void *p);
 /* Frees the staging and device buffers kfmi_search_stream keeps per device. */
 int32_t kfmi_stream_release(void);
+/* Share of the reads of this thread's last kfmi_search_stream that were packed
+ * on the host (the rest went over PCIe as ASCII). */
+double  kfmi_stream_hostpacked_fraction(void);
 
 /* Bytes of the device-resident index for the current backend (incl. SA samples). */
 uint64_t kfmi_device_index_bytes(void *index);

@@ -30,6 +30,8 @@ constexpr int NSLOT = 3;
 struct StreamSlot {
   hipStream_t st = nullptr;
   hipEvent_t done = nullptr;
+  hipEvent_t x0 = nullptr, x1 = nullptr;   /* bracket the chunk's H2D (link time of its mode) */
+  bool packed_mode = false;                /* this chunk's reads went over PCIe as host-packed words */
   kfmi_dev_queries dq;         /* device ascii + packed of one chunk */
   uint32_t* d_res = nullptr;
   uint8_t* h_in = nullptr;     /* pinned staging */
@@ -45,6 +47,7 @@ struct StreamPool {
   StreamSlot slot[NSLOT];
 };
 static StreamPool g_pool[64];
+static thread_local double t_stream_packed_frac = 0;   /* share of the last streamed batch packed on the host */
 /* one streamed search per device at a time; searches on different devices (one
  * host thread each) and every other entry point run concurrently with it */
 static std::mutex g_pool_mu[64];
@@ -63,6 +66,8 @@ static void pool_free(int dev)
     if (s.h_out) (void) hipHostFree(s.h_out);
     if (s.h_pk) (void) hipHostFree(s.h_pk);
     if (s.done) (void) hipEventDestroy(s.done);
+    if (s.x0) (void) hipEventDestroy(s.x0);
+    if (s.x1) (void) hipEventDestroy(s.x1);
     if (s.st) (void) hipStreamDestroy(s.st);
     s = StreamSlot();
   }
@@ -75,7 +80,8 @@ static int32_t slot_reserve(StreamSlot& s, uint64_t cq, uint32_t size, uint32_t 
 {
   if (!s.st) {
     if (hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess)
+        hipEventCreateWithFlags(&s.done, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreate(&s.x0) != hipSuccess || hipEventCreate(&s.x1) != hipSuccess)
       return KFMI_E_NO_DEVICE;
   }
   const uint64_t in = cq * size + 16;
@@ -240,6 +246,8 @@ static void par_pack(const char* src, uint64_t n, uint32_t size, uint32_t* out)
   });
 }
 
+extern "C" double kfmi_stream_hostpacked_fraction(void) { return t_stream_packed_frac; }
+
 extern "C" int32_t kfmi_host_alloc(uint64_t bytes, void** p)
 {
   if (!p) return KFMI_E_BAD_ARGUMENT;
@@ -279,9 +287,16 @@ extern "C" int32_t kfmi_search_stream(void* index, const char* ascii, uint64_t n
   int32_t err = ctx_for(di->device, &ctx);
   if (err) return err;
   if (num == 0) return KFMI_SUCCESS;
+  /* KFMI_STREAM_HOSTPACK: 1 = every chunk packed on the host, 0 = every chunk
+   * sent as ASCII (packed on the device), 3 = alternate (testing), unset / 2 =
+   * adaptive: per chunk, whichever mode a two-resource model (host thread
+   * pool, PCIe link) says finishes first, with per-read costs measured on the
+   * previous chunks -- on a box whose host packs slower than the link carries
+   * ASCII, part of the batch goes as ASCII while the host packs the rest. */
   const char* hp = getenv("KFMI_STREAM_HOSTPACK");
-  const bool host_pack = !hp || atoi(hp) != 0;
-  const uint64_t def_chunk = host_pack ? (1ull << 19) : (1ull << 16);   /* profiles/r01/e2e_sweep*.jsonl */
+  const int mode = hp ? atoi(hp) : 2;
+  const bool any_pack = mode != 0, any_ascii = mode != 1;
+  const uint64_t def_chunk = any_pack ? (1ull << 19) : (1ull << 16);   /* profiles/r01/e2e_sweep*.jsonl */
   if (chunk == 0) {
     const char* e = getenv("KFMI_STREAM_CHUNK");
     chunk = e ? strtoull(e, nullptr, 10) : def_chunk;
@@ -295,10 +310,19 @@ extern "C" int32_t kfmi_search_stream(void* index, const char* ascii, uint64_t n
   StreamPool& pool = g_pool[di->device];
   pool.init = true;
   for (StreamSlot& s : pool.slot) {
-    err = slot_reserve(s, chunk, size, nwords, !pin_in && !host_pack, !pin_out, host_pack);
+    err = slot_reserve(s, chunk, size, nwords, !pin_in && any_ascii, !pin_out, any_pack);
     if (err) return err;
     s.busy = false;
   }
+  /* cost model (ms per read), seeded with nominal rates and refined by EMAs */
+  const double nthr = (double) HostPool::get().size();
+  double c_pack = size / (3.0e6 * nthr);              /* host packing */
+  double c_stage = pin_in ? 0.0 : size / (8.0e6 * nthr);   /* host staging copy of ASCII */
+  double c_xa = size / 50.0e6;                        /* ASCII over PCIe (~50 GB/s) */
+  double c_xp = 4.0 * nwords / 50.0e6;                /* packed words over PCIe */
+  double t_host = 0, t_link = 0;                      /* model clocks */
+  uint64_t npacked = 0;
+  auto ema = [](double& v, double x) { v = 0.6 * v + 0.4 * x; };
   const auto t0 = std::chrono::steady_clock::now();
   const Op op = is_coop(di->backend) ? Op::Coop : Op::Task;
   IdxArgs ix = idx_args(di);
@@ -314,7 +338,11 @@ extern "C" int32_t kfmi_search_stream(void* index, const char* ascii, uint64_t n
     const bool ok = hipEventSynchronize(s.done) == hipSuccess;
     wait_ms += since(tw);
     if (!ok) status = KFMI_E_KERNEL;
-    else if (!pin_out) par_copy(results + 2 * s.q0, s.h_out, 8ull * s.n);
+    else {
+      if (!pin_out) par_copy(results + 2 * s.q0, s.h_out, 8ull * s.n);
+      float x = 0;
+      if (hipEventElapsedTime(&x, s.x0, s.x1) == hipSuccess && s.n) ema(s.packed_mode ? c_xp : c_xa, x / s.n);
+    }
     s.busy = false;
   };
   const uint64_t nchunks = (num + chunk - 1) / chunk;
@@ -327,13 +355,28 @@ extern "C" int32_t kfmi_search_stream(void* index, const char* ascii, uint64_t n
     const char* src = ascii + s.q0 * size;
     const uint64_t bytes = s.n * size;
     const void* hsrc = src;
+    bool host_pack;
+    if (mode == 0 || mode == 1) host_pack = mode == 1;
+    else if (mode == 3) host_pack = (i & 1) == 0;
+    else {
+      const double dn = (double) s.n;
+      const double done_p = std::max(t_host + c_pack * dn, t_link) + c_xp * dn;
+      const double done_a = std::max(t_host + c_stage * dn, t_link) + c_xa * dn;
+      host_pack = done_p <= done_a;
+      t_host += (host_pack ? c_pack : c_stage) * dn;
+      t_link = host_pack ? done_p : done_a;
+    }
+    s.packed_mode = host_pack;
+    npacked += host_pack ? s.n : 0;
     const auto th = clk::now();
     if (host_pack) par_pack(src, s.n, size, s.h_pk);
     else if (!pin_in) {
       par_copy(s.h_in, src, bytes);
       hsrc = s.h_in;
     }
-    host_ms += since(th);
+    const double hms = since(th);
+    host_ms += hms;
+    if (s.n && (host_pack || !pin_in)) ema(host_pack ? c_pack : c_stage, hms / s.n);
     s.dq.device = di->device;
     s.dq.num = s.n;
     s.dq.size = size;
@@ -352,11 +395,12 @@ extern "C" int32_t kfmi_search_stream(void* index, const char* ascii, uint64_t n
     a.nwords = nwords;
     a.res = s.d_res;
     void* hdst = pin_out ? (void*) (results + 2 * s.q0) : (void*) s.h_out;
-    const bool up_ok = host_pack
-                           ? hipMemcpyAsync(s.dq.packed, s.h_pk, 4ull * nwords * s.n, hipMemcpyHostToDevice, s.st) ==
-                                 hipSuccess
-                           : (hipMemcpyAsync(s.dq.ascii, hsrc, bytes, hipMemcpyHostToDevice, s.st) == hipSuccess &&
-                              (a.maxw || launch_pack(&s.dq, s.st) == hipSuccess));
+    const bool up_ok = hipEventRecord(s.x0, s.st) == hipSuccess &&
+                       (host_pack ? hipMemcpyAsync(s.dq.packed, s.h_pk, 4ull * nwords * s.n, hipMemcpyHostToDevice,
+                                                   s.st) == hipSuccess
+                                  : hipMemcpyAsync(s.dq.ascii, hsrc, bytes, hipMemcpyHostToDevice, s.st) == hipSuccess) &&
+                       hipEventRecord(s.x1, s.st) == hipSuccess &&
+                       (host_pack || a.maxw || launch_pack(&s.dq, s.st) == hipSuccess);
     if (!up_ok || dispatch(op, K, di->nb, di->layout, a) != hipSuccess ||
         hipMemcpyAsync(hdst, s.d_res, 8ull * s.n, hipMemcpyDeviceToHost, s.st) != hipSuccess ||
         hipEventRecord(s.done, s.st) != hipSuccess) {
@@ -370,6 +414,7 @@ extern "C" int32_t kfmi_search_stream(void* index, const char* ascii, uint64_t n
   t_ms[0] = ms;
   t_ms[1] = host_ms;   /* host packing or staging copies */
   t_ms[2] = wait_ms;   /* blocked on chunks in flight */
+  t_stream_packed_frac = num ? (double) npacked / (double) num : 0.0;
   return status;
 }
 

@@ -17,6 +17,7 @@
  */
 #define _GNU_SOURCE
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 #include <immintrin.h>
 #include "../kfmi_internal.h"
@@ -72,11 +73,71 @@ __attribute__((target("avx2"))) static void pack_rows_avx2(const uint8_t* a, uin
   }
 }
 
+/* 64 bases per block (AVX-512 BW + VBMI + VL, e.g. Zen 4/5 hosts), every
+ * block branch-free: block k holds reversed bases 64k .. 64k+63.  A full block
+ * is one unaligned load + one vpermb (reverse); the last, partial block of
+ * cnt = m mod 64 bases is a masked load of the row's first cnt bytes (masked
+ * bytes never fault, so the last row of a buffer is safe) + a zero-masking
+ * vpermb.  Codes, 4 per byte (maddubs, madd), vpmovdb -> 16 bytes = 4 words;
+ * zero bytes code as 0, the padding the words need past 2m bits. */
+__attribute__((target("avx512f,avx512bw,avx512vbmi,avx512vl"))) static void pack_rows_avx512(const uint8_t* a,
+                                                                                            uint64_t n, uint32_t m,
+                                                                                            uint32_t* out,
+                                                                                            uint64_t ostride)
+{
+  uint8_t ridx[64], tidx[64];
+  const uint32_t full = m / 64, cnt = m % 64;
+  for (int j = 0; j < 64; ++j) {
+    ridx[j] = (uint8_t) (63 - j);
+    tidx[j] = (uint8_t) (j < (int) cnt ? cnt - 1 - j : 0);
+  }
+  const __m512i rev = _mm512_loadu_si512((const void*) ridx), trev = _mm512_loadu_si512((const void*) tidx);
+  const __mmask64 tmask = cnt ? (~0ull >> (64 - cnt)) : 0;
+  const __m512i m3 = _mm512_set1_epi8(3), m1 = _mm512_set1_epi8(1);
+  const __m512i w14 = _mm512_set1_epi16(0x0401), w116 = _mm512_set1_epi32(0x00100001);
+  const uint32_t tw = (cnt + 15) / 16;   /* words of the partial block */
+  for (uint64_t q = 0; q < n; ++q) {
+    const uint8_t* row = a + q * m;
+    uint32_t* o = out + q;
+    for (uint32_t k = 0; k <= full; ++k) {
+      __m512i v;
+      if (k < full) v = _mm512_permutexvar_epi8(rev, _mm512_loadu_si512((const void*) (row + m - 64 * (k + 1))));
+      else if (cnt) v = _mm512_maskz_permutexvar_epi8(tmask, trev, _mm512_maskz_loadu_epi8(tmask, row));
+      else break;
+      const __m512i c = _mm512_xor_si512(_mm512_and_si512(_mm512_srli_epi16(v, 1), m3),
+                                         _mm512_and_si512(_mm512_srli_epi16(v, 2), m1));
+      const __m512i p = _mm512_madd_epi16(_mm512_maddubs_epi16(c, w14), w116);   /* 8 bits per dword */
+      const __m128i b = _mm512_cvtepi32_epi8(p);                                 /* 16 bytes = 4 words */
+      uint32_t* ow = o + (uint64_t) (4 * k) * ostride;
+      const uint32_t nw = k < full ? 4 : tw;
+      ow[0] = (uint32_t) _mm_extract_epi32(b, 0);
+      if (nw > 1) ow[ostride] = (uint32_t) _mm_extract_epi32(b, 1);
+      if (nw > 2) ow[2 * ostride] = (uint32_t) _mm_extract_epi32(b, 2);
+      if (nw > 3) ow[3 * ostride] = (uint32_t) _mm_extract_epi32(b, 3);
+    }
+  }
+}
+
+/* KFMI_QPACK_ISA=scalar|avx2|avx512 pins the path (tests); default: the widest the host has */
 void kfmi_pack_rows(const uint8_t* ascii, uint64_t n, uint32_t m, uint32_t* out, uint64_t ostride)
 {
-  static int avx2 = -1;
-  if (avx2 < 0) avx2 = __builtin_cpu_supports("avx2") ? 1 : 0;
-  if (avx2) pack_rows_avx2(ascii, n, m, out, ostride);
+  static int isa = -1;   /* 0 scalar, 1 avx2, 2 avx512 */
+  const char* e = getenv("KFMI_QPACK_ISA");
+  int use;
+  if (isa < 0) {
+    isa = 0;
+    if (__builtin_cpu_supports("avx2")) isa = 1;
+    if (isa && __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw") &&
+        __builtin_cpu_supports("avx512vbmi") && __builtin_cpu_supports("avx512vl"))
+      isa = 2;
+  }
+  use = isa;
+  if (e) {
+    const int want = !strcmp(e, "scalar") ? 0 : !strcmp(e, "avx2") ? 1 : 2;
+    use = want < isa ? want : isa;
+  }
+  if (use == 2) pack_rows_avx512(ascii, n, m, out, ostride);
+  else if (use == 1) pack_rows_avx2(ascii, n, m, out, ostride);
   else pack_rows_scalar(ascii, n, m, out, ostride);
 }
 

@@ -100,6 +100,7 @@ def load() -> ctypes.CDLL:
         "kfmi_host_alloc": (i32, [u64, pvp]),
         "kfmi_host_free": (i32, [vp]),
         "kfmi_stream_release": (i32, []),
+        "kfmi_stream_hostpacked_fraction": (ctypes.c_double, []),
         "kfmi_pack_queries": (i32, [vp, u64, u32, vp]),
         "kfmi_set_devices": (i32, [ctypes.POINTER(ctypes.c_int32), i32]),
         "kfmi_get_devices": (i32, [ctypes.POINTER(ctypes.c_int32), i32]),

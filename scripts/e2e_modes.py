@@ -1,0 +1,54 @@
+#!/usr/bin/env python3
+"""Streamed (host -> host) search: per-chunk transfer mode (KFMI_STREAM_HOSTPACK
+0 = ASCII, 1 = host-packed, 2 = adaptive) x host packing ISA, pinned and
+pageable input, 3 Gbase / 10M x 100 bp (dev tool; not the bench contract).
+One JSON line per measurement on stdout."""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "k-step_fm-index_amd"))
+import kstep_fmi as K  # noqa: E402
+from kstep_fmi import synth  # noqa: E402
+
+K.load()
+K.set_device(0)
+text = synth.text_3g()
+idx = K.Index.build(text, k=2, d=64, gpu=True)
+reads = synth.gather_reads(text, synth.read_starts(len(text), 10_000_000, 100, 10), 100)
+del text
+K.set_backend("task-mid")
+want = K.search_array(idx, reads)
+K.transfer_to_gpu(idx, None, None)
+pin = K.pinned_empty(reads.shape, np.uint8)
+pin[:] = reads
+pout = K.pinned_empty((2 * reads.shape[0],), np.uint32)
+for isa in ("avx2", "avx512"):
+    os.environ["KFMI_QPACK_ISA"] = isa
+    t = time.perf_counter()
+    K.pack_queries(reads[:2_000_000])
+    p1 = 2_000_000 * 100 / (time.perf_counter() - t) / 1e9
+    for mode in ("1", "0", "2"):
+        os.environ["KFMI_STREAM_HOSTPACK"] = mode
+        for kind, src, dst in (("pinned", pin, pout), ("pageable", reads, None)):
+            K.search_stream(idx, src, out=dst)
+            ms = []
+            for _ in range(3):
+                t = time.perf_counter()
+                out = K.search_stream(idx, src, out=dst)
+                ms.append((time.perf_counter() - t) * 1e3)
+            lt = K.last_timing()
+            print(json.dumps({"isa": isa, "pack_1thread_GBs": round(p1, 2), "mode": mode, "input": kind,
+                              "ms": round(float(np.median(ms)), 3),
+                              "mqps": round(reads.shape[0] / np.median(ms) * 1e3 / 1e6, 1),
+                              "host_ms": round(lt["pack_ms"], 3), "wait_ms": round(lt["lf_ms"], 3),
+                              "hostpacked_fraction": round(K.load().kfmi_stream_hostpacked_fraction(), 3),
+                              "equal": bool(np.array_equal(out, want))}), flush=True)

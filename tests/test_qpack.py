@@ -23,19 +23,26 @@ def words_ref(reads: np.ndarray, k: int) -> np.ndarray:
     return out
 
 
-@pytest.mark.parametrize("m", [2, 4, 16, 30, 32, 34, 64, 96, 100, 126, 128, 150, 250, 256, 300])
-def test_pack_matches_step_order(kfmi_mod, m):
+@pytest.mark.parametrize("isa", ["scalar", "avx2", "avx512"])
+@pytest.mark.parametrize("m", [2, 4, 16, 30, 32, 34, 63, 64, 65, 96, 100, 126, 128, 150, 160, 250, 256, 300])
+def test_pack_matches_step_order(kfmi_mod, m, isa, monkeypatch):
     K = kfmi_mod
+    monkeypatch.setenv("KFMI_QPACK_ISA", isa)
     rng = np.random.default_rng(m)
     reads = rng.choice(np.frombuffer(b"ACGTNacgtn", np.uint8), size=(37, m))
     got = K.pack_queries(reads)
     for k in (1, 2):
-        assert np.array_equal(got, words_ref(reads, k)), k
+        if m % k == 0:          # odd m is K=1 only
+            assert np.array_equal(got, words_ref(reads, k)), k
 
 
-def test_pack_every_byte_value(kfmi_mod):
+@pytest.mark.parametrize("isa", ["scalar", "avx2", "avx512"])
+def test_pack_every_byte_value(kfmi_mod, isa, monkeypatch):
     K = kfmi_mod
+    monkeypatch.setenv("KFMI_QPACK_ISA", isa)
     reads = np.arange(256, dtype=np.uint8).reshape(4, 64)   # codes of all 256 bytes, both SIMD lanes
+    assert np.array_equal(K.pack_queries(reads), words_ref(reads, 2))
+    reads = np.arange(256, dtype=np.uint8).reshape(2, 128)
     assert np.array_equal(K.pack_queries(reads), words_ref(reads, 2))
 
 

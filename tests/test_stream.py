@@ -27,23 +27,29 @@ def setup(kfmi_mod):
     return K, idx, reads
 
 
-@pytest.mark.parametrize("hostpack", ["1", "0"])
+@pytest.mark.parametrize("hostpack", ["1", "0", "2", "3"])
 @pytest.mark.parametrize("backend", ["task-mid", "coop-mid", "task", "coop-ac", "task-ac128"])
 @pytest.mark.parametrize("chunk", [0, 1_000, 4_099])
 def test_stream_equals_batch_and_oracle(setup, oracle_mod, backend, chunk, hostpack, monkeypatch):
-    """hostpack 1 (default): code words packed on the host (qpack.c) and sent
-    over PCIe; 0: ASCII sent and packed on the device."""
+    """hostpack 1: code words packed on the host (qpack.c) and sent over PCIe;
+    0: ASCII sent and packed on the device; 2 (default): chosen per chunk by
+    the cost model; 3: alternating chunks (both kinds in one batch)."""
     K, idx, reads = setup
     monkeypatch.setenv("KFMI_STREAM_HOSTPACK", hostpack)
     want = K.search_array(idx, reads, backend)
     got = K.search_stream(idx, reads, chunk=chunk)
     assert np.array_equal(got, want)
+    frac = K.load().kfmi_stream_hostpacked_fraction()
+    if hostpack in ("0", "1"):
+        assert frac == float(hostpack)
+    elif hostpack == "3" and chunk:
+        assert 0.0 < frac < 1.0
     if chunk == 1_000 and backend == "task-mid":
         ores, _ = oracle_mod.search(idx.image(), reads, 8)
         assert np.array_equal(got, ores)
 
 
-@pytest.mark.parametrize("hostpack", ["1", "0"])
+@pytest.mark.parametrize("hostpack", ["1", "0", "2", "3"])
 def test_stream_pinned_buffers(setup, hostpack, monkeypatch):
     K, idx, reads = setup
     monkeypatch.setenv("KFMI_STREAM_HOSTPACK", hostpack)
@@ -60,7 +66,7 @@ def test_stream_pinned_buffers(setup, hostpack, monkeypatch):
     assert K.last_timing()["total_ms"] > 0
 
 
-@pytest.mark.parametrize("hostpack", ["1", "0"])
+@pytest.mark.parametrize("hostpack", ["1", "0", "2", "3"])
 def test_stream_k1_and_150bp(kfmi_mod, oracle_mod, hostpack, monkeypatch):
     K = kfmi_mod
     monkeypatch.setenv("KFMI_STREAM_HOSTPACK", hostpack)
@@ -93,7 +99,7 @@ def test_stream_errors(setup):
     K.load().kfmi_stream_release()
 
 
-@pytest.mark.parametrize("hostpack", ["1", "0"])
+@pytest.mark.parametrize("hostpack", ["1", "0", "2", "3"])
 @pytest.mark.parametrize("m", [2, 4, 16, 32, 34, 254, 256, 300, 1000])
 def test_stream_read_lengths(kfmi_mod, hostpack, m, monkeypatch):
     """Every word-count class of the host packer (ceil(m/16) words, partial
