@@ -465,8 +465,9 @@ def main():
         try:
             ingest = ingest_leg(idx, reads, res, D.world)
             log(f"rank {D.rank}: ingest {ingest}")
-        except K.KfmiError as e:
-            ingest = {"error": str(e)}
+        except Exception as e:          # auxiliary leg (e.g. TMPDIR full): report, never abort the bench
+            ingest = {"error": repr(e)}
+            os.environ.pop("KFMI_LOAD_MMAP", None)
     rank_rows = D.gather({"ingest": ingest, "rank": D.rank, "device": dev, "queries": int(reads.shape[0]),
                           "lf_ms": round(float(np.mean(lf_ms)), 4), "step_ms": round(float(np.mean(tot_ms)), 4),
                           "elapsed_s": round(elapsed, 4), "distinct_blocks": int(blocks),
@@ -537,9 +538,9 @@ def main():
                                                   "on this card: host upload + relayout on the first, "
                                                   "hipMemcpyPeerAsync to the others"}
             log(f"group replication {extra['group_replication']}")
-        except K.KfmiError as e:
+        except Exception as e:
             K.set_devices([])
-            extra["group_replication"] = {"error": str(e)}
+            extra["group_replication"] = {"error": repr(e)}
         # ---- end to end from host memory: streamed H2D + search + D2H ------
         if a.e2e_steps > 0:
             try:

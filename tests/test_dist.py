@@ -84,3 +84,14 @@ def test_aggregate_ranks_single_and_cpu_threads():
     agg = bench.aggregate_ranks([{"rank": 0, "queries": 1, "lf_ms": 1, "step_ms": 1, "parity_ok": None}])
     assert agg["parity_ok_all"] is None                       # sample skipped: no claim
     assert bench.cpu_threads() == len(os.sched_getaffinity(0))
+
+
+def test_cpu_thread_counts(monkeypatch):
+    import bench
+    aff = len(os.sched_getaffinity(0))
+    monkeypatch.setattr(bench, "cpu_quota", lambda: None)
+    assert bench.baseline_thread_counts() == [aff] and bench.cpu_effective() == aff
+    monkeypatch.setattr(bench, "cpu_quota", lambda: 0.5)
+    if aff > 1:
+        assert bench.baseline_thread_counts() == [aff, 1]
+    assert bench.cpu_effective() == 1

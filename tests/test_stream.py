@@ -117,3 +117,71 @@ def test_stream_read_lengths(kfmi_mod, hostpack, m, monkeypatch):
     got = K.search_stream(idx, reads, chunk=256)
     assert np.array_equal(got, want)
     K.load().kfmi_stream_release()
+
+
+def test_stream_does_not_block_other_calls(setup):
+    """A long streamed search on device 0 holds only that device's stream pool:
+    resident-batch searches from another thread on the same device complete
+    while it runs (round-1 ADVICE: the pool lock used to be process-wide)."""
+    import threading
+    import time
+    K, idx, reads = setup
+    K.set_backend("task-mid")
+    K.transfer_to_gpu(idx, None, None)
+    big = np.ascontiguousarray(np.tile(reads, (300, 1)))          # 3M reads in 4096-read chunks
+    want_big = np.tile(K.search_array(idx, reads), 300)
+    K.transfer_to_gpu(idx, None, None)
+    stream_out, done = {}, {}
+
+    def streamer():
+        K.set_device(0)
+        K.set_backend("task-mid")
+        stream_out["res"] = K.search_stream(idx, big, chunk=4096)
+        done["stream"] = time.perf_counter()
+
+    th = threading.Thread(target=streamer)
+    th.start()
+    time.sleep(0.01)
+    small = K.search_array(idx, reads[:1000])
+    done["search"] = time.perf_counter()
+    th.join()
+    assert np.array_equal(stream_out["res"], want_big)
+    assert np.array_equal(small, want_big[:2000])
+    assert done["search"] < done["stream"], "search waited for the whole streamed call"
+
+
+def test_threads_with_different_ftab(setup, oracle_mod):
+    """kfmi_set_ftab is per thread; tables are built once per (index, bases) and
+    never freed while the index is on the device, so concurrent searches with
+    different table sizes on one index stay exact (round-1 ADVICE)."""
+    import threading
+    K, idx, reads = setup
+    want, _ = oracle_mod.search(idx.image(), reads, 8)
+    K.set_backend("task-mid")
+    K.transfer_to_gpu(idx, None, None)
+    errs = []
+
+    def worker(bases):
+        try:
+            K.set_device(0)
+            K.set_backend("task-mid")
+            K.set_ftab(bases)
+            for _ in range(5):
+                q = K.Queries.from_array(reads)
+                r = K.Results.alloc(reads.shape[0])
+                K.transfer_to_gpu(idx, q, r)
+                K.search(idx, q, r)
+                K.transfer_to_cpu(r)
+                if not np.array_equal(r.array(), want):
+                    errs.append(bases)
+                q.close()
+                r.close()
+        except Exception as e:      # noqa: BLE001 -- reported below
+            errs.append(repr(e))
+
+    ths = [threading.Thread(target=worker, args=(b,)) for b in (0, 8, 10, 12)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not errs, errs
