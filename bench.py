@@ -62,8 +62,8 @@ def parse():
                    help="reads per rank checked against the CPU oracle after the timed region (0 = skip)")
     p.add_argument("--cpu-port-only", action="store_true",
                    help="time only our restatement, not the reference's CPU binary (oracle/_ref)")
-    p.add_argument("--variants", default="task,coop,task-ac,coop-ac,task-ac128,coop-ac128,task-packed,coop-packed,"
-                                         "task-mid,coop-mid,task-mid+ftab14",
+    p.add_argument("--variants", default="task,coop,task-ac,coop-ac,task-ac128,coop-ac128,task-ac-mid,coop-ac-mid,"
+                                         "task-packed,coop-packed,task-mid,coop-mid,task-mid+ftab14",
                    help="other backends timed on rank 0 at N=1 (empty = none)")
     p.add_argument("--variant-steps", type=int, default=3)
     p.add_argument("--no-ingest", dest="ingest", action="store_false",

@@ -34,7 +34,7 @@ struct CoopCfg {
   static constexpr int WPB0 = 65536 / WAVE_LDS;
   static constexpr int WPB = WPB0 < 1 ? 1 : (WPB0 > 4 ? 4 : WPB0);   // waves per block
   static constexpr bool OK = (G::BMW % 4 == 0) && (G::EW % 4 == 0) && (G::BOFF % 4 == 0) &&
-                             (!G::ACRULE || G::HALF >= 4) && (G::LAY != LAY_MID || G::NC >= 4) &&
+                             (!G::ACRULE || G::HALF >= 4) && (!G::MIDLINES || G::NC >= 4) &&
                              TPR <= 64;
 };
 
@@ -45,7 +45,7 @@ __device__ __forceinline__ const uint8_t* coop_chunk_addr(const IdxArgs& ix, uin
   using C = CoopCfg<G>;
   const uint8_t* base = reinterpret_cast<const uint8_t*>(ix.ent);
   const uint64_t eb = (uint64_t) b * (G::EW * 4);
-  if constexpr (G::LAY == LAY_MID) {
+  if constexpr (G::MIDLINES) {
     const uint64_t lb = (uint64_t) (b >> 1) * (G::EW * 4);
     if (k < C::BC) return base + lb + ((b & 1u) * G::BMW + 4 * k) * 4;
     return base + lb + (G::MIDCNT + (c & ~3u)) * 4;
@@ -74,7 +74,7 @@ __device__ __forceinline__ uint32_t coop_lf(const IdxArgs& ix, const uint8_t* sl
   const int o = (int) (X - b * (uint32_t) G::D);
   bool e = false;
   if constexpr (G::ACRULE) e = ((b & 1u) != 0) == (c < (uint32_t) G::HALF);
-  if constexpr (G::LAY == LAY_MID) e = (b & 1u) == 0;
+  if constexpr (G::MIDLINES) e = (b & 1u) == 0;
   uint32_t pop = 0;
 #pragma unroll
   for (int k = 0; k < C::BC; ++k) {
@@ -94,6 +94,8 @@ __device__ __forceinline__ uint32_t coop_lf(const IdxArgs& ix, const uint8_t* sl
     cnt = sbase + reinterpret_cast<const uint16_t*>(slot + 16 * C::BC)[c & 7u];
   else
     cnt = reinterpret_cast<const uint32_t*>(slot + 16 * C::BC)[c & 3u];
+  if constexpr (G::LAY == LAY_MIDAC)
+    if (b >= ix.ac_tail_b0) return ac_tail_step<G>(ix, b, c, X, sx);
   return finish<G>(ix, cnt, pop, b, c, X, e);
 }
 

@@ -22,6 +22,14 @@
  *                searched backward (e = 1) and an odd block forward from the SAME
  *                line.  K=2, d=64: one 128-byte line per LF and nothing else --
  *                the AltCounters idea packed into one 128-B HBM request.
+ *   LAY_MIDAC  : the LAY_MID lines with tag-201 (AltCounters) semantics.  The
+ *                AltCounters searcher returns the true rank (= LAY_MID's
+ *                result) in every block but the last real one (E-1) and the B5
+ *                block E, where it counts back from the transform's sentinel
+ *                counters (transformIndexAlternateCounters.c:420-431: '$' rows
+ *                of block E-1 counted as their stored code, padding as A);
+ *                blocks >= E-1 take that formula with the AC counters of
+ *                entries E-1, E, E+1 (ix.ac_tail), everything else is LAY_MID.
  *   LAY_AC128  : tag-201 (AltCounters) semantics, one power-of-two line per
  *                d-block: [planes of block b | cnt_half_b | cnt_half_{b+1}],
  *                so both counters the AC rule may pick (entry b or b+1,
@@ -36,7 +44,7 @@
 
 namespace kfmi {
 
-enum Layout : int { LAY_INTER = 0, LAY_AC = 1, LAY_PACKED = 2, LAY_MID = 3, LAY_AC128 = 4 };
+enum Layout : int { LAY_INTER = 0, LAY_AC = 1, LAY_PACKED = 2, LAY_MID = 3, LAY_AC128 = 4, LAY_MIDAC = 5 };
 
 __host__ __device__ constexpr int pow2ceil(int x) { int p = 1; while (p < x) p <<= 1; return p; }
 
@@ -62,7 +70,8 @@ struct Geo {
   static constexpr bool ACRULE = LAY == LAY_AC || LAY == LAY_AC128;   // AltCounters direction rule
   static constexpr int SPW = 32 / (2 * K);                // K-steps per packed query word
   static constexpr bool SMALL = BMW <= 16;                // whole bitmap fits in registers
-  static constexpr bool TWO_SIDED = LAY == LAY_AC || LAY == LAY_MID || LAY == LAY_AC128;
+  static constexpr bool TWO_SIDED = LAY == LAY_AC || LAY == LAY_MID || LAY == LAY_AC128 || LAY == LAY_MIDAC;
+  static constexpr bool MIDLINES = LAY == LAY_MID || LAY == LAY_MIDAC;   // pairs of blocks per line
 };
 
 // Superblock shift of the packed layout: the largest S with (2^S - 1) * d <= 65535.
@@ -89,6 +98,10 @@ struct IdxArgs {
   // indexed by the low 2*K*ftab_steps bits of the query's code stream; null = off
   const uint2* __restrict__ ftab;
   uint32_t ftab_steps, ftab_mask;
+  // LAY_MIDAC: AltCounters counters of entries E-1, E (sentinel), E+1 (zero),
+  // NC each, and E-1 = the first block that takes the AltCounters formula
+  const uint32_t* __restrict__ ac_tail;
+  uint32_t ac_tail_b0;
 };
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
@@ -270,7 +283,7 @@ __device__ __forceinline__ Where<G> locate(const IdxArgs& ix, uint32_t b, uint32
     w.planes = ent;
     w.cnt = nullptr;
     w.e = false;
-  } else {
+  } else {   // LAY_MID, LAY_MIDAC
     const uint32_t* line = ix.ent + (uint64_t) (b >> 1) * G::EW;
     w.e = (b & 1u) == 0;                          // even block: backward from the midpoint
     w.planes = line + (b & 1u) * G::BMW;
@@ -299,6 +312,27 @@ __device__ __forceinline__ uint32_t finish(const IdxArgs& ix, uint32_t cnt, uint
   const uint32_t bc = pop - (uint32_t) corr;
   if constexpr (G::TWO_SIDED) return e ? cnt - bc : cnt + bc;
   return cnt + bc;
+}
+
+// LAY_MIDAC, block b >= E-1: the AltCounters searcher's step
+// (fmIndexCPUBaseline-AltCounters.c:218-303) on this block's planes (read
+// again from its line: rare, L2-resident) and the tail counters.
+template <class G>
+__device__ __noinline__ uint32_t ac_tail_step(const IdxArgs& ix, uint32_t b, uint32_t c, uint32_t X,
+                                              const uint32_t (&sx)[2 * G::K])
+{
+  const uint32_t* pl = ix.ent + (uint64_t) (b >> 1) * G::EW + (b & 1u) * G::BMW;
+  const bool e = ((b & 1u) != 0) == (c < (uint32_t) G::HALF);
+  const int o = (int) (X - b * (uint32_t) G::D);
+  uint32_t pop = 0;
+  for (int w = 0; w < G::NB; ++w) {
+    const uint32_t m = row_mask(o - 32 * w);
+    pop += __popc((e ? ~m : m) & select_rows<G::K>(pl + w * G::PW, sx));
+  }
+  const uint32_t cnt = ix.ac_tail[(b + (e ? 1u : 0u) - ix.ac_tail_b0) * (uint32_t) G::NC + c];
+  const int corr = dollar_fix<G::K, true>(ix.dl, b, c, X, e);
+  const uint32_t bc = pop - (uint32_t) corr;
+  return e ? cnt - bc : cnt + bc;
 }
 
 // ---------------------------------------------------------------------------
@@ -357,6 +391,8 @@ __device__ __forceinline__ uint32_t lf_from_block(const IdxArgs& ix, const Blk<G
     if constexpr (G::TWO_SIDED) m = k.e ? ~m : m;
     pop += __popc(m & select_rows<G::K>(&k.bm[w * G::PW], sx));
   }
+  if constexpr (G::LAY == LAY_MIDAC)
+    if (k.b >= ix.ac_tail_b0) return ac_tail_step<G>(ix, k.b, c, X, sx);
   return finish<G>(ix, k.cnt, pop, k.b, c, X, k.e);
 }
 
@@ -404,6 +440,8 @@ __device__ __forceinline__ uint32_t lf_stream(const IdxArgs& ix, uint32_t X, uin
       pop += __popc(m & select_rows<G::K>(v[j], sx));
     }
   }
+  if constexpr (G::LAY == LAY_MIDAC)
+    if (b >= ix.ac_tail_b0) return ac_tail_step<G>(ix, b, c, X, sx);
   return finish<G>(ix, cnt, pop, b, c, X, wh.e);
 }
 

@@ -47,6 +47,8 @@ struct kfmi_dev_index {
    * kfmi_set_ftab values never free a table another kernel reads) */
   uint2* ftab[17] = {};
   std::mutex ftab_mu;
+  uint32_t* ac_tail = nullptr; /* LAY_MIDAC: 3 x NC AltCounters counters of entries E-1, E, E+1 */
+  uint32_t ac_tail_b0 = 0xFFFFFFFFu;
 };
 
 struct kfmi_dev_queries {

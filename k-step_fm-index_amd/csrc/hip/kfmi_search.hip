@@ -36,7 +36,7 @@ namespace kfmi {
 
 static const char* kBackendNames[KFMI_BK_COUNT] = {
     "task", "coop", "task-ac", "coop-ac", "task-packed", "coop-packed", "task-mid", "coop-mid",
-    "task-ac128", "coop-ac128"};
+    "task-ac128", "coop-ac128", "task-ac-mid", "coop-ac-mid"};
 
 static thread_local int t_backend = -1;
 thread_local int t_device = -1;
@@ -69,7 +69,8 @@ extern "C" kfmi_backend_t kfmi_backend(void)
 
 extern "C" uint32_t kfmi_backend_tag(kfmi_backend_t b)
 {
-  return (b == KFMI_BK_TASK_AC || b == KFMI_BK_COOP_AC || b == KFMI_BK_TASK_AC128 || b == KFMI_BK_COOP_AC128)
+  return (b == KFMI_BK_TASK_AC || b == KFMI_BK_COOP_AC || b == KFMI_BK_TASK_AC128 || b == KFMI_BK_COOP_AC128 ||
+          b == KFMI_BK_TASK_AC_MID || b == KFMI_BK_COOP_AC_MID)
              ? 201u : 101u;
 }
 
@@ -322,6 +323,8 @@ KFMI_FOR_NB(KFMI_EXTERN, 1, LAY_MID)
 KFMI_FOR_NB(KFMI_EXTERN, 2, LAY_MID)
 KFMI_FOR_NB(KFMI_EXTERN, 1, LAY_AC128)
 KFMI_FOR_NB(KFMI_EXTERN, 2, LAY_AC128)
+KFMI_FOR_NB(KFMI_EXTERN, 1, LAY_MIDAC)
+KFMI_FOR_NB(KFMI_EXTERN, 2, LAY_MIDAC)
 
 hipError_t dispatch(Op op, uint32_t K, uint32_t nb, int lay, const SearchLaunch& a, unsigned long long* d_total)
 {
@@ -337,6 +340,8 @@ hipError_t dispatch(Op op, uint32_t K, uint32_t nb, int lay, const SearchLaunch&
   KFMI_FOR_NB(KFMI_CASE, 2, LAY_MID)
   KFMI_FOR_NB(KFMI_CASE, 1, LAY_AC128)
   KFMI_FOR_NB(KFMI_CASE, 2, LAY_AC128)
+  KFMI_FOR_NB(KFMI_CASE, 1, LAY_MIDAC)
+  KFMI_FOR_NB(KFMI_CASE, 2, LAY_MIDAC)
 #undef KFMI_CASE
   return hipErrorInvalidValue;
 }
@@ -359,6 +364,8 @@ static bool geometry_supported(int backend, uint32_t K, uint32_t nb, int lay)
   KFMI_FOR_NB(KFMI_OKC, 2, LAY_MID)
   KFMI_FOR_NB(KFMI_OKC, 1, LAY_AC128)
   KFMI_FOR_NB(KFMI_OKC, 2, LAY_AC128)
+  KFMI_FOR_NB(KFMI_OKC, 1, LAY_MIDAC)
+  KFMI_FOR_NB(KFMI_OKC, 2, LAY_MIDAC)
 #undef KFMI_OKC
   return false;
 }
@@ -417,6 +424,7 @@ static int layout_of(int backend)
     case KFMI_BK_TASK: case KFMI_BK_COOP: return LAY_INTER;
     case KFMI_BK_TASK_AC: case KFMI_BK_COOP_AC: return LAY_AC;
     case KFMI_BK_TASK_MID: case KFMI_BK_COOP_MID: return LAY_MID;
+    case KFMI_BK_TASK_AC_MID: case KFMI_BK_COOP_AC_MID: return LAY_MIDAC;
     case KFMI_BK_TASK_AC128: case KFMI_BK_COOP_AC128: return LAY_AC128;
     default: return LAY_PACKED;
   }
@@ -425,7 +433,7 @@ static int layout_of(int backend)
 bool is_coop(int backend)
 {
   return backend == KFMI_BK_COOP || backend == KFMI_BK_COOP_AC || backend == KFMI_BK_COOP_PACKED ||
-         backend == KFMI_BK_COOP_MID || backend == KFMI_BK_COOP_AC128;
+         backend == KFMI_BK_COOP_MID || backend == KFMI_BK_COOP_AC128 || backend == KFMI_BK_COOP_AC_MID;
 }
 
 /* ------------------------------------------------------------------------ */
@@ -468,7 +476,7 @@ static int32_t host_entries_for(const kfmi_fmi_t* f, int lay, kfmi_fmi_t** owned
 {
   *owned = nullptr;
   *use = f;
-  if (lay == LAY_INTER || lay == LAY_PACKED || lay == LAY_MID) {
+  if (lay == LAY_INTER || lay == LAY_PACKED || lay == LAY_MID || lay == LAY_MIDAC) {
     /* tag 101 as is; tag 100 is interleaved on the device (upload_entries),
      * or on the host with KFMI_HOST_INTERLEAVE=1 (A/B experiment) */
     if (f->tag == 100 && getenv("KFMI_HOST_INTERLEAVE") && atoi(getenv("KFMI_HOST_INTERLEAVE"))) {
@@ -532,6 +540,7 @@ void free_dev_index(kfmi_dev_index* di)
   if (di->ent) (void) hipFree(di->ent);
   if (di->sb) (void) hipFree(di->sb);
   if (di->sa) (void) hipFree(di->sa);
+  if (di->ac_tail) (void) hipFree(di->ac_tail);
   for (uint2* t : di->ftab)
     if (t) (void) hipFree(t);
   delete di;
@@ -719,7 +728,7 @@ int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx, kfmi_dev_
               hipStreamSynchronize(ctx->st) == hipSuccess;
     (void) hipFree(tmp);
     if (!ok) return fail(KFMI_E_KERNEL);
-  } else if (lay == LAY_MID) {
+  } else if (lay == LAY_MID || lay == LAY_MIDAC) {
     /* MID: pairs of blocks per line, built on the device from tag-101 entries;
      * counters of the last line (odd block count) and of one padding line are
      * "rows past n+1 read as A" extensions of the end counters. */
@@ -753,6 +762,17 @@ int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx, kfmi_dev_
     (void) hipFree(tmp);
     (void) hipFree(d_ext);
     if (!ok) return fail(KFMI_E_KERNEL);
+    if (lay == LAY_MIDAC) {   /* the AltCounters searcher's counters past the last real block */
+      std::vector<uint32_t> tail(3 * nc);
+      if (kfmi_ac_tail(src, tail.data(), &di->ac_tail_b0) != KFMI_SUCCESS) return fail(KFMI_E_BAD_ARGUMENT);
+      if (hipMalloc((void**) &di->ac_tail, 12ull * nc) != hipSuccess) {
+        di->ac_tail = nullptr;
+        return fail(KFMI_E_DEVICE_ALLOC);
+      }
+      if (hipMemcpyAsync(di->ac_tail, tail.data(), 12ull * nc, hipMemcpyHostToDevice, ctx->st) != hipSuccess ||
+          hipStreamSynchronize(ctx->st) != hipSuccess)
+        return fail(KFMI_E_KERNEL);
+    }
   } else {
     /* packed: build on the device from tag-101 entries (+ the padding entry) */
     const uint32_t ne = src->nentries + 1;
@@ -818,6 +838,8 @@ IdxArgs idx_args(const kfmi_dev_index* di)
   ix.ftab = nullptr;
   ix.ftab_steps = 0;
   ix.ftab_mask = 0;
+  ix.ac_tail = di->ac_tail;
+  ix.ac_tail_b0 = di->ac_tail_b0;
   return ix;
 }
 

@@ -333,14 +333,40 @@ static uint32_t count_entry100(const kfmi_fmi_t *f, uint32_t entry, uint32_t cod
     uint32_t m = position >= 32 ? 0xFFFFFFFFu : position > 0 ? 0xFFFFFFFFu << (32 - position) : 0u;
     for (s = 0; s < f->steps; s++) {
       uint32_t cs = (code >> (2 * s)) & 3u;
-      uint32_t b0 = e[kfmi_plane_index(100, f->steps, nb, s, 0, n)];
-      uint32_t b1 = e[kfmi_plane_index(100, f->steps, nb, s, 1, n)];
+      uint32_t b0 = e[kfmi_plane_index(f->tag, f->steps, nb, s, 0, n)];   /* tag 100 or 101 */
+      uint32_t b1 = e[kfmi_plane_index(f->tag, f->steps, nb, s, 1, n)];
       m &= ((cs & 1u) ? b0 : ~b0) & ((cs & 2u) ? b1 : ~b1);
     }
     cnt += (uint32_t) __builtin_popcount(m);
     position -= 32;
   }
   return cnt;
+}
+
+/* The counters the AltCounters searcher reads past the last real block:
+ * entry E-1 (its plain counters), the sentinel E (the last entry's counters
+ * plus its first (n+1) mod d rows counted from the bit planes plus the padding
+ * rows for code 0, transformIndexAlternateCounters.c:420-431, exactly as
+ * kfmi_transform_ac below) and E+1 (zero, as the AC device layout's padding).
+ * All NC codes; the searcher only reads the half each entry's parity keeps. */
+int32_t kfmi_ac_tail(const kfmi_fmi_t *f, uint32_t *out, uint32_t *first)
+{
+  uint32_t c, nc, nbw, rem, last;
+  const uint32_t *src;
+  if (!f || !out || (f->tag != 100 && f->tag != 101) || !f->nentries) return KFMI_E_BAD_ARGUMENT;
+  nc = f->ncounters;
+  nbw = 2 * f->nbitmaps * f->steps;
+  last = f->nentries;
+  rem = f->bwtsize % f->chunk;
+  src = f->h_index + (uint64_t) (last - 1) * f->entry_words;
+  for (c = 0; c < nc; c++) {
+    out[c] = src[nbw + c];
+    out[nc + c] = src[nbw + c] + (c == 0 ? f->chunk - rem : 0u) +
+                  (rem ? count_entry100(f, f->bwtsize / f->chunk, c, (int32_t) rem) : 0u);
+    out[2 * nc + c] = 0;
+  }
+  if (first) *first = last - 1;
+  return KFMI_SUCCESS;
 }
 
 /* tag 100 -> 200 and 201: transformIndexAlternateCounters.c:387-479.

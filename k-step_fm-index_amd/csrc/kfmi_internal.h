@@ -80,12 +80,17 @@ uint32_t kfmi_plane_index(uint32_t tag, uint32_t steps, uint32_t nb, uint32_t s,
 typedef enum {
   KFMI_BK_TASK = 0, KFMI_BK_COOP, KFMI_BK_TASK_AC, KFMI_BK_COOP_AC,
   KFMI_BK_TASK_PACKED, KFMI_BK_COOP_PACKED, KFMI_BK_TASK_MID, KFMI_BK_COOP_MID,
-  KFMI_BK_TASK_AC128, KFMI_BK_COOP_AC128, KFMI_BK_COUNT
+  KFMI_BK_TASK_AC128, KFMI_BK_COOP_AC128, KFMI_BK_TASK_AC_MID, KFMI_BK_COOP_AC_MID, KFMI_BK_COUNT
 } kfmi_backend_t;
 kfmi_backend_t kfmi_backend(void);
 uint32_t       kfmi_backend_tag(kfmi_backend_t b);   /* 101 or 201 */
 int32_t        kfmi_current_device(void);
 void           kfmi_set_last_error(int32_t e);
+
+/* AltCounters tail of a tag-100/101 index (fmi_index.c): out[3 * NC] = the
+ * tag-201 counters of entries E-1, E (the tfmiAC sentinel) and E+1 (zero) for
+ * every code, E = nentries; *first = E-1 */
+int32_t kfmi_ac_tail(const kfmi_fmi_t *f, uint32_t *out, uint32_t *first);
 
 /* sampled suffix array (fmi_index.c): (re)allocates h_sa for `rate` */
 int32_t kfmi_sa_alloc(kfmi_fmi_t *f, uint32_t rate);

@@ -15,7 +15,8 @@ from util import GOLDEN, manifest, read_qry
 pytestmark = pytest.mark.gpu
 
 PLAIN = ("task", "coop", "task-packed", "coop-packed", "task-mid", "coop-mid")
-ALT = ("task-ac", "coop-ac", "task-ac128", "coop-ac128")
+ALT = ("task-ac", "coop-ac", "task-ac128", "coop-ac128", "task-ac-mid", "coop-ac-mid")
+ACMID = ("task-ac-mid", "coop-ac-mid")     # AltCounters semantics on MID128 lines: built from tag 100/101
 
 
 def coop_supported(backend, k, d):
@@ -26,6 +27,8 @@ def coop_supported(backend, k, d):
     bmw = 2 * nb * k
     if backend in ("coop-ac", "coop-ac128"):
         return k == 2 and bmw % 4 == 0
+    if backend == "coop-ac-mid":
+        return bmw % 4 == 0
     if backend == "coop":
         return bmw % 4 == 0 and (bmw + 4 ** k) % 4 == 0
     return bmw % 4 == 0
@@ -52,7 +55,7 @@ def test_backend_matches_reference_results(gpu, oracle_mod, backend, case, key):
     ent = c["indexes"][key]
     k, d = ent["k"], ent["d"]
     ac = backend in ALT
-    tags = (200, 201, 100) if ac else (100, 101)
+    tags = (100, 101) if backend in ACMID else (200, 201, 100) if ac else (100, 101)
     checked = 0
     for tag in tags:
         idx = gpu.Index.load(GOLDEN / case / ent["files"][str(tag)]["file"])
@@ -265,3 +268,33 @@ def test_reorder_equals_oracle(gpu, oracle_mod, random_index, backend, monkeypat
             want, _ = oracle_mod.search(ref_img, q)
             got = gpu.search_array(idx, q, backend)
             assert np.array_equal(got, want), (backend, k, d, m)
+
+
+@pytest.mark.parametrize("backend", ACMID + ("task-ac",))
+@pytest.mark.parametrize("n", [63, 127, 191, 255, 1023, 4095, 100, 129, 5000])
+@pytest.mark.parametrize("tail", ["random", "T-run"])
+def test_ac_tail_blocks_against_ac_oracle(gpu, oracle_mod, backend, n, tail):
+    """The AltCounters searcher differs from the true rank only past the last
+    real block: its sentinel counts the '$' rows of block E-1 as their stored
+    code, and (n+1) % d == 0 reads the sentinel itself.  A T-run
+    at the end of the text puts the '$' rows of every BWT_s in the last block;
+    the *-ac-mid backends must reproduce the AltCounters oracle there."""
+    rng = np.random.default_rng(n + (7 if tail == "T-run" else 0))
+    t = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), size=n)
+    if tail == "T-run":
+        t[-min(n, 40):] = ord("T")
+    text = t.tobytes()
+    for k, d in ((2, 64), (1, 32), (2, 32), (2, 128)):
+        idx = gpu.Index.build(text, k=k, d=d)
+        img200 = idx.alt_counters()[0].image()
+        for m in (2, 4, 12):
+            if m > n or m % k:
+                continue
+            st = rng.integers(0, n - m + 1, size=64)
+            q = np.concatenate([t[st[:, None] + np.arange(m)[None, :]],
+                                rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), size=(32, m)),
+                                np.full((4, m), ord("T"), dtype=np.uint8), np.full((4, m), ord("A"), dtype=np.uint8)])
+            want, _ = oracle_mod.search(img200, q)
+            if not coop_supported(backend, k, d):
+                continue
+            assert np.array_equal(gpu.search_array(idx, q, backend), want), (n, tail, k, d, m, backend)
