@@ -304,12 +304,28 @@ __device__ __forceinline__ uint32_t load_counter(const IdxArgs& ix, const Where<
   }
 }
 
+// AltCounters semantics past the last real block: the searcher counts back
+// from the tfmiAC sentinel, whose counters include the '$' rows of block E-1
+// and the padding, so a step can land up to K rows past n+1; there, and when
+// (n+1) % d == 0, the reference reads past its own file and its
+// result is undefined -- a wrapped value would send the next load out of the
+// table.  Every AltCounters-semantics step is therefore capped at n+1+d rows,
+// which no defined result reaches and which keeps every block index inside
+// the layouts' padding.
+template <class G>
+__device__ __forceinline__ uint32_t ac_clamp(const IdxArgs& ix, uint32_t v)
+{
+  const uint32_t cap = ix.bwtsize + (uint32_t) G::D;
+  return v > cap ? cap : v;
+}
+
 template <class G>
 __device__ __forceinline__ uint32_t finish(const IdxArgs& ix, uint32_t cnt, uint32_t pop, uint32_t b, uint32_t c,
                                           uint32_t X, bool e)
 {
   const int corr = dollar_fix<G::K, G::TWO_SIDED>(ix.dl, b, c, X, e);
   const uint32_t bc = pop - (uint32_t) corr;
+  if constexpr (G::ACRULE) return ac_clamp<G>(ix, e ? cnt - bc : cnt + bc);
   if constexpr (G::TWO_SIDED) return e ? cnt - bc : cnt + bc;
   return cnt + bc;
 }
@@ -332,7 +348,7 @@ __device__ __noinline__ uint32_t ac_tail_step(const IdxArgs& ix, uint32_t b, uin
   const uint32_t cnt = ix.ac_tail[(b + (e ? 1u : 0u) - ix.ac_tail_b0) * (uint32_t) G::NC + c];
   const int corr = dollar_fix<G::K, true>(ix.dl, b, c, X, e);
   const uint32_t bc = pop - (uint32_t) corr;
-  return e ? cnt - bc : cnt + bc;
+  return ac_clamp<G>(ix, e ? cnt - bc : cnt + bc);
 }
 
 // ---------------------------------------------------------------------------
