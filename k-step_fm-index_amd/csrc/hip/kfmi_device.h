@@ -309,13 +309,14 @@ __device__ __forceinline__ uint32_t load_counter(const IdxArgs& ix, const Where<
 // and the padding, so a step can land up to K rows past n+1; there, and when
 // (n+1) % d == 0, the reference reads past its own file and its
 // result is undefined -- a wrapped value would send the next load out of the
-// table.  Every AltCounters-semantics step is therefore capped at n+1+d rows,
-// which no defined result reaches and which keeps every block index inside
-// the layouts' padding.
+// table.  Every AltCounters-semantics step is therefore capped at n+d rows
+// (bwtsize + d - 1), which no defined result reaches (they stay within n+1+K)
+// and which keeps the block index at most E, the sentinel, even when
+// (n+1) % d == 0: inside every layout's padding.
 template <class G>
 __device__ __forceinline__ uint32_t ac_clamp(const IdxArgs& ix, uint32_t v)
 {
-  const uint32_t cap = ix.bwtsize + (uint32_t) G::D;
+  const uint32_t cap = ix.bwtsize + (uint32_t) G::D - 1u;
   return v > cap ? cap : v;
 }
 
@@ -345,7 +346,9 @@ __device__ __noinline__ uint32_t ac_tail_step(const IdxArgs& ix, uint32_t b, uin
     const uint32_t m = row_mask(o - 32 * w);
     pop += __popc((e ? ~m : m) & select_rows<G::K>(pl + w * G::PW, sx));
   }
-  const uint32_t cnt = ix.ac_tail[(b + (e ? 1u : 0u) - ix.ac_tail_b0) * (uint32_t) G::NC + c];
+  uint32_t row = b + (e ? 1u : 0u) - ix.ac_tail_b0;   /* 0, 1, 2: entries E-1, E, E+1 */
+  row = row > 2u ? 2u : row;
+  const uint32_t cnt = ix.ac_tail[row * (uint32_t) G::NC + c];
   const int corr = dollar_fix<G::K, true>(ix.dl, b, c, X, e);
   const uint32_t bc = pop - (uint32_t) corr;
   return ac_clamp<G>(ix, e ? cnt - bc : cnt + bc);

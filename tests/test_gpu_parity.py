@@ -280,7 +280,7 @@ def test_ac_tail_blocks(gpu, oracle_mod, n, tail):
     Where the reference reads past its own file -- (n+1) % d == 0
     or a step landing in the sentinel block, (n+1) % d >= d - K -- its result
     is undefined (the CPU oracle may fault); there every AltCounters backend
-    must stay in bounds (steps capped at n+1+d) and agree with the others."""
+    must stay in bounds (steps capped at n+d) and agree with the others."""
     rng = np.random.default_rng(n + (7 if tail == "T-run" else 0))
     t = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), size=n)
     if tail == "T-run":
@@ -302,7 +302,7 @@ def test_ac_tail_blocks(gpu, oracle_mod, n, tail):
                 want, _ = oracle_mod.search(img200, q)
             else:
                 want = gpu.search_array(idx, q, "task-ac")
-                assert int(want.max()) <= n + 1 + d
+                assert int(want.max()) <= n + d
             for b in ACMID + ("task-ac128", "coop-ac128"):
                 if coop_supported(b, k, d):
                     assert np.array_equal(gpu.search_array(idx, q, b), want), (n, tail, k, d, m, b, defined)
