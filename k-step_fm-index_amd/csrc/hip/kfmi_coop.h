@@ -75,7 +75,7 @@ __device__ __forceinline__ uint32_t coop_lf(const IdxArgs& ix, const uint8_t* sl
   bool e = false;
   if constexpr (G::ACRULE) e = ((b & 1u) != 0) == (c < (uint32_t) G::HALF);
   if constexpr (G::MIDLINES) e = (b & 1u) == 0;
-  uint32_t pop = 0;
+  uint32_t pop = 0, all = 0;
 #pragma unroll
   for (int k = 0; k < C::BC; ++k) {
     const uint4 v = *reinterpret_cast<const uint4*>(slot + 16 * k);
@@ -86,7 +86,9 @@ __device__ __forceinline__ uint32_t coop_lf(const IdxArgs& ix, const uint8_t* sl
       const int w = k * (4 / G::PW) + h;
       uint32_t m = row_mask(o - 32 * w);
       if constexpr (G::TWO_SIDED) m = e ? ~m : m;
-      pop += __popc(m & select_rows<G::K>(&pl[h * G::PW], sx));
+      const uint32_t sel = select_rows<G::K>(&pl[h * G::PW], sx);
+      pop += __popc(m & sel);
+      if constexpr (G::LAY == LAY_MIDAC) all += __popc(sel);
     }
   }
   uint32_t cnt;
@@ -95,7 +97,7 @@ __device__ __forceinline__ uint32_t coop_lf(const IdxArgs& ix, const uint8_t* sl
   else
     cnt = reinterpret_cast<const uint32_t*>(slot + 16 * C::BC)[c & 3u];
   if constexpr (G::LAY == LAY_MIDAC)
-    if (b >= ix.ac_tail_b0) return ac_tail_step<G>(ix, b, c, X, sx);
+    if (b >= ix.ac_tail_b0) return ac_tail_step<G>(ix, b, c, X, pop, all);
   return finish<G>(ix, cnt, pop, b, c, X, e);
 }
 

@@ -332,20 +332,18 @@ __device__ __forceinline__ uint32_t finish(const IdxArgs& ix, uint32_t cnt, uint
 }
 
 // LAY_MIDAC, block b >= E-1: the AltCounters searcher's step
-// (fmIndexCPUBaseline-AltCounters.c:218-303) on this block's planes (read
-// again from its line: rare, L2-resident) and the tail counters.
+// (fmIndexCPUBaseline-AltCounters.c:218-303) from what the MID step already
+// has -- its popcount over the MID direction (pop_mid; forward for odd b,
+// backward for even b) and the block's whole count of code c (pop_all), so
+// the AC direction's count is one of pop_mid or pop_all - pop_mid -- plus the
+// AC counter of entry b or b+1 (ix.ac_tail; a rare, cached load).
 template <class G>
-__device__ __noinline__ uint32_t ac_tail_step(const IdxArgs& ix, uint32_t b, uint32_t c, uint32_t X,
-                                              const uint32_t (&sx)[2 * G::K])
+__device__ __forceinline__ uint32_t ac_tail_step(const IdxArgs& ix, uint32_t b, uint32_t c, uint32_t X,
+                                                 uint32_t pop_mid, uint32_t pop_all)
 {
-  const uint32_t* pl = ix.ent + (uint64_t) (b >> 1) * G::EW + (b & 1u) * G::BMW;
   const bool e = ((b & 1u) != 0) == (c < (uint32_t) G::HALF);
-  const int o = (int) (X - b * (uint32_t) G::D);
-  uint32_t pop = 0;
-  for (int w = 0; w < G::NB; ++w) {
-    const uint32_t m = row_mask(o - 32 * w);
-    pop += __popc((e ? ~m : m) & select_rows<G::K>(pl + w * G::PW, sx));
-  }
+  const bool e_mid = (b & 1u) == 0;
+  const uint32_t pop = e == e_mid ? pop_mid : pop_all - pop_mid;
   uint32_t row = b + (e ? 1u : 0u) - ix.ac_tail_b0;   /* 0, 1, 2: entries E-1, E, E+1 */
   row = row > 2u ? 2u : row;
   const uint32_t cnt = ix.ac_tail[row * (uint32_t) G::NC + c];
@@ -410,8 +408,14 @@ __device__ __forceinline__ uint32_t lf_from_block(const IdxArgs& ix, const Blk<G
     if constexpr (G::TWO_SIDED) m = k.e ? ~m : m;
     pop += __popc(m & select_rows<G::K>(&k.bm[w * G::PW], sx));
   }
-  if constexpr (G::LAY == LAY_MIDAC)
-    if (k.b >= ix.ac_tail_b0) return ac_tail_step<G>(ix, k.b, c, X, sx);
+  if constexpr (G::LAY == LAY_MIDAC) {
+    if (k.b >= ix.ac_tail_b0) {   /* rare: the last real block and past it */
+      uint32_t all = 0;
+#pragma unroll
+      for (int w = 0; w < G::NB; ++w) all += __popc(select_rows<G::K>(&k.bm[w * G::PW], sx));
+      return ac_tail_step<G>(ix, k.b, c, X, pop, all);
+    }
+  }
   return finish<G>(ix, k.cnt, pop, k.b, c, X, k.e);
 }
 
@@ -431,7 +435,7 @@ __device__ __forceinline__ uint32_t lf_stream(const IdxArgs& ix, uint32_t X, uin
   const uint32_t cnt = load_counter<G>(ix, wh, b, c);
   const uint32_t* pl = wh.planes;
   constexpr int CH = G::NB < 8 ? G::NB : 8;
-  uint32_t pop = 0;
+  uint32_t pop = 0, all = 0;
 #pragma unroll
   for (int w0 = 0; w0 < G::NB; w0 += CH) {
     uint32_t v[CH][G::PW];
@@ -456,11 +460,13 @@ __device__ __forceinline__ uint32_t lf_stream(const IdxArgs& ix, uint32_t X, uin
       if (w >= G::NB) break;
       uint32_t m = row_mask(o - 32 * w);
       if constexpr (G::TWO_SIDED) m = wh.e ? ~m : m;
-      pop += __popc(m & select_rows<G::K>(v[j], sx));
+      const uint32_t sel = select_rows<G::K>(v[j], sx);
+      pop += __popc(m & sel);
+      if constexpr (G::LAY == LAY_MIDAC) all += __popc(sel);
     }
   }
   if constexpr (G::LAY == LAY_MIDAC)
-    if (b >= ix.ac_tail_b0) return ac_tail_step<G>(ix, b, c, X, sx);
+    if (b >= ix.ac_tail_b0) return ac_tail_step<G>(ix, b, c, X, pop, all);
   return finish<G>(ix, cnt, pop, b, c, X, wh.e);
 }
 
