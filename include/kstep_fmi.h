@@ -117,6 +117,10 @@ char    *errorCommon(int32_t e);
  *   "coop-packed" wave64 cooperative gather on the packed layout            (tag 101 semantics)
  *   "task-mid"    task-per-query on the MID128 layout: one 128-byte line per LF (tag 101 semantics)
  *   "coop-mid"    wave64 cooperative gather on the MID128 layout              (tag 101 semantics)
+ *   "task-ac128" / "coop-ac128"  one 128-byte line per block, both AC counters (tag 201 semantics)
+ *   "task-ac-mid" / "coop-ac-mid" the MID128 lines with AltCounters semantics: the AltCounters
+ *                 step only past the last real block, from the tfmiAC sentinel (tag 201 semantics;
+ *                 built from a tag 100/101 file, an AC file returns 101)
  * The default comes from KFMI_BACKEND, else "task-mid".  transferCPUtoGPU
  * re-lays-out the loaded index for the backend: plain-counter backends take
  * tag 100 or 101 (an AC file returns 101, as the reference loader would);
