@@ -45,6 +45,11 @@ struct StreamSlot {
 struct StreamPool {
   bool init = false;
   StreamSlot slot[NSLOT];
+  /* adaptive transfer mode: measured costs in ms per byte, kept across calls
+   * (0 = not measured yet).  Host: EMA of packing / staging time per ASCII
+   * byte.  Link: the fastest H2D seen per byte sent (the events bracketing a
+   * copy also count time queued behind other slots' copies). */
+  double r_pack = 0, r_stage = 0, r_xa = 0, r_xp = 0;
 };
 static StreamPool g_pool[64];
 static thread_local double t_stream_packed_frac = 0;   /* share of the last streamed batch packed on the host */
@@ -314,15 +319,12 @@ extern "C" int32_t kfmi_search_stream(void* index, const char* ascii, uint64_t n
     if (err) return err;
     s.busy = false;
   }
-  /* cost model (ms per read), seeded with nominal rates and refined by EMAs */
-  const double nthr = (double) HostPool::get().size();
-  double c_pack = size / (3.0e6 * nthr);              /* host packing */
-  double c_stage = pin_in ? 0.0 : size / (8.0e6 * nthr);   /* host staging copy of ASCII */
-  double c_xa = size / 50.0e6;                        /* ASCII over PCIe (~50 GB/s) */
-  double c_xp = 4.0 * nwords / 50.0e6;                /* packed words over PCIe */
-  double t_host = 0, t_link = 0;                      /* model clocks */
+  /* cost model: pool.r_* per byte (see StreamPool) -> ms per read */
+  const double abytes = (double) size, pbytes = 4.0 * nwords;
+  double t_host = 0, t_link = 0;                      /* model clocks of this call */
   uint64_t npacked = 0;
-  auto ema = [](double& v, double x) { v = 0.6 * v + 0.4 * x; };
+  auto ema = [](double& v, double x) { v = v > 0 ? 0.6 * v + 0.4 * x : x; };
+  auto keep_min = [](double& v, double x) { v = (v > 0 && v < x) ? v : x; };
   const auto t0 = std::chrono::steady_clock::now();
   const Op op = is_coop(di->backend) ? Op::Coop : Op::Task;
   IdxArgs ix = idx_args(di);
@@ -341,7 +343,10 @@ extern "C" int32_t kfmi_search_stream(void* index, const char* ascii, uint64_t n
     else {
       if (!pin_out) par_copy(results + 2 * s.q0, s.h_out, 8ull * s.n);
       float x = 0;
-      if (hipEventElapsedTime(&x, s.x0, s.x1) == hipSuccess && s.n) ema(s.packed_mode ? c_xp : c_xa, x / s.n);
+      if (hipEventElapsedTime(&x, s.x0, s.x1) == hipSuccess && s.n && x > 0) {
+        if (s.packed_mode) keep_min(pool.r_xp, x / (s.n * pbytes));
+        else keep_min(pool.r_xa, x / (s.n * abytes));
+      }
     }
     s.busy = false;
   };
@@ -358,12 +363,15 @@ extern "C" int32_t kfmi_search_stream(void* index, const char* ascii, uint64_t n
     bool host_pack;
     if (mode == 0 || mode == 1) host_pack = mode == 1;
     else if (mode == 3) host_pack = (i & 1) == 0;
+    else if (pool.r_pack <= 0 || pool.r_xp <= 0) host_pack = true;      /* measure packing first */
+    else if (pool.r_xa <= 0 || (!pin_in && pool.r_stage <= 0)) host_pack = false;   /* then ASCII */
     else {
       const double dn = (double) s.n;
-      const double done_p = std::max(t_host + c_pack * dn, t_link) + c_xp * dn;
-      const double done_a = std::max(t_host + c_stage * dn, t_link) + c_xa * dn;
+      const double hp_ms = pool.r_pack * abytes * dn, st_ms = pin_in ? 0.0 : pool.r_stage * abytes * dn;
+      const double done_p = std::max(t_host + hp_ms, t_link) + pool.r_xp * pbytes * dn;
+      const double done_a = std::max(t_host + st_ms, t_link) + pool.r_xa * abytes * dn;
       host_pack = done_p <= done_a;
-      t_host += (host_pack ? c_pack : c_stage) * dn;
+      t_host += host_pack ? hp_ms : st_ms;
       t_link = host_pack ? done_p : done_a;
     }
     s.packed_mode = host_pack;
@@ -376,7 +384,7 @@ extern "C" int32_t kfmi_search_stream(void* index, const char* ascii, uint64_t n
     }
     const double hms = since(th);
     host_ms += hms;
-    if (s.n && (host_pack || !pin_in)) ema(host_pack ? c_pack : c_stage, hms / s.n);
+    if (s.n && (host_pack || !pin_in)) ema(host_pack ? pool.r_pack : pool.r_stage, hms / (s.n * abytes));
     s.dq.device = di->device;
     s.dq.num = s.n;
     s.dq.size = size;
