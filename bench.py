@@ -194,6 +194,24 @@ def ingest_leg(idx, reads: np.ndarray, res: np.ndarray, world: int) -> dict:
             else:
                 qp = q2
         os.environ.pop("KFMI_LOAD_MMAP", None)
+        # the same file parsed on the device (kfmi_load_queries_gpu): file -> device reads
+        try:
+            rd = K.Results.alloc(n)
+            t = time.perf_counter()
+            qd = K.Queries.load_gpu(fn, m, n)
+            out["device_parse_load_s"] = round(time.perf_counter() - t, 3)
+            t = time.perf_counter()
+            K.transfer_to_gpu(idx, qd, rd)
+            K.search(idx, qd, rd)
+            K.transfer_to_cpu(rd)
+            tot_d = out["device_parse_load_s"] + time.perf_counter() - t
+            out["device_parse_total_s"] = round(tot_d, 3)
+            out["device_parse_mqps_file_to_results"] = round(n / tot_d / 1e6, 2)
+            out["device_parse_results_equal"] = bool(np.array_equal(rd.array(), res))
+            qd.close()
+            rd.close()
+        except K.KfmiError as e:
+            out["device_parse_error"] = str(e)
     r2 = K.Results.alloc(n)
     t = time.perf_counter()
     K.transfer_to_gpu(idx, qp, r2)

@@ -217,6 +217,14 @@ int32_t kfmi_count_blocks(void *index, void *queries, uint64_t *blocks);
  * Results equal kfmi_search's. */
 int32_t kfmi_search_stream(void *index, const char *ascii, uint64_t num, uint32_t size,
                            uint32_t *results, uint64_t chunk);
+/* loadQueries with the parsing on the device: the file is read
+ * in 64 MB pieces into pinned buffers (parallel pread) and DMA'd to the current
+ * device, where kernels find the read lines, check them and lay the first
+ * `numqueries` reads out as loadQueries would (0 = every read in the file);
+ * same format and errors as loadQueries.  The returned queries live on the
+ * device only (no host copy): transferCPUtoGPU uses them as they are (on the
+ * device they were loaded on; not for device groups). */
+int32_t kfmi_load_queries_gpu(const char *fn, uint32_t sizequery, uint64_t numqueries, void **queries);
 /* Packs num reads of `size` bases (plain layout q*size, as loadQueries keeps
  * them, common.c:163-173) into the 2-bit code words the search consumes, on the
  * host: word-major, word w of read q at words[w * num + q], ceil(size/16) words

@@ -207,6 +207,7 @@ int32_t group_transfer(kfmi_fmi_t* f, kfmi_qrys_t* q, kfmi_res_t* r, const int* 
   }
   if (q) {
     if (!f) return KFMI_E_BAD_ARGUMENT;
+    if (!q->h_queries && q->num) return KFMI_E_NOT_IMPLEMENTED;   /* device-parsed reads stay on their device */
     group_free_queries(q);
     if (q->dev) {
       free_dev_queries(q->dev);

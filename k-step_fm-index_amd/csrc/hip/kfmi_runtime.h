@@ -107,6 +107,7 @@ int32_t search_finish(hipStream_t st, hipEvent_t* ev, double* ms);
 /* host memory helpers (kfmi_stream.hip) */
 bool host_pinned(const void* p);
 void par_copy(void* dst, const void* src, uint64_t bytes);
+bool par_pread(int fd, void* dst, uint64_t off, uint64_t bytes);
 
 /* device groups (kfmi_group.hip) */
 constexpr int KFMI_MAX_GROUP = 16;

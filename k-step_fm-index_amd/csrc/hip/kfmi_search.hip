@@ -962,8 +962,16 @@ extern "C" int32_t transferCPUtoGPU(void* index, void* queries, void* results)
   }
   if (q) {
     if (!f) return KFMI_E_BAD_ARGUMENT;
-    err = upload_queries(q, f->steps, dev, ctx);
-    if (err) return err;
+    if (!q->h_queries && q->num) {   /* parsed on the device (kfmi_load_queries_gpu): already there */
+      if (!q->dev) return KFMI_E_NOT_ON_DEVICE;
+      if (q->dev->device != dev) return KFMI_E_BAD_ARGUMENT;
+      if (q->size % f->steps) return KFMI_E_BAD_ARGUMENT;   /* B6 */
+      q->dev->K = f->steps;
+      q->dev->steps = q->size / f->steps;
+    } else {
+      err = upload_queries(q, f->steps, dev, ctx);
+      if (err) return err;
+    }
   }
   if (r) {
     if (r->d_results) {

@@ -4,7 +4,9 @@
  */
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <functional>
@@ -238,6 +240,26 @@ void par_copy(void* dst, const void* src, uint64_t bytes)
     const uint64_t len = bytes - b < part ? bytes - b : part;
     memcpy((uint8_t*) dst + b, (const uint8_t*) src + b, len);
   });
+}
+
+/* pread of [off, off + bytes) of fd into dst, split over the host workers
+ * (page-cache reads run at memcpy speed per thread); false on a short read */
+bool par_pread(int fd, void* dst, uint64_t off, uint64_t bytes)
+{
+  HostPool& hp = HostPool::get();
+  const int nt = bytes < (4u << 20) ? 1 : hp.size();
+  const uint64_t part = ((bytes + nt - 1) / nt + 4095) & ~4095ull;
+  std::atomic<bool> ok{true};
+  hp.run(nt, [&](int t) {
+    uint64_t b = part * t;
+    const uint64_t e = b + part < bytes ? b + part : bytes;
+    while (b < e) {
+      const ssize_t r = pread(fd, (uint8_t*) dst + b, (size_t) (e - b), (off_t) (off + b));
+      if (r <= 0) { ok = false; return; }
+      b += (uint64_t) r;
+    }
+  });
+  return ok;
 }
 
 /* ASCII rows -> word-major code words of one chunk, over the host workers */

@@ -88,6 +88,7 @@ def load() -> ctypes.CDLL:
         "kfmi_transform_interleave": (i32, [vp, pvp]),
         "kfmi_transform_ac": (i32, [vp, pvp, pvp]),
         "kfmi_queries_from_buffer": (i32, [vp, u64, u32, pvp]),
+        "kfmi_load_queries_gpu": (i32, [ctypes.c_char_p, u32, u64, pvp]),
         "kfmi_results_alloc": (i32, [u64, pvp]),
         "kfmi_results_host": (ctypes.POINTER(ctypes.c_uint32), [vp]),
         "kfmi_results_num": (u64, [vp]),
@@ -319,6 +320,17 @@ class Queries(_Handle):
         p = ctypes.c_void_p()
         _check(load().loadQueries(str(path).encode(), size, num, ctypes.byref(p)), f"loadQueries {path}")
         return cls(p.value)
+
+    @classmethod
+    def load_gpu(cls, path, size: int, num: int = 0) -> "Queries":
+        """FASTA parsed on the device (kfmi_load_queries_gpu); num = 0: every read."""
+        p = ctypes.c_void_p()
+        _check(load().kfmi_load_queries_gpu(str(path).encode(), size, num, ctypes.byref(p)),
+               f"kfmi_load_queries_gpu {path}")
+        return cls(p.value)
+
+    def num(self) -> int:
+        return int(ctypes.c_uint64.from_address(self._p.value).value)
 
     def free_gpu(self) -> None:
         load().freeQueriesGPU(ctypes.byref(self._p))

@@ -92,3 +92,97 @@ def test_edge_cases_equal(kfmi_mod, tmp_path, monkeypatch, body, n, ok):
             assert isinstance(a, np.ndarray) and np.array_equal(a, b), (body, pad)
         else:
             assert a == b == 12, (body, pad, a, b)     # KFMI_E_READING_MFASTA_FILE
+
+
+# ---- device parse (kfmi_load_queries_gpu) -----------------------------------
+
+@pytest.fixture(scope="module")
+def gpu_idx(kfmi_mod):
+    K = kfmi_mod
+    if K.device_count() < 1:
+        pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
+    K.set_device(0)
+    rng = np.random.default_rng(9)
+    text = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=200_001).tobytes()
+    return K.Index.build(text, k=2, d=64, gpu=True), text
+
+
+def search_loaded(K, idx, q):
+    K.set_backend("task-mid")
+    r = K.Results.alloc(q.num())
+    K.transfer_to_gpu(idx, q, r)
+    K.search(idx, q, r)
+    K.transfer_to_cpu(r)
+    out = r.array().copy()
+    r.close()
+    return out
+
+
+@pytest.mark.gpu
+def test_gpu_parse_golden_and_large(kfmi_mod, gpu_idx, tmp_path):
+    K = kfmi_mod
+    idx, text = gpu_idx
+    for case, c in sorted(util.manifest().items()):
+        for m, qd in sorted(c["queries"].items()):
+            m = int(m)
+            if m % 2:
+                continue
+            path = util.GOLDEN / case / qd["file"]
+            q = K.Queries.load_gpu(path, m, qd["num"])
+            assert q.num() == qd["num"]
+            want = K.search_array(idx, util.read_qry(path, m), "task-mid")
+            assert np.array_equal(search_loaded(K, idx, q), want), (case, m)
+            q.close()
+    # 300K reads, ragged headers and CRLF, several 64 KiB tiles; all reads (num 0) and a prefix
+    rng = np.random.default_rng(4)
+    t = np.frombuffer(text, np.uint8)
+    reads = np.concatenate([t[rng.integers(0, len(t) - 150, size=250_000)[:, None] + np.arange(150)],
+                            rng.choice(np.frombuffer(b"ACGTNacgt", np.uint8), size=(50_000, 150))])
+    path = tmp_path / "q.fa"
+    with open(path, "wb") as f:
+        f.write(b"".join(b">r%d%s\n%s%s\n" % (j, b" x" * (j % 7), reads[j].tobytes(), b"\r" * (j % 3 == 0))
+                         for j in range(reads.shape[0])))
+    want = K.search_array(idx, reads, "task-mid")
+    q = K.Queries.load_gpu(path, 150)
+    assert q.num() == reads.shape[0]
+    assert np.array_equal(search_loaded(K, idx, q), want)
+    q.close()
+    q = K.Queries.load_gpu(path, 150, 12_345)
+    assert np.array_equal(search_loaded(K, idx, q), want[:2 * 12_345])
+    q.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("body,n,ok", [
+    (b">a\nACGT\n>b\nTTTT\n", 2, True),
+    (b">a\nACGT\n>b\nTTTT", 2, True),
+    (b"ACGT\nTTTT\nGGGG\n", 3, True),
+    (b">a\nACGT\n>b\nTTTT\n", 3, False),
+    (b">a\nACGT\n>b\nTTT\n", 2, False),
+    (b">a\nACGT\n>b\nTTTT\n>c\nTT\n", 2, True),
+    (b">a\nACGT\n\n>b\nTTTT\n", 2, False),
+    (b">a\r\nACGT\r\n>b\r\nTTTT\r\n", 2, True),
+    (b">\n>\nACGT\n", 1, True),
+    (b">a\nACGTA\n>b\nTTTT\n", 2, False),              # long line
+    (b">a\nAC\rT\n", 1, True),                         # '\r' inside the read is a base, as on the host
+])
+def test_gpu_parse_edge_cases_match_host(kfmi_mod, gpu_idx, tmp_path, body, n, ok):
+    K = kfmi_mod
+    idx, _ = gpu_idx
+    for pad in (0, 300_000):    # the read lines in the first tile, or after several
+        path = tmp_path / "e.fa"
+        path.write_bytes(b">pad\n" * (pad // 5) + body if pad else body)
+        try:
+            host = K.Queries.load(path, 4, n)
+        except K.KfmiError as e:
+            host = e.code
+        try:
+            dev = K.Queries.load_gpu(path, 4, n)
+        except K.KfmiError as e:
+            dev = e.code
+        if ok:
+            assert not isinstance(host, int) and not isinstance(dev, int), (body, pad, host, dev)
+            want = search_loaded(K, idx, host)
+            assert np.array_equal(search_loaded(K, idx, dev), want), (body, pad)
+        else:
+            assert host == dev == 12, (body, pad, host, dev)
