@@ -66,6 +66,9 @@ def parse():
                                          "task-packed,coop-packed,task-mid,coop-mid,task-mid+ftab14",
                    help="other backends timed on rank 0 at N=1 (empty = none)")
     p.add_argument("--variant-steps", type=int, default=3)
+    p.add_argument("--config5-queries", type=int, default=10_000_000,
+                   help="reads per GPU of the config #5 leg (0 = skip)")
+    p.add_argument("--config5-qlen", type=int, default=150)
     p.add_argument("--no-ingest", dest="ingest", action="store_false",
                    help="skip the FASTA file -> loadQueries -> search -> results leg (f2)")
     p.add_argument("--no-md5", action="store_true")
@@ -339,6 +342,47 @@ def config1_leg(backend: str, thr: int, steps: int = 5) -> dict:
     return out
 
 
+def config5_leg(D, idx, text: bytes, backend: str, qlen: int, nq: int, steps: int, warmup: int, ac: bool) -> dict:
+    """BASELINE config #5's read shape on every rank: this rank's shard of nq
+    reads of qlen bases (seed 20 + rank; 10M x 150 bp = one eighth of the
+    80M x 150 bp batch at N = 8), searched on the resident index; timed like
+    the main leg (barrier + synchronize, max over ranks), then an evenly spread
+    100 K-read sample of every rank checked against the CPU oracle."""
+    from oracle import oracle
+    reads = synth.gather_reads(text, synth.read_starts(len(text), nq, qlen, seed=20 + D.rank), qlen)
+    q = K.Queries.from_array(reads)
+    r = K.Results.alloc(nq)
+    K.set_backend(backend)
+    K.transfer_to_gpu(idx, q, r)
+    for _ in range(warmup):
+        K.search(idx, q, r)
+    D.barrier()
+    lf = []
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        K.search(idx, q, r)
+        lf.append(K.last_timing()["lf_ms"])
+    D.barrier()
+    el = D.max(time.perf_counter() - t0)
+    K.transfer_to_cpu(r)
+    res = r.array().copy()
+    sel = np.linspace(0, nq - 1, min(100_000, nq)).astype(np.int64)
+    img_idx = idx.alt_counters()[0] if ac else idx
+    want, _ = oracle.search(img_idx.image(), reads[sel], nthreads=max(1, cpu_effective() // D.world))
+    ok = bool(np.array_equal(want.reshape(-1, 2), res.reshape(-1, 2)[sel]))
+    if ac:
+        img_idx.close()
+    oks = D.gather(ok)
+    lfs = D.gather(round(float(np.mean(lf)), 4))
+    total = D.sum(float(nq))
+    q.close()
+    r.close()
+    return {"what": f"config #5 shape: {nq // 1_000_000}M x {qlen} bp reads per GPU (seed 20 + rank), "
+                    f"{D.world} GPU(s), index replicated",
+            "mqps": round(total * steps / el / 1e6, 2), "ms_per_step": round(el / steps * 1e3, 4),
+            "lf_ms_per_rank": lfs, "oracle_sample_ok_per_rank": oks, "oracle_sample_per_rank": int(sel.size)}
+
+
 def time_backend(idx, q, r, backend, steps, warmup):
     """`backend` may carry "+ftabN": the Bowtie-style jump-start table of N bases."""
     name, _, opt = backend.partition("+")
@@ -478,6 +522,15 @@ def main():
         except Exception:
             traffic = None
 
+    c5 = None
+    if a.config5_queries > 0:
+        try:
+            c5 = config5_leg(D, idx, text, a.backend, a.config5_qlen, a.config5_queries, a.steps, 5,
+                             a.backend in ("task-ac", "coop-ac", "task-ac128", "coop-ac128", "task-ac-mid",
+                                           "coop-ac-mid"))
+            log(f"rank {D.rank}: config #5 leg {c5}")
+        except K.KfmiError as e:
+            c5 = {"error": str(e)}
     ingest = None
     if a.ingest:
         try:
@@ -494,6 +547,8 @@ def main():
     ranks = aggregate_ranks(rank_rows)
 
     extra = {}
+    if c5 is not None:
+        extra["config5"] = c5
     if ingest is not None:
         extra["ingest_file"] = ingest          # rank 0's; every rank's is under "ranks"
     cpu = None
