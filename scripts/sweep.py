@@ -41,6 +41,10 @@ def main():
     p.add_argument("--sort-suffix", default="0",
                    help="experiment: comma list of N; order reads by their last N bases (backward-search "
                         "order, N <= 32), one pass over the backends per N")
+    p.add_argument("--xcd-tiles", default="",
+                   help="experiment: comma list of bucket counts B; reads grouped by their last 2*ceil(log4 B)... "
+                        "bases into B buckets and laid out so that 256-read tile i holds bucket i % B "
+                        "(with round-robin workgroup dispatch, XCD x then sees only buckets = x mod 8)")
     a = p.parse_args()
 
     K.load()
@@ -59,10 +63,25 @@ def main():
         var, vals = spec.split("=")
         knobs = [dict(k, **{var: v}) for k in knobs for v in vals.split(",")]
     ref = None
-    for ss in [int(x) for x in a.sort_suffix.split(",")]:
+    plans = [("sort", int(x)) for x in a.sort_suffix.split(",")] + \
+            [("xcd", int(x)) for x in a.xcd_tiles.split(",") if x]
+    for kind, ss in plans:
         inv = None
         reads = reads0
-        if ss:
+        if kind == "xcd":
+            codes = ((reads0[:, -3:] >> 1) & 3).astype(np.int64)       # last 3 bases, a bijection per base
+            key = codes[:, 2] * 16 + codes[:, 1] * 4 + codes[:, 0]      # 64 suffix classes
+            bucket = key % ss
+            per = [np.flatnonzero(bucket == b) for b in range(ss)]
+            ntile = max((x.size + 255) // 256 for x in per)
+            order = [per[bk][256 * r:256 * (r + 1)] for r in range(ntile) for bk in range(ss)]
+            order = np.concatenate(order)
+            assert order.size == reads0.shape[0], (order.size, reads0.shape[0])
+            reads = np.ascontiguousarray(reads0[order])
+            inv = np.empty_like(order)
+            inv[order] = np.arange(order.size)
+            log(f"reads laid out in 256-read tiles of {ss} suffix buckets")
+        elif ss:
             # key: code of base m-1 most significant, then m-2, ... (the order the
             # backward search consumes them), so reads sharing their last j bases
             # are contiguous for every j <= ss
@@ -99,12 +118,12 @@ def main():
                         res = res.reshape(-1, 2)[inv].reshape(-1)
                     if ref is None:
                         ref = res
-                    out = {"backend": b, "knobs": kn, "sort_suffix": ss, "lf_ms": round(float(np.median(lf)), 3),
+                    out = {"backend": b, "knobs": kn, "order": kind, "sort_suffix": ss, "lf_ms": round(float(np.median(lf)), 3),
                            "lf_ms_min": round(float(np.min(lf)), 3), "step_ms": round(float(np.median(tot)), 3),
                            "wall_ms": round(wall * 1e3, 3), "mqps": round(reads.shape[0] / wall / 1e6, 1),
                            "equal": bool(np.array_equal(res, ref)), "dev_bytes": idx.device_bytes()}
                 except K.KfmiError as e:
-                    out = {"backend": b, "knobs": kn, "sort_suffix": ss, "error": str(e)}
+                    out = {"backend": b, "knobs": kn, "order": kind, "sort_suffix": ss, "error": str(e)}
                 print(json.dumps(out), flush=True)
                 log(out)
                 for var in kn:
