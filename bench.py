@@ -320,6 +320,41 @@ def cpu_reference_baseline(idx, reads, ns, k, d, thr, res_gpu):
     return best
 
 
+def probe_leg() -> dict | None:
+    """The random-line request ceiling on this box, measured beside the kernel:
+    bin/gather_probe (csrc/tools/gather_probe.hip) reads uniformly random lines
+    of a 3 GB table -- independent per lane, cooperative, and dependent chains
+    (the LF shape) -- and reports lines/s.  Run as a child process while this
+    one idles.  None when the tool is missing or fails."""
+    import subprocess
+    exe = ROOT / "k-step_fm-index_amd" / "bin" / "gather_probe"
+    if not exe.exists():
+        return None
+    try:
+        p = subprocess.run([str(exe), "3", "512"], capture_output=True, text=True, timeout=300)
+    except (OSError, subprocess.SubprocessError):
+        return None
+    if p.returncode != 0:
+        return None
+    rows, table = [], None
+    for ln in p.stdout.splitlines():
+        try:
+            d = json.loads(ln)
+        except ValueError:
+            continue
+        if "table_bytes" in d:
+            table = d["table_bytes"]
+        elif "kind" in d and table == 3_000_000_000:
+            rows.append(d)
+    if not rows:
+        return None
+    best = max(rows, key=lambda x: x["Glines_s"])
+    chain = [x for x in rows if x["kind"].startswith("chain")]
+    return {"best_G_lines_per_s": best["Glines_s"], "best_kind": f"{best['kind']} {best['line_B']} B",
+            "chain_G_lines_per_s": max(x["Glines_s"] for x in chain) if chain else None,
+            "table_bytes": 3_000_000_000, "rows": rows}
+
+
 def config1_leg(backend: str, thr: int, steps: int = 5) -> dict:
     """BASELINE config #1 (64 Mbase recipe text, 2^20 x 100 bp reads): GPU
     search rate on the md5-pinned inputs and the reference's CPU searcher on
@@ -547,6 +582,10 @@ def main():
     ranks = aggregate_ranks(rank_rows)
 
     extra = {}
+    probe = probe_leg() if D.world == 1 and D.rank == 0 else None
+    if probe:
+        extra["line_request_probe"] = probe
+        log(f"gather probe: best {probe['best_G_lines_per_s']} G lines/s ({probe['best_kind']})")
     if c5 is not None:
         extra["config5"] = c5
     if ingest is not None:
@@ -730,7 +769,12 @@ def main():
                          # requests, calibrated by gather_probe on the same 3 GB table size
                          # (profiles/r01/gather_probe_table_size.txt, per-lane 64-B lines)
                          "line_requests_G_per_s": round(rdreq / (lf_avg_ms / 1e3) / 1e9, 2) if rdreq else None,
-                         "line_request_ceiling_G_per_s": PROBE_CEILING_GLINES},
+                         "line_request_ceiling_G_per_s": probe["best_G_lines_per_s"] if probe else PROBE_CEILING_GLINES,
+                         "line_request_ceiling_source": "gather_probe on this box, this run" if probe else
+                         "profiles/r01/gather_probe_table_size.txt (another box)",
+                         "line_request_frac": round(rdreq / (lf_avg_ms / 1e3) / 1e9 /
+                                                    (probe["best_G_lines_per_s"] if probe else PROBE_CEILING_GLINES), 3)
+                         if rdreq else None},
             "cpu_baseline": cpu,
             "parity": {"index_md5_pinned": index_md5_ok, "results_md5_pinned": results_md5_ok,
                        "oracle_sample_ok": ranks["parity_ok_all"], "oracle_sample_per_rank": int(ns_par)},
