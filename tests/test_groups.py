@@ -56,7 +56,7 @@ def run_trio(K, idx, reads):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("backend", ["task-mid", "coop-mid", "task", "coop-ac", "task-ac128"])
+@pytest.mark.parametrize("backend", ["task-mid", "coop-mid", "task", "coop-ac", "task-ac128", "task-ac-mid"])
 @pytest.mark.parametrize("group", [[0, 0], [0, 0, 0]])
 @pytest.mark.parametrize("num", [3_333, 130, 64, 1, 0])
 def test_group_equals_single_device(setup, backend, group, num):
@@ -157,3 +157,31 @@ def test_group_replication_setup_time(kfmi_mod):
         K.set_devices([])
         idx.free_gpu()
         idx.close()
+
+
+@pytest.mark.gpu
+def test_group_rejects_device_parsed_queries(setup, tmp_path):
+    """Reads parsed on the device (kfmi_load_queries_gpu) live on that device
+    only: a device group refuses them (KFMI_E_NOT_IMPLEMENTED) instead of
+    uploading an empty host copy; single-device mode takes them as they are."""
+    K, idx, reads = setup
+    path = tmp_path / "q.fa"
+    path.write_bytes(b"".join(b">r\n" + r.tobytes() + b"\n" for r in reads[:500]))
+    K.set_backend("task-mid")
+    q = K.Queries.load_gpu(path, 100)
+    r = K.Results.alloc(500)
+    try:
+        K.set_devices([0, 0])
+        with pytest.raises(K.KfmiError) as e:
+            K.transfer_to_gpu(idx, q, r)
+        assert e.value.code == 19
+        K.set_devices([])
+        K.transfer_to_gpu(idx, q, r)
+        K.search(idx, q, r)
+        K.transfer_to_cpu(r)
+        assert np.array_equal(r.array(), K.search_array(idx, reads[:500]))
+    finally:
+        K.set_devices([])
+        idx.free_gpu()
+        q.close()
+        r.close()
