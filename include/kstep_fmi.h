@@ -118,6 +118,9 @@ char    *errorCommon(int32_t e);
  *   "task-mid"    task-per-query on the MID128 layout: one 128-byte line per LF (tag 101 semantics)
  *   "coop-mid"    wave64 cooperative gather on the MID128 layout              (tag 101 semantics)
  *   "task-ac128" / "coop-ac128"  one 128-byte line per block, both AC counters (tag 201 semantics)
+ *   "task-grp" / "coop-grp"   K = 4 indexes (d = 64): one 128-byte line per (block, 16-code
+ *                 group) holding the block's planes and those 16 counters -- one line per LF,
+ *                 25 K-steps for 100 bases; 16 x the index memory (tag 101 semantics)
  *   "task-ac-mid" / "coop-ac-mid" the MID128 lines with AltCounters semantics: the AltCounters
  *                 step only past the last real block, from the tfmiAC sentinel (tag 201 semantics;
  *                 built from a tag 100/101 file, an AC file returns 101)

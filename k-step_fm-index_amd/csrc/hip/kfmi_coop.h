@@ -19,6 +19,8 @@
 #ifndef KFMI_COOP_H_
 #define KFMI_COOP_H_
 
+#include <type_traits>
+
 #include "kfmi_device.h"
 
 namespace kfmi {
@@ -30,7 +32,8 @@ struct CoopCfg {
   static constexpr int RPR = 64 / TPR;                  // requests per round
   static constexpr int SLOT = TPR * 16;                 // LDS bytes per request slot
   static constexpr int MAXREQ = 128;                    // 64 L + up to 64 R
-  static constexpr int WAVE_LDS = MAXREQ * SLOT + MAXREQ * 4;
+  using Desc = typename std::conditional<(G::NC > 16), uint64_t, uint32_t>::type;   // b * NC + c
+  static constexpr int WAVE_LDS = MAXREQ * SLOT + MAXREQ * (int) sizeof(Desc);
   static constexpr int WPB0 = 65536 / WAVE_LDS;
   static constexpr int WPB = WPB0 < 1 ? 1 : (WPB0 > 4 ? 4 : WPB0);   // waves per block
   static constexpr bool OK = (G::BMW % 4 == 0) && (G::EW % 4 == 0) && (G::BOFF % 4 == 0) &&
@@ -49,6 +52,11 @@ __device__ __forceinline__ const uint8_t* coop_chunk_addr(const IdxArgs& ix, uin
     const uint64_t lb = (uint64_t) (b >> 1) * (G::EW * 4);
     if (k < C::BC) return base + lb + ((b & 1u) * G::BMW + 4 * k) * 4;
     return base + lb + (G::MIDCNT + (c & ~3u)) * 4;
+  }
+  if constexpr (G::LAY == LAY_GRP) {
+    const uint64_t lb = ((uint64_t) b * G::NGRP + c / G::NCG) * (G::EW * 4);
+    if (k < C::BC) return base + lb + 16 * k;
+    return base + lb + (G::BMW + ((c % G::NCG) & ~3u)) * 4;
   }
   if constexpr (G::LAY == LAY_AC128) {
     if (k < C::BC) return base + eb + 4 * k * 4;
@@ -76,19 +84,34 @@ __device__ __forceinline__ uint32_t coop_lf(const IdxArgs& ix, const uint8_t* sl
   if constexpr (G::ACRULE) e = ((b & 1u) != 0) == (c < (uint32_t) G::HALF);
   if constexpr (G::MIDLINES) e = (b & 1u) == 0;
   uint32_t pop = 0, all = 0;
+  if constexpr (G::PW <= 4) {
 #pragma unroll
-  for (int k = 0; k < C::BC; ++k) {
-    const uint4 v = *reinterpret_cast<const uint4*>(slot + 16 * k);
-    const uint32_t pl[4] = {v.x, v.y, v.z, v.w};
-    // K=2: one 32-row word per chunk; K=1: two words per chunk
+    for (int k = 0; k < C::BC; ++k) {
+      const uint4 v = *reinterpret_cast<const uint4*>(slot + 16 * k);
+      const uint32_t pl[4] = {v.x, v.y, v.z, v.w};
+      // K=2: one 32-row word per chunk; K=1: two words per chunk
 #pragma unroll
-    for (int h = 0; h < 4 / G::PW; ++h) {
-      const int w = k * (4 / G::PW) + h;
+      for (int h = 0; h < 4 / G::PW; ++h) {
+        const int w = k * (4 / G::PW) + h;
+        uint32_t m = row_mask(o - 32 * w);
+        if constexpr (G::TWO_SIDED) m = e ? ~m : m;
+        const uint32_t sel = select_rows<G::K>(&pl[h * G::PW], sx);
+        pop += __popc(m & sel);
+        if constexpr (G::LAY == LAY_MIDAC) all += __popc(sel);
+      }
+    }
+  } else {   // K > 2: one 32-row word spans PW / 4 chunks
+#pragma unroll
+    for (int w = 0; w < G::NB; ++w) {
+      uint32_t pl[G::PW];
+#pragma unroll
+      for (int k = 0; k < G::PW / 4; ++k) {
+        const uint4 v = *reinterpret_cast<const uint4*>(slot + 16 * (w * (G::PW / 4) + k));
+        pl[4 * k] = v.x; pl[4 * k + 1] = v.y; pl[4 * k + 2] = v.z; pl[4 * k + 3] = v.w;
+      }
       uint32_t m = row_mask(o - 32 * w);
       if constexpr (G::TWO_SIDED) m = e ? ~m : m;
-      const uint32_t sel = select_rows<G::K>(&pl[h * G::PW], sx);
-      pop += __popc(m & sel);
-      if constexpr (G::LAY == LAY_MIDAC) all += __popc(sel);
+      pop += __popc(m & select_rows<G::K>(pl, sx));
     }
   }
   uint32_t cnt;
@@ -129,7 +152,8 @@ __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, 
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   uint8_t* wl = lds + wave * C::WAVE_LDS;
-  uint32_t* tab = reinterpret_cast<uint32_t*>(wl + C::MAXREQ * C::SLOT);
+  using Desc = typename C::Desc;
+  Desc* tab = reinterpret_cast<Desc*>(wl + C::MAXREQ * C::SLOT);
   const uint64_t q0 = ((uint64_t) blockIdx.x * C::WPB + wave) * 64;
   if (q0 >= num) return;                       // whole wave idle (wave-uniform)
   const uint64_t q = q0 + lane;
@@ -189,8 +213,8 @@ __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, 
       const uint32_t nreq = 64u + (uint32_t) __popcll(mask);
       const uint32_t slotR = 64u + __builtin_amdgcn_mbcnt_hi((uint32_t) (mask >> 32),
                                                              __builtin_amdgcn_mbcnt_lo((uint32_t) mask, 0u));
-      tab[lane] = bl * (uint32_t) G::NC + c;
-      if (needR) tab[slotR] = br * (uint32_t) G::NC + c;
+      tab[lane] = (Desc) bl * (Desc) G::NC + c;
+      if (needR) tab[slotR] = (Desc) br * (Desc) G::NC + c;
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       uint32_t sbL = 0, sbR = 0;
       if constexpr (G::LAY == LAY_PACKED) {
@@ -201,8 +225,8 @@ __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, 
       for (uint32_t r = 0; r < rounds; ++r) {
         const uint32_t s = r * C::RPR + g;
         if (s < nreq && k <= C::BC) {
-          const uint32_t desc = tab[s];
-          const uint32_t b = desc / (uint32_t) G::NC, cc = desc % (uint32_t) G::NC;
+          const Desc desc = tab[s];
+          const uint32_t b = (uint32_t) (desc / (Desc) G::NC), cc = (uint32_t) (desc % (Desc) G::NC);
           const uint8_t* src = coop_chunk_addr<G>(ix, b, cc, k);
           __builtin_amdgcn_global_load_lds((const void*) src,
                                            (__attribute__((address_space(3))) void*) (wl + r * 1024), 16, 0, 0);

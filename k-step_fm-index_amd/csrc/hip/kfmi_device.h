@@ -30,6 +30,12 @@
  *                of block E-1 counted as their stored code, padding as A);
  *                blocks >= E-1 take that formula with the AC counters of
  *                entries E-1, E, E+1 (ix.ac_tail), everything else is LAY_MID.
+ *   LAY_GRP    : K = 4 (256 counters per block): one power-of-two line per
+ *                (d-block, group of 16 codes), [planes of block b | cnt_b[16g ..
+ *                16g+15]], the planes repeated in the block's 16 lines.  K=4,
+ *                d=64: 64 B of planes + 64 B of counters = one 128-B line per
+ *                LF, 25 K-steps for a 100-bp read instead of 50 -- in 16 x
+ *                the index memory (96 GB at 3 Gbase, which one MI355X holds).
  *   LAY_AC128  : tag-201 (AltCounters) semantics, one power-of-two line per
  *                d-block: [planes of block b | cnt_half_b | cnt_half_{b+1}],
  *                so both counters the AC rule may pick (entry b or b+1,
@@ -44,7 +50,8 @@
 
 namespace kfmi {
 
-enum Layout : int { LAY_INTER = 0, LAY_AC = 1, LAY_PACKED = 2, LAY_MID = 3, LAY_AC128 = 4, LAY_MIDAC = 5 };
+enum Layout : int { LAY_INTER = 0, LAY_AC = 1, LAY_PACKED = 2, LAY_MID = 3, LAY_AC128 = 4, LAY_MIDAC = 5,
+                    LAY_GRP = 6 };
 
 __host__ __device__ constexpr int pow2ceil(int x) { int p = 1; while (p < x) p <<= 1; return p; }
 
@@ -59,10 +66,13 @@ struct Geo {
   static constexpr int PW = 2 * K;               // planes per 32-row word
   static constexpr int BMW = PW * NB;            // bitmap words per block
   // u32 words per entry (per line for LAY_MID)
+  static constexpr int NCG = NC < 16 ? NC : 16;          // counters per line (LAY_GRP)
+  static constexpr int NGRP = NC / NCG;                   // lines per block (LAY_GRP)
   static constexpr int EW = LAY == LAY_INTER ? BMW + NC
                           : LAY == LAY_AC    ? HALF + BMW
                           : LAY == LAY_PACKED ? pow2ceil(BMW + NC / 2)
                           : LAY == LAY_AC128  ? pow2ceil(BMW + NC)
+                          : LAY == LAY_GRP    ? pow2ceil(BMW + NCG)
                           : pow2ceil(2 * BMW + NC);
   static constexpr int BOFF = LAY == LAY_AC ? HALF : 0;   // first bitmap word
   static constexpr int DELTA16 = 2 * BMW;                 // first u16 delta (packed)
@@ -83,9 +93,9 @@ __host__ __device__ constexpr int sb_shift_for(int d)
 }
 
 struct DollarArgs {
-  uint32_t dpos[2];   // dollarPositionBWT[s]
-  uint32_t dbase[2];  // dollarBaseBWT[s]
-  uint32_t dblk[2];   // dollarPositionBWT[s] / d (modposdollarBWT)
+  uint32_t dpos[4];   // dollarPositionBWT[s], s < K <= 4
+  uint32_t dbase[4];  // dollarBaseBWT[s]
+  uint32_t dblk[4];   // dollarPositionBWT[s] / d (modposdollarBWT)
 };
 
 struct IdxArgs {
@@ -282,6 +292,11 @@ __device__ __forceinline__ Where<G> locate(const IdxArgs& ix, uint32_t b, uint32
     const uint32_t* ent = ix.ent + (uint64_t) b * G::EW;
     w.planes = ent;
     w.cnt = nullptr;
+    w.e = false;
+  } else if constexpr (G::LAY == LAY_GRP) {
+    const uint32_t* line = ix.ent + ((uint64_t) b * G::NGRP + c / G::NCG) * G::EW;
+    w.planes = line;
+    w.cnt = line + G::BMW + c % G::NCG;
     w.e = false;
   } else {   // LAY_MID, LAY_MIDAC
     const uint32_t* line = ix.ent + (uint64_t) (b >> 1) * G::EW;

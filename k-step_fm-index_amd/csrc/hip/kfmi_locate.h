@@ -73,13 +73,15 @@ __global__ __launch_bounds__(256) void locate_kernel(IdxArgs ix, const uint32_t*
   uint32_t steps = 0;
   for (;;) {   // a lane leaves once all its slots are done
     const bool smp = (r & mask) == 0u;
-    const bool d0 = r == ix.dl.dpos[0];
-    const bool d1 = G::K > 1 && r == ix.dl.dpos[1];
+    int ds = -1;   /* r = D_s (SA = s): the walk cannot step past it */
+#pragma unroll
+    for (int s = G::K - 1; s >= 0; --s)
+      if (r == ix.dl.dpos[s]) ds = s;
     uint32_t p = 0, nr = 0;
     if (smp) p = sa[r >> rate_log2];
-    else if (!d0 && !d1) nr = lf_row<G>(ix, r);
-    if (smp || d0 || d1) {
-      pos[i] = (smp ? p : (d0 ? 0u : 1u)) + steps;
+    else if (ds < 0) nr = lf_row<G>(ix, r);
+    if (smp || ds >= 0) {
+      pos[i] = (smp ? p : (uint32_t) ds) + steps;
       i += stride;
       if (i >= total) break;
       r = r_next;

@@ -36,7 +36,7 @@ namespace kfmi {
 
 static const char* kBackendNames[KFMI_BK_COUNT] = {
     "task", "coop", "task-ac", "coop-ac", "task-packed", "coop-packed", "task-mid", "coop-mid",
-    "task-ac128", "coop-ac128", "task-ac-mid", "coop-ac-mid"};
+    "task-ac128", "coop-ac128", "task-ac-mid", "coop-ac-mid", "task-grp", "coop-grp"};
 
 static thread_local int t_backend = -1;
 thread_local int t_device = -1;
@@ -273,6 +273,24 @@ __global__ __launch_bounds__(256) void build_mid_kernel(const uint32_t* __restri
   for (int i = GM::MIDCNT + GI::NC; i < GM::EW; ++i) dst[i] = 0;
 }
 
+/* GRP layout construction from tag-101 entries (plus the padding entry with
+ * the end counters): line b * NGRP + g = [planes of entry b | cnt_b[NCG g ..]]. */
+template <int K, int NB>
+__global__ __launch_bounds__(256) void build_grp_kernel(const uint32_t* __restrict__ inter, uint64_t nlines,
+                                                        uint32_t* __restrict__ lines)
+{
+  using GI = Geo<K, NB, LAY_INTER>;
+  using GG = Geo<K, NB, LAY_GRP>;
+  const uint64_t l = (uint64_t) blockIdx.x * 256 + threadIdx.x;
+  if (l >= nlines) return;
+  const uint64_t b = l / GG::NGRP, g = l % GG::NGRP;
+  const uint32_t* src = inter + b * GI::EW;
+  uint32_t* dst = lines + l * GG::EW;
+  for (int i = 0; i < GI::BMW; ++i) dst[i] = src[i];
+  for (int c = 0; c < GG::NCG; ++c) dst[GI::BMW + c] = src[GI::BMW + g * GG::NCG + c];
+  for (int i = GI::BMW + GG::NCG; i < GG::EW; ++i) dst[i] = 0;
+}
+
 /* AC128 layout construction from tag-201 entries (E + 1 of them, the last
  * being the sentinel): line b = [planes of b | cnt_half_b | cnt_half_{b+1}],
  * the counters of entries past the sentinel read as 0 (as the AC backend's
@@ -325,6 +343,7 @@ KFMI_FOR_NB(KFMI_EXTERN, 1, LAY_AC128)
 KFMI_FOR_NB(KFMI_EXTERN, 2, LAY_AC128)
 KFMI_FOR_NB(KFMI_EXTERN, 1, LAY_MIDAC)
 KFMI_FOR_NB(KFMI_EXTERN, 2, LAY_MIDAC)
+KFMI_EXTERN(4, 2, LAY_GRP)
 
 hipError_t dispatch(Op op, uint32_t K, uint32_t nb, int lay, const SearchLaunch& a, unsigned long long* d_total)
 {
@@ -342,14 +361,21 @@ hipError_t dispatch(Op op, uint32_t K, uint32_t nb, int lay, const SearchLaunch&
   KFMI_FOR_NB(KFMI_CASE, 2, LAY_AC128)
   KFMI_FOR_NB(KFMI_CASE, 1, LAY_MIDAC)
   KFMI_FOR_NB(KFMI_CASE, 2, LAY_MIDAC)
+  KFMI_CASE(4, 2, LAY_GRP)
 #undef KFMI_CASE
   return hipErrorInvalidValue;
 }
+
+bool is_coop(int backend);
 
 /* Whether the backend's kernel exists for this geometry (the cooperative
  * kernel needs 16-byte-aligned chunks, CoopCfg::OK). */
 static bool geometry_supported(int backend, uint32_t K, uint32_t nb, int lay)
 {
+  if (lay == LAY_GRP) {   /* instantiated for K = 4, d = 64 only (K <= 2 has the MID128 lines) */
+    if (K != 4 || nb != 2) return false;
+    return !is_coop(backend) || CoopCfg<Geo<4, 2, LAY_GRP>>::OK;
+  }
   if (!nb_supported(nb) || (K != 1 && K != 2)) return false;
   if (!is_coop(backend)) return true;
 #define KFMI_OKC(KK, NBV, LAYV) \
@@ -418,6 +444,15 @@ static hipError_t dispatch_build_ac128(uint32_t K, uint32_t nb, const uint32_t* 
   return hipErrorInvalidValue;
 }
 
+static hipError_t dispatch_build_grp(uint32_t K, uint32_t nb, const uint32_t* inter, uint64_t nlines, uint32_t* lines,
+                                     hipStream_t st)
+{
+  if (K != 4 || nb != 2) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((build_grp_kernel<4, 2>), dim3((uint32_t) ((nlines + 255) / 256)), dim3(256), 0, st, inter, nlines,
+                     lines);
+  return hipGetLastError();
+}
+
 static int layout_of(int backend)
 {
   switch (backend) {
@@ -425,6 +460,7 @@ static int layout_of(int backend)
     case KFMI_BK_TASK_AC: case KFMI_BK_COOP_AC: return LAY_AC;
     case KFMI_BK_TASK_MID: case KFMI_BK_COOP_MID: return LAY_MID;
     case KFMI_BK_TASK_AC_MID: case KFMI_BK_COOP_AC_MID: return LAY_MIDAC;
+    case KFMI_BK_TASK_GRP: case KFMI_BK_COOP_GRP: return LAY_GRP;
     case KFMI_BK_TASK_AC128: case KFMI_BK_COOP_AC128: return LAY_AC128;
     default: return LAY_PACKED;
   }
@@ -433,7 +469,8 @@ static int layout_of(int backend)
 bool is_coop(int backend)
 {
   return backend == KFMI_BK_COOP || backend == KFMI_BK_COOP_AC || backend == KFMI_BK_COOP_PACKED ||
-         backend == KFMI_BK_COOP_MID || backend == KFMI_BK_COOP_AC128 || backend == KFMI_BK_COOP_AC_MID;
+         backend == KFMI_BK_COOP_MID || backend == KFMI_BK_COOP_AC128 || backend == KFMI_BK_COOP_AC_MID ||
+         backend == KFMI_BK_COOP_GRP;
 }
 
 /* ------------------------------------------------------------------------ */
@@ -476,7 +513,7 @@ static int32_t host_entries_for(const kfmi_fmi_t* f, int lay, kfmi_fmi_t** owned
 {
   *owned = nullptr;
   *use = f;
-  if (lay == LAY_INTER || lay == LAY_PACKED || lay == LAY_MID || lay == LAY_MIDAC) {
+  if (lay == LAY_INTER || lay == LAY_PACKED || lay == LAY_MID || lay == LAY_MIDAC || lay == LAY_GRP) {
     /* tag 101 as is; tag 100 is interleaved on the device (upload_entries),
      * or on the host with KFMI_HOST_INTERLEAVE=1 (A/B experiment) */
     if (f->tag == 100 && getenv("KFMI_HOST_INTERLEAVE") && atoi(getenv("KFMI_HOST_INTERLEAVE"))) {
@@ -581,7 +618,7 @@ hipError_t h2d(void* dst, const void* src, uint64_t bytes, hipStream_t st)
 /* tag-100 -> tag-101 entries (kfmi_transform_interleave's plane order,
  * transformIndexBitmaps.c) on the device: out word p of an entry is in word
  * perm[p] of the same entry. */
-constexpr uint32_t KFMI_MAX_ENTRY_WORDS = 160;   /* K <= 2, d <= 960: 2*30*2 + 16 = 136 */
+constexpr uint32_t KFMI_MAX_ENTRY_WORDS = 320;   /* K <= 2, d <= 960: 2*30*2 + 16 = 136; K = 4, d = 64: 272 */
 struct EntryPerm {
   uint32_t p[KFMI_MAX_ENTRY_WORDS];
 };
@@ -662,7 +699,7 @@ int32_t upload_sa(const kfmi_fmi_t* f, kfmi_dev_index* di, DevCtx* ctx)
 /* Uploads f for `backend` to `dev`: into f->dev, or into *out (group replicas). */
 int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx, kfmi_dev_index** out)
 {
-  if (f->steps < 1 || f->steps > 2) return KFMI_E_BAD_ARGUMENT;   /* GPU kernels: K in {1,2} */
+  if (f->steps < 1 || f->steps > 4) return KFMI_E_BAD_ARGUMENT;   /* GPU kernels: K in {1,2}; 4 on LAY_GRP */
   if (!nb_supported(f->nbitmaps)) return KFMI_E_BAD_ARGUMENT;
   const int lay = layout_of(backend);
   if (!geometry_supported(backend, f->steps, f->nbitmaps, lay)) return KFMI_E_BAD_ARGUMENT;
@@ -684,7 +721,7 @@ int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx, kfmi_dev_
   di->nb = f->nbitmaps;
   di->bwtsize = f->bwtsize;
   di->nentries = src->nentries;
-  for (uint32_t s = 0; s < 2; ++s) {
+  for (uint32_t s = 0; s < 4; ++s) {
     di->dl.dpos[s] = s < f->steps ? f->dollarPositionBWT[s] : 0xFFFFFFFFu;
     di->dl.dbase[s] = s < f->steps ? f->dollarBaseBWT[s] : 0xFFFFFFFFu;
     di->dl.dblk[s] = s < f->steps ? f->dollarPositionBWT[s] / f->chunk : 0xFFFFFFFFu;
@@ -710,6 +747,28 @@ int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx, kfmi_dev_
             hipSuccess ||
         hipStreamSynchronize(ctx->st) != hipSuccess)
       return fail(KFMI_E_KERNEL);
+  } else if (lay == LAY_GRP) {
+    /* NGRP lines per block (planes repeated, one counter group each), built on
+     * the device from the tag-101 entries plus one padding entry carrying the
+     * end counters (B5: R/d == nentries) */
+    const uint32_t ngrp = nc < 16 ? 1u : nc / 16;
+    const uint32_t lw = (uint32_t) pow2ceil((int) (2 * f->nbitmaps * f->steps + (nc < 16 ? nc : 16)));
+    const uint64_t nlines = (uint64_t) (src->nentries + 1) * ngrp;
+    end_counters(src, pad.data() + 2 * f->nbitmaps * f->steps);
+    uint32_t* tmp = nullptr;
+    di->ent_bytes = 4ull * lw * nlines;
+    if (hipMalloc((void**) &tmp, body + 4ull * ew) != hipSuccess) return fail(KFMI_E_DEVICE_ALLOC);
+    if (hipMalloc((void**) &di->ent, di->ent_bytes) != hipSuccess) {
+      (void) hipFree(tmp);
+      return fail(KFMI_E_DEVICE_ALLOC);
+    }
+    bool ok = upload_entries(tmp, src, body, ctx->st) == hipSuccess &&
+              hipMemcpyAsync((uint8_t*) tmp + body, pad.data(), 4ull * ew, hipMemcpyHostToDevice, ctx->st) ==
+                  hipSuccess &&
+              dispatch_build_grp(f->steps, f->nbitmaps, tmp, nlines, di->ent, ctx->st) == hipSuccess &&
+              hipStreamSynchronize(ctx->st) == hipSuccess;
+    (void) hipFree(tmp);
+    if (!ok) return fail(KFMI_E_KERNEL);
   } else if (lay == LAY_AC128) {
     /* one line per tag-201 entry (sentinel included) + one padding line, built on
      * the device from the entries; padding entry b+1 of the sentinel reads 0 */
@@ -926,6 +985,9 @@ hipError_t launch_pack(const kfmi_dev_queries* dq, hipStream_t st)
   const size_t lds = (size_t) tq * dq->size + 16;
   if (dq->K == 1)
     hipLaunchKernelGGL((pack_queries_kernel<1>), dim3((uint32_t) blocks), dim3(256), lds, st, dq->ascii, dq->num,
+                       dq->size, dq->steps, dq->nwords, tq, dq->packed);
+  else if (dq->K == 4)
+    hipLaunchKernelGGL((pack_queries_kernel<4>), dim3((uint32_t) blocks), dim3(256), lds, st, dq->ascii, dq->num,
                        dq->size, dq->steps, dq->nwords, tq, dq->packed);
   else
     hipLaunchKernelGGL((pack_queries_kernel<2>), dim3((uint32_t) blocks), dim3(256), lds, st, dq->ascii, dq->num,

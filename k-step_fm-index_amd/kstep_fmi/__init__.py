@@ -21,10 +21,11 @@ LIB_PATH = PKG_DIR / "lib" / "libkstepfmi.so"
 BIN_DIR = PKG_DIR / "bin"
 
 BACKENDS = ("task", "coop", "task-ac", "coop-ac", "task-packed", "coop-packed", "task-mid", "coop-mid",
-            "task-ac128", "coop-ac128", "task-ac-mid", "coop-ac-mid")
+            "task-ac128", "coop-ac128", "task-ac-mid", "coop-ac-mid", "task-grp", "coop-grp")
 BACKEND_TAG = {"task": 101, "coop": 101, "task-ac": 201, "coop-ac": 201,
                "task-packed": 101, "coop-packed": 101, "task-mid": 101, "coop-mid": 101,
-               "task-ac128": 201, "coop-ac128": 201, "task-ac-mid": 201, "coop-ac-mid": 201}
+               "task-ac128": 201, "coop-ac128": 201, "task-ac-mid": 201, "coop-ac-mid": 201,
+               "task-grp": 101, "coop-grp": 101}
 
 _lib = None
 

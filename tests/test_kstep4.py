@@ -1,0 +1,161 @@
+"""K = 4 (the reference's K_STEPS is generic, genFMindex.c:29-56 and
+fmIndexCPUBaseline.c:30-41; its GPU files stop at K = 2): the grouped-counter
+backends task-grp / coop-grp (LAY_GRP).
+
+Pins: the reference builder and CPU searcher compiled at K = 3, 4
+(oracle/_ref/gfmi_{3,4}_64, cpu_{3,4}_64) against our builders and the C
+restatement (CPU tests); the GPU backends against that restatement, against
+the K = 2 results for the same reads (the interval of a read does not depend
+on K), against brute-force suffix ranks at the B5 boundary, and through the
+ftab, locate and streamed paths."""
+import hashlib
+import subprocess
+
+import numpy as np
+import pytest
+
+import util
+
+GRP = ("task-grp", "coop-grp")
+
+
+def _text(n, seed, repeats=False):
+    rng = np.random.default_rng(seed)
+    t = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, size=n)].copy()
+    if repeats:
+        for _ in range(20):
+            a, b = rng.integers(0, n - 600, size=2)
+            t[b:b + 500] = t[a:a + 500]
+        t[-60:] = ord("T")
+    return t
+
+
+def _reads(t, n, m, seed):
+    rng = np.random.default_rng(seed)
+    st = rng.integers(0, t.size - m, size=n)
+    return np.concatenate([t[st[:, None] + np.arange(m)[None, :]],
+                           rng.choice(np.frombuffer(b"ACGTNacgt", np.uint8), size=(n // 4, m)),
+                           np.full((4, m), ord("T"), np.uint8), np.full((4, m), ord("A"), np.uint8)])
+
+
+@pytest.mark.parametrize("k", [3, 4])
+@pytest.mark.parametrize("repeats", [False, True])
+def test_k34_builder_and_oracle_match_reference_binaries(kfmi_mod, oracle_mod, tmp_path, k, repeats):
+    gfmi, cpu = oracle_mod.ref_binary("gfmi", k, 64), oracle_mod.ref_binary("cpu", k, 64)
+    if not gfmi.exists() or not cpu.exists():
+        pytest.skip("oracle/_ref not built (needs /root/reference)")
+    n = 40_003
+    t = _text(n, 10 * k + repeats, repeats)
+    text = t.tobytes()
+    (tmp_path / "ref.fa").write_bytes(b">x\n" + b"\n".join(text[i:i + 70] for i in range(0, n, 70)) + b"\n")
+    subprocess.run([str(gfmi), "ref.fa", str(n)], cwd=tmp_path, check=True, capture_output=True, timeout=300)
+    fn = tmp_path / f"ref.fa.{n}.64fmi{k}steps.fmi"
+    ref = fn.read_bytes()
+    ours = kfmi_mod.Index.build(text, k=k, d=64, gpu=False).image().tobytes()
+    assert hashlib.md5(ours).hexdigest() == hashlib.md5(ref).hexdigest()
+    for m in (12, 24, 100 if k == 4 else 102):
+        q = _reads(t, 800, m, m)
+        (tmp_path / "q.qry").write_bytes(b"".join(b">r\n" + r.tobytes() + b"\n" for r in q))
+        subprocess.run([str(cpu), str(fn), "q.qry", str(m), str(q.shape[0])], cwd=tmp_path, check=True,
+                       capture_output=True, timeout=300)
+        want = oracle_mod.read_results_file(str(fn) + ".res.cpu")
+        got, _ = oracle_mod.search(ref, q)
+        assert np.array_equal(got, want), (k, m)
+        i2 = kfmi_mod.Index.build(text, k=2, d=64, gpu=False)
+        assert np.array_equal(oracle_mod.search(i2.image(), q)[0], want)   # K-independent intervals
+
+
+@pytest.fixture(scope="module")
+def k4(kfmi_mod):
+    K = kfmi_mod
+    if K.device_count() < 1:
+        pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
+    K.set_device(0)
+    t = _text(500_003, 4, repeats=True)
+    text = t.tobytes()
+    return t, K.Index.build(text, k=4, d=64, gpu=True), K.Index.build(text, k=2, d=64, gpu=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("backend", GRP)
+def test_grp_matches_oracle_and_k2(kfmi_mod, oracle_mod, k4, backend):
+    K = kfmi_mod
+    t, i4, i2 = k4
+    for m, n in ((100, 20_000), (16, 4_000), (4, 2_000), (256, 1_000), (300, 1_000), (8, 500)):
+        q = _reads(t, n, m, m + 1)
+        want, _ = oracle_mod.search(i4.image(), q)
+        got = K.search_array(i4, q, backend)
+        assert np.array_equal(got, want), (backend, m, int(np.flatnonzero(got != want)[0]))
+        assert np.array_equal(got, K.search_array(i2, q, "task-mid")), (backend, m)
+
+
+@pytest.mark.gpu
+def test_grp_rejects_other_k_and_odd_m(kfmi_mod, k4):
+    K = kfmi_mod
+    t, i4, i2 = k4
+    q = _reads(t, 100, 100, 3)
+    for backend, idx in (("task-grp", i2), ("coop-grp", i2), ("task-mid", i4), ("coop", i4)):
+        with pytest.raises(K.KfmiError) as e:
+            K.search_array(idx, q, backend)
+        assert e.value.code == 33, backend
+    with pytest.raises(K.KfmiError):
+        K.search_array(i4, _reads(t, 10, 102, 1), "task-grp")        # 102 % 4 != 0 (B6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [63, 127, 255, 1023, 100])
+def test_grp_b5_boundary_against_bruteforce(kfmi_mod, n):
+    K = kfmi_mod
+    rng = np.random.default_rng(n)
+    t = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, size=n)].copy()
+    bf = util.BruteForce(t.tobytes().decode())
+    idx = K.Index.build(t.tobytes(), k=4, d=64)
+    for m in (4, 8, 12):
+        if m > n:
+            continue
+        st = rng.integers(0, n - m + 1, size=48)
+        q = np.concatenate([t[st[:, None] + np.arange(m)[None, :]],
+                            np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, size=(32, m))]])
+        want = np.array([x for i in range(q.shape[0]) for x in bf.interval(q[i].tobytes())], dtype=np.uint32)
+        for b in GRP:
+            assert np.array_equal(K.search_array(idx, q, b), want), (n, m, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("backend", GRP)
+def test_grp_ftab_stream_locate(kfmi_mod, oracle_mod, k4, backend):
+    K = kfmi_mod
+    t, i4, _ = k4
+    q = _reads(t, 6_000, 100, 77)
+    want, _ = oracle_mod.search(i4.image(), q)
+    for bases in (8, 12):
+        K.set_ftab(bases)
+        try:
+            assert np.array_equal(K.search_array(i4, q, backend), want), bases
+        finally:
+            K.set_ftab(0)
+    K.set_backend(backend)
+    K.transfer_to_gpu(i4, None, None)
+    for mode in ("1", "0"):
+        import os
+        os.environ["KFMI_STREAM_HOSTPACK"] = mode
+        try:
+            assert np.array_equal(K.search_stream(i4, q, chunk=1000), want), mode
+        finally:
+            os.environ.pop("KFMI_STREAM_HOSTPACK", None)
+    K.load().kfmi_stream_release()
+    i4.free_gpu()
+
+
+@pytest.mark.gpu
+def test_grp_locate_against_bruteforce(kfmi_mod):
+    K = kfmi_mod
+    t = _text(20_011, 8, repeats=True)
+    text = t.tobytes()
+    idx = K.Index.build(text, k=4, d=64, gpu=True, sa_rate=8)
+    sa = util.suffix_array(text + b"$")
+    q = _reads(t, 400, 12, 5)[:400]
+    res, off, pos = K.locate_array(idx, q, backend="task-grp")
+    for i in range(q.shape[0]):
+        L, R = int(res[2 * i]), int(res[2 * i + 1])
+        assert list(pos[off[i]:off[i + 1]]) == [int(x) for x in sa[L:R]], i
