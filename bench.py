@@ -69,6 +69,8 @@ def parse():
     p.add_argument("--config5-queries", type=int, default=10_000_000,
                    help="reads per GPU of the config #5 leg (0 = skip)")
     p.add_argument("--config5-qlen", type=int, default=150)
+    p.add_argument("--no-kstep4", dest="kstep4", action="store_false",
+                   help="skip the K=4 (coop-grp) leg at N=1")
     p.add_argument("--no-ingest", dest="ingest", action="store_false",
                    help="skip the FASTA file -> loadQueries -> search -> results leg (f2)")
     p.add_argument("--no-md5", action="store_true")
@@ -418,6 +420,43 @@ def config5_leg(D, idx, text: bytes, backend: str, qlen: int, nq: int, steps: in
             "lf_ms_per_rank": lfs, "oracle_sample_ok_per_rank": oks, "oracle_sample_per_rank": int(sel.size)}
 
 
+def kstep4_leg(text: bytes, reads: np.ndarray, res: np.ndarray, steps: int, pinned_md5: str | None) -> dict:
+    """The same reads on a K = 4 index (the reference's K_STEPS parameter;
+    its GPU files stop at K = 2): built on the device, laid out as LAY_GRP --
+    one 128-B line per (block, 16-code group) -- and searched by the wave64
+    cooperative kernel in 25 K-steps per 100-bp read.  The intervals do not
+    depend on K, so the results must equal the K = 2 run's (and its md5)."""
+    out = {"what": "coop-grp: K=4, d=64 index (96 GB LAY_GRP lines), wave64 cooperative LF, same reads"}
+    t = time.perf_counter()
+    i4 = K.Index.build(text, k=4, d=64, gpu=True)
+    out["build_s"] = round(time.perf_counter() - t, 2)
+    q = K.Queries.from_array(reads)
+    r = K.Results.alloc(reads.shape[0])
+    try:
+        t = time.perf_counter()
+        K.set_backend("coop-grp")
+        K.transfer_to_gpu(i4, q, r)
+        out["upload_s"] = round(time.perf_counter() - t, 2)
+        wall, lf, tot = time_backend(i4, q, r, "coop-grp", steps, 10)
+        got = r.array().copy()
+        out.update({"mqps": round(reads.shape[0] * steps / wall / 1e6, 2), "lf_ms": round(lf, 3),
+                    "step_ms": round(tot, 3), "device_index_bytes": i4.device_bytes(),
+                    "results_equal_k2": bool(np.array_equal(got, res))})
+        if pinned_md5:
+            out["results_md5_pinned"] = synth.results_md5(got) == pinned_md5
+        blocks = K.count_blocks(i4, q)
+        bytes_alg = blocks * (4 * 64 // 4 + 4)              # SURVEY 8(d): K*d/4 + 4 B per distinct block
+        out["roofline"] = {"distinct_blocks": blocks, "bytes_per_block": 68, "bytes_per_launch": bytes_alg,
+                           "achieved_GBs": round(bytes_alg / (lf / 1e3) / 1e9, 1),
+                           "frac": round(bytes_alg / (lf / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
+    finally:
+        q.close()
+        r.close()
+        i4.free_gpu()
+        i4.close()
+    return out
+
+
 def time_backend(idx, q, r, backend, steps, warmup):
     """`backend` may carry "+ftabN": the Bowtie-style jump-start table of N bases."""
     name, _, opt = backend.partition("+")
@@ -632,6 +671,15 @@ def main():
             except K.KfmiError as e:
                 extra[b] = {"error": str(e)}
             idx.free_gpu()
+        # ---- K = 4 on the same reads (LAY_GRP, coop kernel) -----------------
+        if a.kstep4 and a.qlen % 4 == 0:
+            try:
+                extra["kstep4"] = kstep4_leg(text, reads, res, a.variant_steps + 2,
+                                             synth.MD5["res3g.q10M"] if (pinned and a.qlen == 100 and
+                                                                         a.queries == 10_000_000) else None)
+                log(f"K=4 leg {extra['kstep4']}")
+            except K.KfmiError as e:
+                extra["kstep4"] = {"error": str(e)}
         # ---- device-group replication (kfmi_set_devices): the layout is built
         # once and fanned out device-to-device; here one card listed n times ----
         try:
