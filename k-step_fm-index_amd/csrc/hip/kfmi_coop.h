@@ -161,6 +161,7 @@ __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, 
   const int k = lane % C::TPR;
   const int g = lane / C::TPR;
   uint32_t cw[CW];
+  uint32_t rc = 0;
   if constexpr (MAXW > 0) {
     const uint32_t rpr = coop_stage_rows<G>(m);
 #pragma unroll 1
@@ -171,12 +172,16 @@ __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, 
       const uint4* src = reinterpret_cast<const uint4*>(ascii + r0 * m);
       for (uint32_t i = lane; i < n16; i += 64) reinterpret_cast<uint4*>(wl)[i] = src[i];
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      if ((uint32_t) lane / rpr == h) row_codes<MAXW>(wl, (uint64_t) (lane % rpr) * m, m, cw);
+      if ((uint32_t) lane / rpr == h) {   // K-step stream of bases 0 .. m-rem-1; the last rem apart
+        row_codes<MAXW>(wl, (uint64_t) (lane % rpr) * m, m - ix.rem, cw);
+        rc = rem_code(wl + (uint64_t) (lane % rpr) * m + m - ix.rem, ix.rem);
+      }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
     if (q >= num) {
 #pragma unroll
       for (int i = 0; i < CW; ++i) cw[i] = 0;
+      rc = 0;
     }
   }
   uint32_t L = 0, R = ix.bwtsize;
@@ -188,6 +193,12 @@ __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, 
     if constexpr (MAXW > 0) w0 = cw[0];
     else w0 = qp[qs];
     const uint2 lr = ix.ftab[w0 & ix.ftab_mask];
+    L = lr.x;
+    R = lr.y;
+  }
+  if (ix.rem) {   // wave-uniform: m % K != 0, the last rem bases from the remainder table
+    if constexpr (MAXW == 0) rc = qp[(uint64_t) nwords * num + qs];
+    const uint2 lr = ix.rtab[rc];
     L = lr.x;
     R = lr.y;
   }

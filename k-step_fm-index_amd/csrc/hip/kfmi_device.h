@@ -112,6 +112,10 @@ struct IdxArgs {
   // NC each, and E-1 = the first block that takes the AltCounters formula
   const uint32_t* __restrict__ ac_tail;
   uint32_t ac_tail_b0;
+  // reads with m % K = rem != 0: [L, R) after their last rem bases (code of
+  // bases m-1 .. m-rem at bits 0-1 ..), the start of their K-steps; null = rem 0
+  const uint2* __restrict__ rtab;
+  uint32_t rem;
 };
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
@@ -193,6 +197,15 @@ __device__ __forceinline__ void row_codes(const uint8_t* __restrict__ base, uint
   }
 }
 
+// Code of the last `rem` bases of a row (base m-1 at bits 0-1): the remainder
+// table's index for reads with m % K = rem.  p = the row's base m - rem.
+__device__ __forceinline__ uint32_t rem_code(const uint8_t* __restrict__ p, uint32_t rem)
+{
+  uint32_t c = 0;
+  for (uint32_t u = 0; u < rem; ++u) c |= code_of(p[rem - 1 - u]) << (2 * u);
+  return c;
+}
+
 // Fused query packing for a 256-thread block, one query per thread: each
 // wave copies its rows HBM -> LDS with coalesced 16-byte loads, RPR rows per
 // round, and the lanes owning those rows convert them from LDS (a lane reading
@@ -203,7 +216,8 @@ __host__ __device__ constexpr uint32_t stage_slot_bytes(uint32_t m) { return (st
 
 template <int MAXW>
 __device__ __forceinline__ void stage_query_codes(const uint8_t* __restrict__ ascii, uint64_t num, uint32_t m,
-                                                  uint8_t* __restrict__ lds, uint32_t (&cw)[MAXW])
+                                                  uint8_t* __restrict__ lds, uint32_t (&cw)[MAXW], uint32_t rem,
+                                                  uint32_t& rc)
 {
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint32_t rpr = stage_rows(m);
@@ -217,7 +231,10 @@ __device__ __forceinline__ void stage_query_codes(const uint8_t* __restrict__ as
     const uint4* src = reinterpret_cast<const uint4*>(ascii + r0 * m);   /* r0*m % 16 == 0 */
     for (uint32_t i = lane; i < n16; i += 64) reinterpret_cast<uint4*>(wl)[i] = src[i];
     __syncthreads();
-    if (lane / rpr == h) row_codes<MAXW>(wl, (uint64_t) (lane % rpr) * m, m, cw);
+    if (lane / rpr == h) {   /* K-step stream of bases 0 .. m-rem-1; the rem last ones apart */
+      row_codes<MAXW>(wl, (uint64_t) (lane % rpr) * m, m - rem, cw);
+      rc = rem_code(wl + (uint64_t) (lane % rpr) * m + m - rem, rem);
+    }
     __syncthreads();
   }
 }

@@ -228,7 +228,7 @@ extern "C" int32_t kfmi_load_queries_gpu(const char* fn, uint32_t sizequery, uin
   const uint64_t abytes = num * (uint64_t) sizequery;
   auto fail = [&](int32_t e) { free_dev_queries(dq); return e; };
   if (hipMalloc((void**) &dq->ascii, ((abytes + 3) & ~3ull) + 16) != hipSuccess ||
-      hipMalloc((void**) &dq->packed, 4ull * dq->nwords * (num ? num : 1)) != hipSuccess)
+      hipMalloc((void**) &dq->packed, 4ull * (dq->nwords + 1) * (num ? num : 1)) != hipSuccess)
     return fail(KFMI_E_DEVICE_ALLOC);
   if (num) {
     if (starts.alloc(8 * num) != hipSuccess) return fail(KFMI_E_DEVICE_ALLOC);

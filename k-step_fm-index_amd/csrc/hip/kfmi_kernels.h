@@ -34,9 +34,10 @@ __global__ __launch_bounds__(256) void task_kernel(IdxArgs ix, const uint32_t* _
   static_assert(MAXW == 0 || QPT == 1, "fused packing: one query per thread");
   const uint64_t base = (uint64_t) blockIdx.x * (256 * QPT) + threadIdx.x;
   uint32_t cw[QPT][CW];
+  uint32_t rc = 0;
   if constexpr (MAXW > 0) {
     extern __shared__ __attribute__((aligned(16))) uint8_t stage[];
-    stage_query_codes<MAXW>(ascii, num, m, stage, cw[0]);   /* whole block, before any exit */
+    stage_query_codes<MAXW>(ascii, num, m, stage, cw[0], ix.rem, rc);   /* whole block, before any exit */
   }
   if (base >= num) return;
   uint64_t q[QPT];
@@ -57,6 +58,14 @@ __global__ __launch_bounds__(256) void task_kernel(IdxArgs ix, const uint32_t* _
       if constexpr (MAXW > 0) w0 = cw[i][0];
       else w0 = qp[q[i]];
       const uint2 lr = ix.ftab[w0 & ix.ftab_mask];
+      L[i] = lr.x;
+      R[i] = lr.y;
+    }
+  }
+  if (ix.rem) {   /* wave-uniform: m % K != 0, the last rem bases from the remainder table */
+#pragma unroll
+    for (int i = 0; i < QPT; ++i) {
+      const uint2 lr = ix.rtab[MAXW > 0 ? rc : qp[(uint64_t) nwords * num + q[i]]];
       L[i] = lr.x;
       R[i] = lr.y;
     }
@@ -151,8 +160,8 @@ __global__ __launch_bounds__(256) void reorder_keys_kernel(const uint8_t* __rest
                                                            uint32_t* __restrict__ vals, uint32_t* __restrict__ pk)
 {
   extern __shared__ __attribute__((aligned(16))) uint8_t stage[];
-  uint32_t cw[MAXW];
-  stage_query_codes<MAXW>(ascii, num, m, stage, cw);   /* whole block, before any exit */
+  uint32_t cw[MAXW], rc;
+  stage_query_codes<MAXW>(ascii, num, m, stage, cw, 0u, rc);   /* whole block, before any exit */
   const uint64_t q = (uint64_t) blockIdx.x * 256 + threadIdx.x;
   if (q >= num) return;
   keys[q] = suffix_key(cw[0]);
@@ -227,6 +236,34 @@ __global__ __launch_bounds__(256) void ftab_build_kernel(IdxArgs ix, uint32_t fs
   }
 }
 
+/* Remainder table for reads with m % K = rem (1 <= rem < K): [L, R) of every
+ * rem-base string x (base m-1 at bits 0-1, the code order of the K-steps).
+ * A K-step from [0, n+1) gives the suffix-array range of a K-mer, so
+ *   R(x) = R of x.T^(K-rem)  (the last K-mer range inside x's),
+ *   L(x) = L of x.A^(K-rem) - #{j < K-rem : T ends with x.A^j}
+ * (the suffixes x.A^j.$ sort below x.A^(K-rem) but inside x's range).  Whether
+ * T ends with x.A^j is read from row 0 (suffix "$"), whose K-mer code holds
+ * T[n-1-s] at bits 2s.  One thread per x (4^rem <= 64). */
+template <class G>
+__global__ __launch_bounds__(64) void rem_tab_kernel(IdxArgs ix, uint32_t rem, uint2* __restrict__ out)
+{
+  const uint32_t x = threadIdx.x;
+  if (rem == 0 || rem >= (uint32_t) G::K || x >= (1u << (2 * rem))) return;
+  const uint32_t pad = 2 * ((uint32_t) G::K - rem);
+  const uint32_t cA = x << pad, cT = cA | ((1u << pad) - 1u);
+  uint32_t sx[2 * G::K];
+  plane_xor<G::K>(cA, sx);
+  uint32_t L = lf_stream<G>(ix, 0u, cA, sx);
+  plane_xor<G::K>(cT, sx);
+  const uint32_t R = lf_stream<G>(ix, ix.bwtsize, cT, sx);
+  const uint32_t n = ix.bwtsize - 1u;
+  const uint32_t tail = row_code<G>(ix, 0u);
+  for (uint32_t j = 0; j + rem < (uint32_t) G::K; ++j)
+    if (j + rem <= n && (tail & ((1u << (2 * j)) - 1u)) == 0u && ((tail >> (2 * j)) & ((1u << (2 * rem)) - 1u)) == x)
+      --L;
+  out[x] = make_uint2(L, R);
+}
+
 /* distinct d-blocks touched per step (1 if L/d == R/d else 2): the
  * dedup-aware algorithmic traffic of SURVEY 8(d).  Same LF math as the
  * task kernel; a separate launch so the timed kernels carry no counters. */
@@ -239,6 +276,11 @@ __global__ __launch_bounds__(256) void count_blocks_kernel(IdxArgs ix, const uin
   uint32_t cnt = 0;
   if (q < num) {
     uint32_t L = 0, R = ix.bwtsize;
+    if (ix.rem) {   /* a table lookup, no index line */
+      const uint2 lr = ix.rtab[qp[(uint64_t) nwords * num + q]];
+      L = lr.x;
+      R = lr.y;
+    }
     for (uint32_t t = 0; t < steps; ++t) {
       const uint32_t word = qp[(uint64_t) (t / G::SPW) * num + q];
       const uint32_t c = (word >> (2 * G::K * (t % G::SPW))) & (uint32_t) (G::NC - 1);
@@ -282,6 +324,8 @@ struct SearchLaunch {
   uint2* ftab_out;
   uint32_t ftab_steps;
   uint64_t ftab_n;
+  /* remainder table build: rem bases -> ftab_out */
+  uint32_t rem;
 };
 
 static inline int task_qpt(void)
@@ -364,6 +408,13 @@ static hipError_t launch_ftab(const SearchLaunch& a)
 }
 
 template <class G>
+static hipError_t launch_rem_tab(const SearchLaunch& a)
+{
+  hipLaunchKernelGGL((rem_tab_kernel<G>), dim3(1), dim3(64), 0, a.st, a.ix, a.rem, a.ftab_out);
+  return hipGetLastError();
+}
+
+template <class G>
 static hipError_t launch_task_sorted(const SearchLaunch& a)
 {
   const uint64_t blocks = (a.num + 255) / 256;
@@ -372,7 +423,7 @@ static hipError_t launch_task_sorted(const SearchLaunch& a)
   return hipGetLastError();
 }
 
-enum class Op { Task, Coop, Count, Locate, Ftab, TaskSorted };
+enum class Op { Task, Coop, Count, Locate, Ftab, TaskSorted, RemTab };
 
 /* Defined here, instantiated once per (K, NB, LAY) in kfmi_inst_*.hip. */
 template <int K, int NB, int LAY>
@@ -385,6 +436,7 @@ hipError_t dispatch_one(Op op, const SearchLaunch& a, unsigned long long* d_tota
     case Op::Locate: return launch_locate<G>(a);
     case Op::Ftab: return launch_ftab<G>(a);
     case Op::TaskSorted: return launch_task_sorted<G>(a);
+    case Op::RemTab: return launch_rem_tab<G>(a);
     default: return launch_count<G>(a, d_total);
   }
 }

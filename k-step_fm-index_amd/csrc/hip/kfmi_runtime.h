@@ -47,6 +47,9 @@ struct kfmi_dev_index {
    * kfmi_set_ftab values never free a table another kernel reads) */
   uint2* ftab[17] = {};
   std::mutex ftab_mu;
+  /* remainder tables: [L, R) of every r-base read suffix, r = m % K in 1..3
+   * (same lifetime rule as the ftabs, same mutex) */
+  uint2* rtab[4] = {};
   uint32_t* ac_tail = nullptr; /* LAY_MIDAC: 3 x NC AltCounters counters of entries E-1, E, E+1 */
   uint32_t ac_tail_b0 = 0xFFFFFFFFu;
 };
@@ -54,14 +57,16 @@ struct kfmi_dev_index {
 struct kfmi_dev_queries {
   int device = -1;
   uint8_t* ascii = nullptr;    /* num*size bytes, plain layout */
-  uint32_t* packed = nullptr;  /* nwords x num u32 codes */
+  uint32_t* packed = nullptr;  /* (nwords + 1) x num u32 codes; row nwords: remainder codes */
   /* in-call reorder (KFMI_REORDER=1): keys/reads double buffers, row-major
    * code words, rocPRIM temporary storage; allocated on first use */
   uint32_t* ro_buf = nullptr;
   void* ro_tmp = nullptr;
   size_t ro_tmp_bytes = 0;
   uint64_t num = 0;
-  uint32_t size = 0, K = 0, steps = 0, nwords = 0;
+  /* m = size = rem + K * steps: the last rem (< K) bases of a read are resolved
+   * by one remainder-table lookup before its K-steps (query_geometry) */
+  uint32_t size = 0, K = 0, steps = 0, nwords = 0, rem = 0;
 };
 
 namespace kfmi {
@@ -95,6 +100,7 @@ hipError_t launch_pack(const kfmi_dev_queries* dq, hipStream_t st);
 int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx, kfmi_dev_index** out = nullptr);
 int32_t upload_sa(const kfmi_fmi_t* f, kfmi_dev_index* di, DevCtx* ctx);
 int32_t upload_queries(kfmi_qrys_t* q, uint32_t K, int dev, DevCtx* ctx);
+void query_geometry(kfmi_dev_queries* dq, uint32_t K);
 void free_dev_index(kfmi_dev_index* di);
 void free_dev_queries(kfmi_dev_queries* dq);
 hipError_t h2d(void* dst, const void* src, uint64_t bytes, hipStream_t st);

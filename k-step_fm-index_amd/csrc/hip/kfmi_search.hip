@@ -177,7 +177,7 @@ hipEvent_t* thread_events(int dev)
 template <int K>
 __global__ __launch_bounds__(256) void pack_queries_kernel(const uint8_t* __restrict__ q, uint64_t num,
                                                            uint32_t m, uint32_t steps, uint32_t nwords,
-                                                           uint32_t tq, uint32_t* __restrict__ out)
+                                                           uint32_t tq, uint32_t* __restrict__ out, uint32_t rem)
 {
   extern __shared__ __attribute__((aligned(16))) uint8_t tile[];
   constexpr int SPW = 32 / (2 * K);
@@ -202,7 +202,7 @@ __global__ __launch_bounds__(256) void pack_queries_kernel(const uint8_t* __rest
       for (int j = 0; j < SPW; ++j) {
         const uint32_t st = w * SPW + j;
         if (st < steps) {
-          const int pos = (int) m - 1 - (int) (K * st);
+          const int pos = (int) (m - rem) - 1 - (int) (K * st);
           uint32_t c = 0;
 #pragma unroll
           for (int i = 0; i < K; ++i) c |= code_of(p[pos - i]) << (2 * i);
@@ -211,6 +211,7 @@ __global__ __launch_bounds__(256) void pack_queries_kernel(const uint8_t* __rest
       }
       out[(uint64_t) w * num + q0 + t] = word;
     }
+    if (rem) out[(uint64_t) nwords * num + q0 + t] = rem_code(p + m - rem, rem);   /* remainder table index */
   }
 }
 
@@ -580,6 +581,8 @@ void free_dev_index(kfmi_dev_index* di)
   if (di->ac_tail) (void) hipFree(di->ac_tail);
   for (uint2* t : di->ftab)
     if (t) (void) hipFree(t);
+  for (uint2* t : di->rtab)
+    if (t) (void) hipFree(t);
   delete di;
 }
 
@@ -899,7 +902,53 @@ IdxArgs idx_args(const kfmi_dev_index* di)
   ix.ftab_mask = 0;
   ix.ac_tail = di->ac_tail;
   ix.ac_tail_b0 = di->ac_tail_b0;
+  ix.rtab = nullptr;
+  ix.rem = 0;
   return ix;
+}
+
+/* Reads with m % K = rem != 0 (the reference reads P[-1] there, defect B6):
+ * their last rem bases are resolved by the remainder table, built once per
+ * (index, rem) from the uploaded layout (rem_tab_kernel), and the K-steps
+ * cover bases 0 .. m-rem-1.  The result is the reads' suffix-array interval,
+ * which is what every plain-semantics backend returns for m % K = 0; the
+ * AltCounters-semantics backends keep rejecting such reads (their intervals
+ * differ from the true ones where the reference's sentinel counts, and the
+ * reference defines no result here).  The ftab is not combined with it. */
+static bool rem_supported(int layout)
+{
+  return layout == LAY_INTER || layout == LAY_PACKED || layout == LAY_MID || layout == LAY_GRP;
+}
+
+static int32_t use_rtab(kfmi_dev_index* di, hipStream_t st, IdxArgs& ix, uint32_t rem)
+{
+  ix.rtab = nullptr;
+  ix.rem = 0;
+  if (!rem) return KFMI_SUCCESS;
+  if (rem >= di->K || rem > 3 || !rem_supported(di->layout)) return KFMI_E_BAD_ARGUMENT;
+  {
+    std::lock_guard<std::mutex> lk(di->ftab_mu);
+    if (!di->rtab[rem]) {
+      uint2* t = nullptr;
+      if (hipMalloc((void**) &t, 8ull << (2 * rem)) != hipSuccess) return KFMI_E_DEVICE_ALLOC;
+      SearchLaunch a{};
+      a.st = st;
+      a.ix = idx_args(di);
+      a.ftab_out = t;
+      a.rem = rem;
+      if (dispatch(Op::RemTab, di->K, di->nb, di->layout, a) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
+        (void) hipFree(t);
+        return KFMI_E_KERNEL;
+      }
+      di->rtab[rem] = t;   /* published complete; never replaced */
+    }
+  }
+  ix.rtab = di->rtab[rem];
+  ix.rem = rem;
+  ix.ftab = nullptr;
+  ix.ftab_steps = 0;
+  ix.ftab_mask = 0;
+  return KFMI_SUCCESS;
 }
 
 /* The ftab of `bases` bases, (re)built on the device from the uploaded layout
@@ -947,22 +996,28 @@ void free_dev_queries(kfmi_dev_queries* dq)
   delete dq;
 }
 
+void query_geometry(kfmi_dev_queries* dq, uint32_t K)
+{
+  dq->K = K;
+  dq->rem = dq->size % K;
+  dq->steps = (dq->size - dq->rem) / K;
+  const uint32_t spw = 32 / (2 * K);
+  dq->nwords = (dq->steps + spw - 1) / spw;
+}
+
 int32_t upload_queries(kfmi_qrys_t* q, uint32_t K, int dev, DevCtx* ctx)
 {
-  if (q->size == 0 || (q->size % K) != 0) return KFMI_E_BAD_ARGUMENT;   /* B6 */
+  if (q->size == 0 || K == 0) return KFMI_E_BAD_ARGUMENT;
   if (64ull * q->size > 160ull * 1024) return KFMI_E_BAD_ARGUMENT;       /* pack tile must fit LDS */
   kfmi_dev_queries* dq = new (std::nothrow) kfmi_dev_queries();
   if (!dq) return KFMI_E_ALLOCATING_MFASTA;
   dq->device = dev;
   dq->num = q->num;
   dq->size = q->size;
-  dq->K = K;
-  dq->steps = q->size / K;
-  const uint32_t spw = 32 / (2 * K);
-  dq->nwords = (dq->steps + spw - 1) / spw;
+  query_geometry(dq, K);
   const uint64_t abytes = q->num * (uint64_t) q->size;
   if (hipMalloc((void**) &dq->ascii, abytes + 16) != hipSuccess ||
-      hipMalloc((void**) &dq->packed, 4ull * dq->nwords * (q->num ? q->num : 1)) != hipSuccess) {
+      hipMalloc((void**) &dq->packed, 4ull * (dq->nwords + 1) * (q->num ? q->num : 1)) != hipSuccess) {
     free_dev_queries(dq);
     return KFMI_E_DEVICE_ALLOC;
   }
@@ -985,13 +1040,13 @@ hipError_t launch_pack(const kfmi_dev_queries* dq, hipStream_t st)
   const size_t lds = (size_t) tq * dq->size + 16;
   if (dq->K == 1)
     hipLaunchKernelGGL((pack_queries_kernel<1>), dim3((uint32_t) blocks), dim3(256), lds, st, dq->ascii, dq->num,
-                       dq->size, dq->steps, dq->nwords, tq, dq->packed);
+                       dq->size, dq->steps, dq->nwords, tq, dq->packed, dq->rem);
   else if (dq->K == 4)
     hipLaunchKernelGGL((pack_queries_kernel<4>), dim3((uint32_t) blocks), dim3(256), lds, st, dq->ascii, dq->num,
-                       dq->size, dq->steps, dq->nwords, tq, dq->packed);
+                       dq->size, dq->steps, dq->nwords, tq, dq->packed, dq->rem);
   else
     hipLaunchKernelGGL((pack_queries_kernel<2>), dim3((uint32_t) blocks), dim3(256), lds, st, dq->ascii, dq->num,
-                       dq->size, dq->steps, dq->nwords, tq, dq->packed);
+                       dq->size, dq->steps, dq->nwords, tq, dq->packed, dq->rem);
   return hipGetLastError();
 }
 
@@ -1027,9 +1082,7 @@ extern "C" int32_t transferCPUtoGPU(void* index, void* queries, void* results)
     if (!q->h_queries && q->num) {   /* parsed on the device (kfmi_load_queries_gpu): already there */
       if (!q->dev) return KFMI_E_NOT_ON_DEVICE;
       if (q->dev->device != dev) return KFMI_E_BAD_ARGUMENT;
-      if (q->size % f->steps) return KFMI_E_BAD_ARGUMENT;   /* B6 */
-      q->dev->K = f->steps;
-      q->dev->steps = q->size / f->steps;
+      query_geometry(q->dev, f->steps);
     } else {
       err = upload_queries(q, f->steps, dev, ctx);
       if (err) return err;
@@ -1104,6 +1157,7 @@ int32_t search_enqueue(kfmi_dev_index* di, kfmi_dev_queries* dq, uint32_t* d_res
   a.st = st;
   a.ix = idx_args(di);
   int32_t err = use_ftab(di, st, a.ix, ftab);
+  if (!err) err = use_rtab(di, st, a.ix, dq->rem);
   if (err) return err;
   a.qp = dq->packed;
   a.ascii = dq->ascii;
@@ -1113,7 +1167,7 @@ int32_t search_enqueue(kfmi_dev_index* di, kfmi_dev_queries* dq, uint32_t* d_res
   a.steps = dq->steps;
   a.nwords = dq->nwords;
   a.res = d_res;
-  const bool reorder = reorder_wanted(di, dq, a.maxw, a.ix.ftab != nullptr);
+  const bool reorder = reorder_wanted(di, dq, a.maxw, a.ix.ftab != nullptr || dq->rem);
   HIP_OK(hipEventRecord(ev[0], st));
   if (!a.maxw) HIP_OK(launch_pack(dq, st));
   if (reorder) {
@@ -1183,11 +1237,14 @@ extern "C" int32_t kfmi_count_blocks(void* index, void* queries, uint64_t* block
   DevCtx* ctx = nullptr;
   int32_t err = ctx_for(di->device, &ctx);
   if (err) return err;
-  unsigned long long* d_total = nullptr;
-  HIP_OK(hipMalloc((void**) &d_total, sizeof(unsigned long long)));
-  SearchLaunch a;
+  SearchLaunch a{};
   a.st = ctx->st;
   a.ix = idx_args(di);
+  if (dq->device != di->device || dq->K != di->K) return KFMI_E_BAD_ARGUMENT;
+  err = use_rtab(di, ctx->st, a.ix, dq->rem);
+  if (err) return err;
+  unsigned long long* d_total = nullptr;
+  HIP_OK(hipMalloc((void**) &d_total, sizeof(unsigned long long)));
   a.qp = dq->packed;
   a.ascii = dq->ascii;
   a.m = dq->size;

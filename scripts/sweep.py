@@ -121,7 +121,8 @@ def main():
                     out = {"backend": b, "knobs": kn, "order": kind, "sort_suffix": ss, "lf_ms": round(float(np.median(lf)), 3),
                            "lf_ms_min": round(float(np.min(lf)), 3), "step_ms": round(float(np.median(tot)), 3),
                            "wall_ms": round(wall * 1e3, 3), "mqps": round(reads.shape[0] / wall / 1e6, 1),
-                           "equal": bool(np.array_equal(res, ref)), "dev_bytes": idx.device_bytes()}
+                           "equal": bool(np.array_equal(res, ref)), "dev_bytes": idx.device_bytes(),
+                           "res_md5": synth.results_md5(res)}
                 except K.KfmiError as e:
                     out = {"backend": b, "knobs": kn, "order": kind, "sort_suffix": ss, "error": str(e)}
                 print(json.dumps(out), flush=True)

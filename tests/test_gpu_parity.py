@@ -144,9 +144,14 @@ def test_edge_cases(gpu, oracle_mod, random_index):
         want, _ = oracle_mod.search(idx.image(), q)
         for b in PLAIN:
             assert np.array_equal(gpu.search_array(idx, q, b), want), (b, n)
-    # m % K != 0 is rejected (reference reads query[-1])
+    # m % K != 0 (reference reads query[-1]): the AltCounters
+    # backends reject it, the plain ones take the remainder table
+    # (tests/test_remainder.py): here 4 x "AAAAA" -> the interval of A^5
     with pytest.raises(gpu.KfmiError):
-        gpu.search_array(idx, np.zeros((4, 5), dtype=np.uint8) + 65, "task")
+        gpu.search_array(idx, np.zeros((4, 5), dtype=np.uint8) + 65, "task-ac")
+    a5 = gpu.search_array(idx, np.zeros((4, 5), dtype=np.uint8) + 65, "task")
+    t8 = np.frombuffer(text, dtype=np.uint8)
+    assert a5[1] - a5[0] == int(np.sum(np.all(np.lib.stride_tricks.sliding_window_view(t8, 5) == 65, axis=1)))
     # search before transfer
     q = gpu.Queries.from_array(np.zeros((4, 8), dtype=np.uint8) + 65)
     r = gpu.Results.alloc(4)

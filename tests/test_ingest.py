@@ -124,9 +124,7 @@ def test_gpu_parse_golden_and_large(kfmi_mod, gpu_idx, tmp_path):
     idx, text = gpu_idx
     for case, c in sorted(util.manifest().items()):
         for m, qd in sorted(c["queries"].items()):
-            m = int(m)
-            if m % 2:
-                continue
+            m = int(m)                    # odd m included: remainder table (test_remainder.py)
             path = util.GOLDEN / case / qd["file"]
             q = K.Queries.load_gpu(path, m, qd["num"])
             assert q.num() == qd["num"]

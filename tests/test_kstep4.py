@@ -90,7 +90,7 @@ def test_grp_matches_oracle_and_k2(kfmi_mod, oracle_mod, k4, backend):
 
 
 @pytest.mark.gpu
-def test_grp_rejects_other_k_and_odd_m(kfmi_mod, k4):
+def test_grp_rejects_other_k_and_takes_any_m(kfmi_mod, k4):
     K = kfmi_mod
     t, i4, i2 = k4
     q = _reads(t, 100, 100, 3)
@@ -98,8 +98,11 @@ def test_grp_rejects_other_k_and_odd_m(kfmi_mod, k4):
         with pytest.raises(K.KfmiError) as e:
             K.search_array(idx, q, backend)
         assert e.value.code == 33, backend
-    with pytest.raises(K.KfmiError):
-        K.search_array(i4, _reads(t, 10, 102, 1), "task-grp")        # 102 % 4 != 0 (B6)
+    # 102 % 4 = 2 (reference defect B6): the last 2 bases from the remainder
+    # table (tests/test_remainder.py), the interval equals the K = 2 one
+    q = _reads(t, 2000, 102, 1)
+    for backend in GRP:
+        assert np.array_equal(K.search_array(i4, q, backend), K.search_array(i2, q, "task-mid")), backend
 
 
 @pytest.mark.gpu
