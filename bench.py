@@ -420,12 +420,15 @@ def config5_leg(D, idx, text: bytes, backend: str, qlen: int, nq: int, steps: in
             "lf_ms_per_rank": lfs, "oracle_sample_ok_per_rank": oks, "oracle_sample_per_rank": int(sel.size)}
 
 
-def kstep4_leg(text: bytes, reads: np.ndarray, res: np.ndarray, steps: int, pinned_md5: str | None) -> dict:
+def kstep4_leg(D, text: bytes, reads: np.ndarray, res: np.ndarray, steps: int, pinned_md5: str | None,
+               c5_qlen: int, c5_queries: int) -> dict:
     """The same reads on a K = 4 index (the reference's K_STEPS parameter;
     its GPU files stop at K = 2): built on the device, laid out as LAY_GRP --
     one 128-B line per (block, 16-code group) -- and searched by the wave64
     cooperative kernel in 25 K-steps per 100-bp read.  The intervals do not
-    depend on K, so the results must equal the K = 2 run's (and its md5)."""
+    depend on K, so the results must equal the K = 2 run's (and its md5).
+    Config #5's read shape runs on it too (150 % 4 = 2: the last two bases of
+    each read from the remainder table, then 37 K-steps), oracle-sampled."""
     out = {"what": "coop-grp: K=4, d=64 index (96 GB LAY_GRP lines), wave64 cooperative LF, same reads"}
     t = time.perf_counter()
     i4 = K.Index.build(text, k=4, d=64, gpu=True)
@@ -449,6 +452,8 @@ def kstep4_leg(text: bytes, reads: np.ndarray, res: np.ndarray, steps: int, pinn
         out["roofline"] = {"distinct_blocks": blocks, "bytes_per_block": 68, "bytes_per_launch": bytes_alg,
                            "achieved_GBs": round(bytes_alg / (lf / 1e3) / 1e9, 1),
                            "frac": round(bytes_alg / (lf / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
+        if c5_queries > 0:
+            out["config5"] = config5_leg(D, i4, text, "coop-grp", c5_qlen, c5_queries, steps, 5, False)
     finally:
         q.close()
         r.close()
@@ -674,9 +679,10 @@ def main():
         # ---- K = 4 on the same reads (LAY_GRP, coop kernel) -----------------
         if a.kstep4 and a.qlen % 4 == 0:
             try:
-                extra["kstep4"] = kstep4_leg(text, reads, res, a.variant_steps + 2,
+                extra["kstep4"] = kstep4_leg(D, text, reads, res, a.variant_steps + 2,
                                              synth.MD5["res3g.q10M"] if (pinned and a.qlen == 100 and
-                                                                         a.queries == 10_000_000) else None)
+                                                                         a.queries == 10_000_000) else None,
+                                             a.config5_qlen, a.config5_queries)
                 log(f"K=4 leg {extra['kstep4']}")
             except K.KfmiError as e:
                 extra["kstep4"] = {"error": str(e)}
