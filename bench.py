@@ -379,12 +379,14 @@ def config1_leg(backend: str, thr: int, steps: int = 5) -> dict:
     return out
 
 
-def config5_leg(D, idx, text: bytes, backend: str, qlen: int, nq: int, steps: int, warmup: int, ac: bool) -> dict:
+def config5_leg(D, idx, text: bytes, backend: str, qlen: int, nq: int, steps: int, warmup: int, ac: bool,
+                oracle_idx=None) -> dict:
     """BASELINE config #5's read shape on every rank: this rank's shard of nq
     reads of qlen bases (seed 20 + rank; 10M x 150 bp = one eighth of the
     80M x 150 bp batch at N = 8), searched on the resident index; timed like
     the main leg (barrier + synchronize, max over ranks), then an evenly spread
-    100 K-read sample of every rank checked against the CPU oracle."""
+    100 K-read sample of every rank checked against the CPU oracle (on
+    `oracle_idx`'s image when given: another index of the same text)."""
     from oracle import oracle
     reads = synth.gather_reads(text, synth.read_starts(len(text), nq, qlen, seed=20 + D.rank), qlen)
     q = K.Queries.from_array(reads)
@@ -404,7 +406,8 @@ def config5_leg(D, idx, text: bytes, backend: str, qlen: int, nq: int, steps: in
     K.transfer_to_cpu(r)
     res = r.array().copy()
     sel = np.linspace(0, nq - 1, min(100_000, nq)).astype(np.int64)
-    img_idx = idx.alt_counters()[0] if ac else idx
+    src = oracle_idx if oracle_idx is not None else idx
+    img_idx = src.alt_counters()[0] if ac else src
     want, _ = oracle.search(img_idx.image(), reads[sel], nthreads=max(1, cpu_effective() // D.world))
     ok = bool(np.array_equal(want.reshape(-1, 2), res.reshape(-1, 2)[sel]))
     if ac:
@@ -420,43 +423,66 @@ def config5_leg(D, idx, text: bytes, backend: str, qlen: int, nq: int, steps: in
             "lf_ms_per_rank": lfs, "oracle_sample_ok_per_rank": oks, "oracle_sample_per_rank": int(sel.size)}
 
 
-def kstep4_leg(D, text: bytes, reads: np.ndarray, res: np.ndarray, steps: int, pinned_md5: str | None,
+def kstep4_leg(D, text: bytes, reads: np.ndarray, res: np.ndarray, idx2, steps: int, pinned_md5: str | None,
                c5_qlen: int, c5_queries: int) -> dict:
-    """The same reads on a K = 4 index (the reference's K_STEPS parameter;
-    its GPU files stop at K = 2): built on the device, laid out as LAY_GRP --
-    one 128-B line per (block, 16-code group) -- and searched by the wave64
-    cooperative kernel in 25 K-steps per 100-bp read.  The intervals do not
-    depend on K, so the results must equal the K = 2 run's (and its md5).
-    Config #5's read shape runs on it too (150 % 4 = 2: the last two bases of
-    each read from the remainder table, then 37 K-steps), oracle-sampled."""
-    out = {"what": "coop-grp: K=4, d=64 index (96 GB LAY_GRP lines), wave64 cooperative LF, same reads"}
+    """Every rank's reads on a K = 4 index (the reference's K_STEPS parameter;
+    its GPU files stop at K = 2): built on the device with no host image (the
+    51 GB of tag-100 entries stay in HBM), laid out as LAY_GRP -- one 128-B line
+    per (block, 16-code group) -- and searched by the wave64 cooperative kernel
+    in 25 K-steps per 100-bp read.  Timed like the main leg (barrier, max over
+    ranks).  The intervals do not depend on K, so every rank's results must
+    equal its K = 2 results (rank 0: and the pinned md5).  Config #5's read
+    shape runs on it too (150 % 4 = 2: the last two bases of each read from the
+    remainder table, then 37 K-steps), oracle-sampled against the K = 2 image."""
+    out = {"what": "coop-grp: K=4, d=64 index (96 GB LAY_GRP lines), wave64 cooperative LF, "
+                   "the main leg's reads on every rank"}
     t = time.perf_counter()
-    i4 = K.Index.build(text, k=4, d=64, gpu=True)
-    out["build_s"] = round(time.perf_counter() - t, 2)
+    i4 = K.Index.build(text, k=4, d=64, gpu=True, host_image=False)
+    build_s = time.perf_counter() - t
     q = K.Queries.from_array(reads)
     r = K.Results.alloc(reads.shape[0])
     try:
         t = time.perf_counter()
         K.set_backend("coop-grp")
         K.transfer_to_gpu(i4, q, r)
-        out["upload_s"] = round(time.perf_counter() - t, 2)
-        wall, lf, tot = time_backend(i4, q, r, "coop-grp", steps, 10)
+        upload_s = time.perf_counter() - t
+        for _ in range(5):
+            K.search(i4, q, r)
+        D.barrier()
+        lf = []
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            K.search(i4, q, r)
+            lf.append(K.last_timing()["lf_ms"])
+        D.barrier()
+        el = D.max(time.perf_counter() - t0)
+        K.transfer_to_cpu(r)
         got = r.array().copy()
-        out.update({"mqps": round(reads.shape[0] * steps / wall / 1e6, 2), "lf_ms": round(lf, 3),
-                    "step_ms": round(tot, 3), "device_index_bytes": i4.device_bytes(),
-                    "results_equal_k2": bool(np.array_equal(got, res))})
-        if pinned_md5:
+        total = D.sum(float(reads.shape[0]))
+        out.update({"mqps": round(total * steps / el / 1e6, 2), "ms_per_step": round(el / steps * 1e3, 4),
+                    "lf_ms": round(float(np.mean(lf)), 3), "lf_ms_per_rank": D.gather(round(float(np.mean(lf)), 4)),
+                    "device_index_bytes": i4.device_bytes(),
+                    "build_s_max": round(D.max(build_s), 2), "upload_s_max": round(D.max(upload_s), 2),
+                    "results_equal_k2_per_rank": D.gather(bool(np.array_equal(got, res)))})
+        if pinned_md5 and D.rank == 0:
             out["results_md5_pinned"] = synth.results_md5(got) == pinned_md5
         blocks = K.count_blocks(i4, q)
         bytes_alg = blocks * (4 * 64 // 4 + 4)              # SURVEY 8(d): K*d/4 + 4 B per distinct block
+        lfm = float(np.mean(lf))
         out["roofline"] = {"distinct_blocks": blocks, "bytes_per_block": 68, "bytes_per_launch": bytes_alg,
-                           "achieved_GBs": round(bytes_alg / (lf / 1e3) / 1e9, 1),
-                           "frac": round(bytes_alg / (lf / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
-        if c5_queries > 0:
-            out["config5"] = config5_leg(D, i4, text, "coop-grp", c5_qlen, c5_queries, steps, 5, False)
-    finally:
+                           "achieved_GBs": round(bytes_alg / (lfm / 1e3) / 1e9, 1),
+                           "frac": round(bytes_alg / (lfm / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                           "note": "rank 0's launch"}
         q.close()
         r.close()
+        q = r = None
+        if c5_queries > 0:
+            out["config5"] = config5_leg(D, i4, text, "coop-grp", c5_qlen, c5_queries, steps, 5, False,
+                                         oracle_idx=idx2)
+    finally:
+        if q is not None:
+            q.close()
+            r.close()
         i4.free_gpu()
         i4.close()
     return out
@@ -618,6 +644,16 @@ def main():
         except Exception as e:          # auxiliary leg (e.g. TMPDIR full): report, never abort the bench
             ingest = {"error": repr(e)}
             os.environ.pop("KFMI_LOAD_MMAP", None)
+    k4 = None
+    if a.kstep4 and a.k == 2 and a.d == 64:
+        # ---- K = 4 on every rank's reads (LAY_GRP, coop kernel) --------------
+        try:
+            k4 = kstep4_leg(D, text, reads, res, idx, a.steps,
+                            synth.MD5["res3g.q10M"] if (pinned and a.qlen == 100 and a.queries == 10_000_000)
+                            else None, a.config5_qlen, a.config5_queries)
+            log(f"rank {D.rank}: K=4 leg {k4}")
+        except K.KfmiError as e:
+            k4 = {"error": str(e)}
     rank_rows = D.gather({"ingest": ingest, "rank": D.rank, "device": dev, "queries": int(reads.shape[0]),
                           "lf_ms": round(float(np.mean(lf_ms)), 4), "step_ms": round(float(np.mean(tot_ms)), 4),
                           "elapsed_s": round(elapsed, 4), "distinct_blocks": int(blocks),
@@ -632,6 +668,8 @@ def main():
         log(f"gather probe: best {probe['best_G_lines_per_s']} G lines/s ({probe['best_kind']})")
     if c5 is not None:
         extra["config5"] = c5
+    if k4 is not None:
+        extra["kstep4"] = k4
     if ingest is not None:
         extra["ingest_file"] = ingest          # rank 0's; every rank's is under "ranks"
     cpu = None
@@ -676,16 +714,6 @@ def main():
             except K.KfmiError as e:
                 extra[b] = {"error": str(e)}
             idx.free_gpu()
-        # ---- K = 4 on the same reads (LAY_GRP, coop kernel) -----------------
-        if a.kstep4 and a.qlen % 4 == 0:
-            try:
-                extra["kstep4"] = kstep4_leg(D, text, reads, res, a.variant_steps + 2,
-                                             synth.MD5["res3g.q10M"] if (pinned and a.qlen == 100 and
-                                                                         a.queries == 10_000_000) else None,
-                                             a.config5_qlen, a.config5_queries)
-                log(f"K=4 leg {extra['kstep4']}")
-            except K.KfmiError as e:
-                extra["kstep4"] = {"error": str(e)}
         # ---- device-group replication (kfmi_set_devices): the layout is built
         # once and fanned out device-to-device; here one card listed n times ----
         try:

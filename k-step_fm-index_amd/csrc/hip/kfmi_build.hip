@@ -398,7 +398,8 @@ int32_t resolve_ties(const uint64_t* keys, uint32_t* sa, uint64_t n, hipStream_t
   return KFMI_SUCCESS;
 }
 
-int32_t build_gpu(const char* text, uint64_t n, uint32_t k, uint32_t d, uint32_t sa_rate, int dev, kfmi_fmi_t** out)
+int32_t build_gpu(const char* text, uint64_t n, uint32_t k, uint32_t d, uint32_t sa_rate, int dev, bool host_image,
+                  kfmi_fmi_t** out)
 {
   /* n + 1 >= k: every D_s (s < k) exists -- SA = s is a suffix of T for s < n and
    * the '$' row 0 for s == n -- and (SA - 1 - s) wraps at most once. */
@@ -489,7 +490,7 @@ int32_t build_gpu(const char* text, uint64_t n, uint32_t k, uint32_t d, uint32_t
     /* suffix s < K always exists when n >= K; for n < K the missing ones never match */
   }
   kfmi_fmi_t* f = nullptr;
-  int32_t err = kfmi_index_alloc(100, k, (uint32_t) rows, nentries, d, nullptr, nullptr, &f);
+  int32_t err = kfmi_index_alloc_ex(100, k, (uint32_t) rows, nentries, d, nullptr, nullptr, host_image ? 1 : 0, &f);
   if (err) return err;
   const uint32_t ew = f->entry_words;
   DevBuf ent, counts, occ, cp;
@@ -582,17 +583,25 @@ int32_t build_gpu(const char* text, uint64_t n, uint32_t k, uint32_t d, uint32_t
   hipLaunchKernelGGL(k_fill, dim3((nentries + 255) / 256), dim3(256), 0, st, occ.as<uint32_t>(), nentries, nc,
                      2 * nb * k, ew, cp.as<uint32_t>(), ent.as<uint32_t>());
   if (hipGetLastError() != hipSuccess ||
-      hipMemcpyAsync(f->h_index, ent.p, (uint64_t) ew * 4 * nentries, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      (host_image &&
+       hipMemcpyAsync(f->h_index, ent.p, (uint64_t) ew * 4 * nentries, hipMemcpyDeviceToHost, st) != hipSuccess) ||
       hipStreamSynchronize(st) != hipSuccess)
     return fail(KFMI_E_BUILDING_FMI);
+  if (!host_image) {   /* the entries stay in HBM, owned by the handle */
+    f->d_entries = ent.as<uint32_t>();
+    f->d_entries_dev = dev;
+    ent.p = nullptr;
+  }
   for (uint32_t s = 0; s < k; ++s) {
     f->dollarPositionBWT[s] = drow[s];
     f->dollarBaseBWT[s] = dbase[s];
     f->modposdollarBWT[s] = drow[s] / d;
   }
-  const void* img;
-  uint64_t bytes;
-  kfmi_index_image(f, &img, &bytes);   /* refresh the header words */
+  uint32_t* hdr = reinterpret_cast<uint32_t*>(f->image);   /* the header words of the image */
+  for (uint32_t s = 0; s < k; ++s) {
+    hdr[6 + s] = drow[s];
+    hdr[6 + k + s] = dbase[s];
+  }
   *out = f;
   return KFMI_SUCCESS;
 }
@@ -604,7 +613,7 @@ extern "C" int32_t kfmi_build_index_gpu_sa(const char* text, uint64_t n, uint32_
 {
   if (sa_rate && !kfmi_sa_rate_ok(sa_rate)) return KFMI_E_BAD_ARGUMENT;
   if (kfmi_device_count() < 1) return KFMI_E_NO_DEVICE;
-  int32_t e = build_gpu(text, n, k, d, sa_rate, kfmi_current_device(), (kfmi_fmi_t**) index);
+  int32_t e = build_gpu(text, n, k, d, sa_rate, kfmi_current_device(), true, (kfmi_fmi_t**) index);
   if (e == KFMI_E_NOT_IMPLEMENTED) {
     fprintf(stderr, "kstepfmi build: text of %llu bases exceeds one dispatch per base (2^32 - 256), "
                     "using the host builder\n", (unsigned long long) n);
@@ -623,6 +632,43 @@ extern "C" int32_t kfmi_build_stats(uint64_t* ties, uint32_t* rounds)
 extern "C" int32_t kfmi_build_index_gpu(const char* text, uint64_t n, uint32_t k, uint32_t d,
                                         int32_t want_host_image, void** index)
 {
-  (void) want_host_image;   /* the host image is always produced (saveIndex, oracle, md5 pins) */
-  return kfmi_build_index_gpu_sa(text, n, k, d, 0, index);
+  if (want_host_image) return kfmi_build_index_gpu_sa(text, n, k, d, 0, index);
+  if (kfmi_device_count() < 1) return KFMI_E_NO_DEVICE;
+  int32_t e = build_gpu(text, n, k, d, 0, kfmi_current_device(), false, (kfmi_fmi_t**) index);
+  if (e == KFMI_E_NOT_IMPLEMENTED) return kfmi_build_index_gpu_sa(text, n, k, d, 0, index);   /* host builder */
+  return e;
+}
+
+/* The host image of an index whose entries are only in HBM: fetched once (one
+ * D2H), then kept beside the device copy. */
+extern "C" int32_t kfmi_host_entries(kfmi_fmi_t* f)
+{
+  if (!f) return KFMI_E_BAD_ARGUMENT;
+  if (f->h_index) return KFMI_SUCCESS;
+  if (!f->d_entries) return KFMI_E_BAD_ARGUMENT;
+  const uint64_t body = 4ull * f->entry_words * f->nentries;
+  uint8_t* img = (uint8_t*) realloc(f->image, f->header_bytes + body + 64);
+  if (!img) return KFMI_E_ALLOCATING_FMI;
+  f->image = img;
+  int cur = 0;
+  (void) hipGetDevice(&cur);
+  if (hipSetDevice(f->d_entries_dev) != hipSuccess ||
+      hipMemcpy(img + f->header_bytes, f->d_entries, body, hipMemcpyDeviceToHost) != hipSuccess) {
+    (void) hipSetDevice(cur);
+    return KFMI_E_KERNEL;
+  }
+  (void) hipSetDevice(cur);
+  f->h_index = (uint32_t*) (img + f->header_bytes);
+  return KFMI_SUCCESS;
+}
+
+extern "C" void kfmi_free_dev_entries(kfmi_fmi_t* f)
+{
+  if (!f || !f->d_entries) return;
+  int cur = 0;
+  (void) hipGetDevice(&cur);
+  (void) hipSetDevice(f->d_entries_dev);
+  (void) hipFree(f->d_entries);
+  (void) hipSetDevice(cur);
+  f->d_entries = nullptr;
 }

@@ -486,7 +486,20 @@ static void end_counters(const kfmi_fmi_t* f, uint32_t* out)
 {
   const uint32_t nc = 1u << (2 * f->steps), nb = f->nbitmaps;
   const uint32_t last = f->nentries - 1;
-  const uint32_t* e = f->h_index + (uint64_t) last * f->entry_words;
+  std::vector<uint32_t> dev_last;
+  const uint32_t* e;
+  if (f->h_index) {
+    e = f->h_index + (uint64_t) last * f->entry_words;
+  } else {   /* entries only in HBM: fetch the last one */
+    dev_last.assign(f->entry_words, 0u);
+    int cur = 0;
+    (void) hipGetDevice(&cur);
+    (void) hipSetDevice(f->d_entries_dev);
+    (void) hipMemcpy(dev_last.data(), f->d_entries + (uint64_t) last * f->entry_words, 4ull * f->entry_words,
+                     hipMemcpyDeviceToHost);
+    (void) hipSetDevice(cur);
+    e = dev_last.data();
+  }
   const uint32_t o = f->bwtsize - last * f->chunk;  /* rows of the last block, in (0, d] */
   for (uint32_t c = 0; c < nc; ++c) {
     uint32_t pop = 0;
@@ -652,11 +665,24 @@ __global__ __launch_bounds__(256) void interleave_entries_kernel(uint32_t* __res
   }
 }
 
+/* The stored entries of `src` into device memory at dst: from the host image,
+ * or device to device when they only live in HBM (built there). */
+static hipError_t entries_in(void* dst, const kfmi_fmi_t* src, uint64_t body, hipStream_t st)
+{
+  if (src->h_index) return h2d(dst, src->h_index, body, st);
+  if (!src->d_entries) return hipErrorInvalidValue;
+  int cur = 0;
+  hipError_t e = hipGetDevice(&cur);
+  if (e != hipSuccess) return e;
+  if (cur == src->d_entries_dev) return hipMemcpyAsync(dst, src->d_entries, body, hipMemcpyDeviceToDevice, st);
+  return hipMemcpyPeerAsync(dst, cur, src->d_entries, src->d_entries_dev, body, st);
+}
+
 /* The entries of `src` as tag 101 (plain family) or as stored, into device
  * memory at dst (`body` bytes). */
 static hipError_t upload_entries(void* dst, const kfmi_fmi_t* src, uint64_t body, hipStream_t st)
 {
-  if (src->tag != 100) return h2d(dst, src->h_index, body, st);
+  if (src->tag != 100) return entries_in(dst, src, body, st);
   const uint32_t ew = src->entry_words, K = src->steps, nb = src->nbitmaps;
   if (ew > KFMI_MAX_ENTRY_WORDS || ew == 0) return hipErrorInvalidValue;
   EntryPerm perm;
@@ -664,7 +690,7 @@ static hipError_t upload_entries(void* dst, const kfmi_fmi_t* src, uint64_t body
   for (uint32_t w = 0; w < nb; ++w)
     for (uint32_t k = 0; k < K; ++k)
       for (uint32_t t = 0; t < 2; ++t) perm.p[kfmi_plane_index(101, K, nb, k, t, w)] = kfmi_plane_index(100, K, nb, k, t, w);
-  hipError_t e = h2d(dst, src->h_index, body, st);
+  hipError_t e = entries_in(dst, src, body, st);
   const uint64_t nent = body / (4ull * ew), nbatch = (nent + IL_LDS_WORDS / ew - 1) / (IL_LDS_WORDS / ew);
   if (e == hipSuccess && nent) {
     hipLaunchKernelGGL(interleave_entries_kernel, dim3((uint32_t) (nbatch < (1u << 16) ? nbatch : (1u << 16))),

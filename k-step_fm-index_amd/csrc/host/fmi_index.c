@@ -46,6 +46,15 @@ int32_t kfmi_index_alloc(uint32_t tag, uint32_t steps, uint32_t bwtsize, uint32_
                          uint32_t chunk, const uint32_t *dpos, const uint32_t *dbase,
                          kfmi_fmi_t **out)
 {
+  return kfmi_index_alloc_ex(tag, steps, bwtsize, nentries, chunk, dpos, dbase, 1, out);
+}
+
+/* with_entries = 0: header only (h_index NULL), for indexes whose entries stay
+ * on the device until asked for (kfmi_host_entries). */
+int32_t kfmi_index_alloc_ex(uint32_t tag, uint32_t steps, uint32_t bwtsize, uint32_t nentries,
+                            uint32_t chunk, const uint32_t *dpos, const uint32_t *dbase,
+                            int with_entries, kfmi_fmi_t **out)
+{
   kfmi_fmi_t *f;
   uint32_t s, *h;
   uint32_t nc = 1u << (2 * steps);
@@ -58,7 +67,7 @@ int32_t kfmi_index_alloc(uint32_t tag, uint32_t steps, uint32_t bwtsize, uint32_
   f->entry_words = kfmi_entry_words(tag, steps, chunk);
   f->header_bytes = 24 + 8 * steps;
   f->image_bytes = f->header_bytes + 4ull * f->entry_words * nentries;
-  f->image = (uint8_t *) calloc(1, f->image_bytes + 64);
+  f->image = (uint8_t *) calloc(1, (with_entries ? f->image_bytes : f->header_bytes) + 64);
   if (!f->image) { free(f); return KFMI_E_ALLOCATING_FMI; }
   h = (uint32_t *) f->image;
   h[0] = tag; h[1] = steps; h[2] = bwtsize; h[3] = ncounters; h[4] = nentries; h[5] = chunk;
@@ -69,7 +78,7 @@ int32_t kfmi_index_alloc(uint32_t tag, uint32_t steps, uint32_t bwtsize, uint32_
     h[6 + s] = f->dollarPositionBWT[s];
     h[6 + steps + s] = f->dollarBaseBWT[s];
   }
-  f->h_index = (uint32_t *) (f->image + f->header_bytes);
+  f->h_index = with_entries ? (uint32_t *) (f->image + f->header_bytes) : NULL;
   *out = f;
   return KFMI_SUCCESS;
 }
@@ -158,7 +167,9 @@ int32_t loadIndex(const char *fn, void **index)
 int32_t kfmi_index_image(void *index, const void **image, uint64_t *bytes)
 {
   kfmi_fmi_t *f = (kfmi_fmi_t *) index;
+  int32_t err;
   if (!f || !f->image) return KFMI_E_BAD_ARGUMENT;
+  if ((err = kfmi_host_entries(f)) != KFMI_SUCCESS) return err;
   refresh_header(f);
   *image = f->image;
   *bytes = f->image_bytes;
@@ -186,6 +197,7 @@ int32_t saveIndex(const char *fn, void *index)
   char name[1024];
   FILE *fp;
   if (!f) return KFMI_E_BAD_ARGUMENT;
+  if (kfmi_host_entries(f) != KFMI_SUCCESS) return KFMI_E_SAVING_INDEX_FILE;
   switch (f->tag) {
     case 100: snprintf(name, sizeof(name), "%s.%u.%ufmi%usteps.fmi", fn, f->bwtsize - 1, f->chunk, f->steps); break;
     case 101: snprintf(name, sizeof(name), "%s.interleaving", fn); break;
@@ -206,6 +218,7 @@ int32_t freeIndex(void **index)
   kfmi_fmi_t *f = index ? (kfmi_fmi_t *) *index : NULL;
   if (!f) return KFMI_SUCCESS;
   if (f->dev || f->grp) freeIndexGPU(index);
+  if (f->d_entries) kfmi_free_dev_entries(f);
   free(f->h_sa);
   free(f->image);
   free(f);
@@ -305,6 +318,7 @@ int32_t kfmi_transform_interleave(void *index100, void **index101)
   uint32_t nb, K, i, w, s, t, c, nbw;
   int32_t err;
   if (!f || f->tag != 100) return KFMI_INDEX_VER_BASELINE;
+  if ((err = kfmi_host_entries(f)) != KFMI_SUCCESS) return err;
   err = kfmi_index_alloc(101, f->steps, f->bwtsize, f->nentries, f->chunk,
                          f->dollarPositionBWT, f->dollarBaseBWT, &g);
   if (err) return err;
@@ -354,6 +368,7 @@ int32_t kfmi_ac_tail(const kfmi_fmi_t *f, uint32_t *out, uint32_t *first)
   uint32_t c, nc, nbw, rem, last;
   const uint32_t *src;
   if (!f || !out || (f->tag != 100 && f->tag != 101) || !f->nentries) return KFMI_E_BAD_ARGUMENT;
+  if (kfmi_host_entries(f) != KFMI_SUCCESS) return KFMI_E_NOT_ON_DEVICE;
   nc = f->ncounters;
   nbw = 2 * f->nbitmaps * f->steps;
   last = f->nentries;
@@ -383,6 +398,7 @@ int32_t kfmi_transform_ac(void *index100, void **index200, void **index201)
   uint32_t *lastCnt;
   int32_t err, v;
   if (!f || f->tag != 100) return KFMI_INDEX_VER_BASELINE;
+  if ((err = kfmi_host_entries(f)) != KFMI_SUCCESS) return err;
   nb = f->nbitmaps; K = f->steps; nc = f->ncounters; half = nc / 2; nbw = 2 * nb * K;
   last = f->nentries;          /* index of the sentinel entry */
   rem = f->bwtsize % f->chunk;

@@ -34,7 +34,14 @@ typedef struct {
   uint8_t  *image;
   uint64_t  image_bytes;
   uint32_t  header_bytes;
-  uint32_t *h_index;       /* = (uint32_t *)(image + header_bytes), may be unaligned to 16 */
+  uint32_t *h_index;       /* = (uint32_t *)(image + header_bytes), may be unaligned to 16;
+                              NULL while the entries live only on the device (d_entries) */
+  /* entries of an index built on the device without a host image
+   * (kfmi_build_index_gpu, want_host_image = 0): uploads relayout them on the
+   * device; the host image is fetched only when something asks for it
+   * (kfmi_host_entries).  Owned by the handle, freed by freeIndex. */
+  uint32_t *d_entries;
+  int       d_entries_dev;
   struct kfmi_dev_index *dev;
   char      src_name[512]; /* file the index came from (for saveIndex/saveResults naming) */
   /* row-sampled suffix array for locate (not in the reference):
@@ -70,9 +77,16 @@ typedef struct {
 } kfmi_ref_t;
 
 /* fmi_index.c */
+/* Host entries of an index whose entries are only on the device (fetched once,
+ * then kept); KFMI_SUCCESS at once when the host image exists (kfmi_build.hip). */
+int32_t kfmi_host_entries(kfmi_fmi_t *f);
+void kfmi_free_dev_entries(kfmi_fmi_t *f);
 int32_t kfmi_index_alloc(uint32_t tag, uint32_t steps, uint32_t bwtsize, uint32_t nentries,
                          uint32_t chunk, const uint32_t *dpos, const uint32_t *dbase,
                          kfmi_fmi_t **out);
+int32_t kfmi_index_alloc_ex(uint32_t tag, uint32_t steps, uint32_t bwtsize, uint32_t nentries,
+                            uint32_t chunk, const uint32_t *dpos, const uint32_t *dbase,
+                            int with_entries, kfmi_fmi_t **out);
 uint32_t kfmi_entry_words(uint32_t tag, uint32_t steps, uint32_t chunk);
 uint32_t kfmi_plane_index(uint32_t tag, uint32_t steps, uint32_t nb, uint32_t s, uint32_t t, uint32_t w);
 

@@ -16,6 +16,8 @@
 
 /* ---- stubs for the HIP layer (csrc/hip) ---- */
 int32_t freeIndexGPU(void **index) { (void) index; return KFMI_SUCCESS; }
+int32_t kfmi_host_entries(kfmi_fmi_t *f) { return f->h_index ? KFMI_SUCCESS : KFMI_E_NOT_ON_DEVICE; }
+void kfmi_free_dev_entries(kfmi_fmi_t *f) { f->d_entries = NULL; }
 int32_t freeQueriesGPU(void **q) { (void) q; return KFMI_SUCCESS; }
 int32_t freeResultsGPU(void **r) { (void) r; return KFMI_SUCCESS; }
 kfmi_backend_t kfmi_backend(void) { return KFMI_BK_TASK_MID; }
