@@ -276,18 +276,27 @@ __global__ __launch_bounds__(256) void build_mid_kernel(const uint32_t* __restri
 
 /* GRP layout construction from tag-101 entries (plus the padding entry with
  * the end counters): line b * NGRP + g = [planes of entry b | cnt_b[NCG g ..]]. */
+/* Reads the entries as stored (tag 100 or 101: plane word i of the tag-101
+ * order is word perm[i] of the stored entry), so neither a second copy nor an
+ * interleave pass is needed; entry nent (the padding block) comes from `pad`. */
+struct PlanePerm {
+  uint32_t p[32];
+};
+
 template <int K, int NB>
-__global__ __launch_bounds__(256) void build_grp_kernel(const uint32_t* __restrict__ inter, uint64_t nlines,
-                                                        uint32_t* __restrict__ lines)
+__global__ __launch_bounds__(256) void build_grp_kernel(const uint32_t* __restrict__ ent, uint64_t nent,
+                                                        const uint32_t* __restrict__ pad, PlanePerm perm,
+                                                        uint64_t nlines, uint32_t* __restrict__ lines)
 {
   using GI = Geo<K, NB, LAY_INTER>;
   using GG = Geo<K, NB, LAY_GRP>;
+  static_assert(GI::BMW <= 32, "plane permutation table");
   const uint64_t l = (uint64_t) blockIdx.x * 256 + threadIdx.x;
   if (l >= nlines) return;
   const uint64_t b = l / GG::NGRP, g = l % GG::NGRP;
-  const uint32_t* src = inter + b * GI::EW;
+  const uint32_t* src = b < nent ? ent + b * GI::EW : pad;
   uint32_t* dst = lines + l * GG::EW;
-  for (int i = 0; i < GI::BMW; ++i) dst[i] = src[i];
+  for (int i = 0; i < GI::BMW; ++i) dst[i] = src[perm.p[i]];
   for (int c = 0; c < GG::NCG; ++c) dst[GI::BMW + c] = src[GI::BMW + g * GG::NCG + c];
   for (int i = GI::BMW + GG::NCG; i < GG::EW; ++i) dst[i] = 0;
 }
@@ -445,12 +454,17 @@ static hipError_t dispatch_build_ac128(uint32_t K, uint32_t nb, const uint32_t* 
   return hipErrorInvalidValue;
 }
 
-static hipError_t dispatch_build_grp(uint32_t K, uint32_t nb, const uint32_t* inter, uint64_t nlines, uint32_t* lines,
-                                     hipStream_t st)
+static hipError_t dispatch_build_grp(uint32_t K, uint32_t nb, uint32_t tag, const uint32_t* ent, uint64_t nent,
+                                     const uint32_t* pad, uint64_t nlines, uint32_t* lines, hipStream_t st)
 {
-  if (K != 4 || nb != 2) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((build_grp_kernel<4, 2>), dim3((uint32_t) ((nlines + 255) / 256)), dim3(256), 0, st, inter, nlines,
-                     lines);
+  if (K != 4 || nb != 2 || (tag != 100 && tag != 101)) return hipErrorInvalidValue;
+  PlanePerm perm;
+  for (uint32_t w = 0; w < nb; ++w)
+    for (uint32_t s = 0; s < K; ++s)
+      for (uint32_t t = 0; t < 2; ++t)
+        perm.p[kfmi_plane_index(101, K, nb, s, t, w)] = kfmi_plane_index(tag, K, nb, s, t, w);
+  hipLaunchKernelGGL((build_grp_kernel<4, 2>), dim3((uint32_t) ((nlines + 255) / 256)), dim3(256), 0, st, ent, nent, pad,
+                     perm, nlines, lines);
   return hipGetLastError();
 }
 
@@ -784,19 +798,24 @@ int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx, kfmi_dev_
     const uint32_t lw = (uint32_t) pow2ceil((int) (2 * f->nbitmaps * f->steps + (nc < 16 ? nc : 16)));
     const uint64_t nlines = (uint64_t) (src->nentries + 1) * ngrp;
     end_counters(src, pad.data() + 2 * f->nbitmaps * f->steps);
-    uint32_t* tmp = nullptr;
+    /* entries that already live on this device (built here, no host image) are
+     * read in place; otherwise one staging copy as stored (no interleave pass) */
+    const bool in_place = !src->h_index && src->d_entries && src->d_entries_dev == dev;
+    uint32_t *tmp = nullptr, *d_pad = nullptr;
     di->ent_bytes = 4ull * lw * nlines;
-    if (hipMalloc((void**) &tmp, body + 4ull * ew) != hipSuccess) return fail(KFMI_E_DEVICE_ALLOC);
-    if (hipMalloc((void**) &di->ent, di->ent_bytes) != hipSuccess) {
-      (void) hipFree(tmp);
+    if ((!in_place && hipMalloc((void**) &tmp, body + 16) != hipSuccess) ||
+        hipMalloc((void**) &d_pad, 4ull * ew) != hipSuccess || hipMalloc((void**) &di->ent, di->ent_bytes) != hipSuccess) {
+      if (tmp) (void) hipFree(tmp);
+      if (d_pad) (void) hipFree(d_pad);
       return fail(KFMI_E_DEVICE_ALLOC);
     }
-    bool ok = upload_entries(tmp, src, body, ctx->st) == hipSuccess &&
-              hipMemcpyAsync((uint8_t*) tmp + body, pad.data(), 4ull * ew, hipMemcpyHostToDevice, ctx->st) ==
-                  hipSuccess &&
-              dispatch_build_grp(f->steps, f->nbitmaps, tmp, nlines, di->ent, ctx->st) == hipSuccess &&
+    bool ok = (in_place || entries_in(tmp, src, body, ctx->st) == hipSuccess) &&
+              hipMemcpyAsync(d_pad, pad.data(), 4ull * ew, hipMemcpyHostToDevice, ctx->st) == hipSuccess &&
+              dispatch_build_grp(f->steps, f->nbitmaps, src->tag, in_place ? src->d_entries : tmp, src->nentries, d_pad,
+                                 nlines, di->ent, ctx->st) == hipSuccess &&
               hipStreamSynchronize(ctx->st) == hipSuccess;
-    (void) hipFree(tmp);
+    if (tmp) (void) hipFree(tmp);
+    (void) hipFree(d_pad);
     if (!ok) return fail(KFMI_E_KERNEL);
   } else if (lay == LAY_AC128) {
     /* one line per tag-201 entry (sentinel included) + one padding line, built on

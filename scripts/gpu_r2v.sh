@@ -18,3 +18,9 @@ import json
 b = json.loads(open("$OUT/bench_r2v_n2.json").read().strip().splitlines()[-1])
 print(json.dumps(b["variants"].get("kstep4"))[:1500])
 PY
+cd $R
+timeout -k 10 400 python3 -u -m pytest tests/test_kstep4.py tests/test_device_resident.py tests/test_remainder.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/gpu_tests_r2v.log 2>&1 || { tail -40 $OUT/gpu_tests_r2v.log; exit 34; }
+tail -2 $OUT/gpu_tests_r2v.log
+cd /tmp
+timeout -k 10 300 python3 -u $R/scripts/k4_upload_probe.py > $OUT/k4_upload_r2v.txt 2>&1 || { tail -20 $OUT/k4_upload_r2v.txt; exit 35; }
+cat $OUT/k4_upload_r2v.txt
