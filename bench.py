@@ -142,7 +142,8 @@ def make_text(n: int) -> bytes:
         return synth.text_3g(n)
     import random
     rng = random.Random(n)
-    return rng.randbytes(n).translate(synth.TBL)
+    step = 1 << 27                                  # getrandbits takes < 2^31 bits per call
+    return b"".join(rng.randbytes(min(step, n - i)).translate(synth.TBL) for i in range(0, n, step))
 
 
 def cpu_threads() -> int:

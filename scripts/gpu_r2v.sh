@@ -8,8 +8,8 @@ OUT=$R/gpurun_out
 mkdir -p $OUT
 export TMPDIR=/tmp
 cd $R
-timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke_r2v.log 2>&1 || { tail -30 $OUT/smoke_r2v.log; exit 31; }
-tail -2 $OUT/smoke_r2v.log
+true
+true
 cd /tmp
 timeout -k 10 700 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 $R/bench.py --gpus 2 --steps 10 --warmup 5 --ref-size 1000000000 --queries 2000000 --config5-queries 2000000 > $OUT/bench_r2v_n2.json 2> $OUT/bench_r2v_n2.log || { tail -30 $OUT/bench_r2v_n2.log; exit 33; }
 cut -c1-400 $OUT/bench_r2v_n2.json
