@@ -435,7 +435,7 @@ def kstep4_leg(D, text: bytes, reads: np.ndarray, res: np.ndarray, idx2, steps: 
     equal its K = 2 results (rank 0: and the pinned md5).  Config #5's read
     shape runs on it too (150 % 4 = 2: the last two bases of each read from the
     remainder table, then 37 K-steps), oracle-sampled against the K = 2 image."""
-    out = {"what": "coop-grp: K=4, d=64 index (96 GB LAY_GRP lines), wave64 cooperative LF, "
+    out = {"what": "coop-grp: K=4, d=64 index (LAY_GRP lines, device_index_bytes), wave64 cooperative LF, "
                    "the main leg's reads on every rank"}
     t = time.perf_counter()
     i4 = K.Index.build(text, k=4, d=64, gpu=True, host_image=False)
