@@ -188,9 +188,12 @@ uint32_t *kfmi_results_host(void *results);      /* 2*num u32, [L0,R0,L1,R1,...]
 uint64_t  kfmi_results_num(void *results);
 
 /* Index construction (genFMindex.c:457-543) from an ACGT text of n bases.
- * _gpu: suffix sort and all layout passes on the device; the tag-100 host
- * image is produced as well when `want_host_image` != 0 (needed for
- * saveIndex / md5 pinning / the CPU oracle).  Returns a tag-100 index. */
+ * _gpu: suffix sort and all layout passes on the device.  want_host_image != 0
+ * copies the tag-100 image to host memory at once; 0 keeps the entries in HBM
+ * only (the handle owns them): transferCPUtoGPU then lays them out device to
+ * device, and the host image is fetched on first use (kfmi_index_image,
+ * saveIndex, the transforms, the AltCounters layouts).  Returns a tag-100
+ * index. */
 int32_t kfmi_build_index_cpu(const char *text, uint64_t n, uint32_t k, uint32_t d, void **index);
 int32_t kfmi_build_index_gpu(const char *text, uint64_t n, uint32_t k, uint32_t d,
                              int32_t want_host_image, void **index);
