@@ -124,7 +124,9 @@ char    *errorCommon(int32_t e);
  *   "task-ac-mid" / "coop-ac-mid" the MID128 lines with AltCounters semantics: the AltCounters
  *                 step only past the last real block, from the tfmiAC sentinel (tag 201 semantics;
  *                 built from a tag 100/101 file, an AC file returns 101)
- * The default comes from KFMI_BACKEND, else "task-mid".  transferCPUtoGPU
+ * The default comes from KFMI_BACKEND, else "task-mid" -- and "coop-grp" for a
+ * K = 4 index while neither KFMI_BACKEND nor kfmi_set_backend has chosen one
+ * (kfmi_get_backend still names the selection).  transferCPUtoGPU
  * re-lays-out the loaded index for the backend: plain-counter backends take
  * tag 100 or 101 (an AC file returns 101, as the reference loader would);
  * AC backends take any tag -- a tag-100/101 file first goes through the tfmiAC

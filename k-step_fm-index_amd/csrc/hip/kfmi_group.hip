@@ -156,7 +156,7 @@ static int32_t each_member(int n, F fn)
 
 int32_t group_transfer(kfmi_fmi_t* f, kfmi_qrys_t* q, kfmi_res_t* r, const int* devs, int n)
 {
-  const int backend = kfmi_backend();
+  const int backend = f ? backend_for(f->steps) : kfmi_backend();
   int32_t err = KFMI_SUCCESS;
   if (f) {
     GroupIndex* g = (GroupIndex*) f->grp;

@@ -89,6 +89,7 @@ uint32_t ftab_bases(void);
 
 /* backends and kernel dispatch (kfmi_search.hip) */
 bool is_coop(int backend);
+int backend_for(uint32_t K);   /* the selected backend, or coop-grp for K = 4 under the implicit default */
 int fused_maxw(int backend, uint32_t nwords);
 hipError_t dispatch(Op op, uint32_t K, uint32_t nb, int lay, const SearchLaunch& a,
                     unsigned long long* d_total = nullptr);

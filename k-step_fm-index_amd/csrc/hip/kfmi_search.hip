@@ -39,6 +39,7 @@ static const char* kBackendNames[KFMI_BK_COUNT] = {
     "task-ac128", "coop-ac128", "task-ac-mid", "coop-ac-mid", "task-grp", "coop-grp"};
 
 static thread_local int t_backend = -1;
+static thread_local bool t_backend_implicit = true;   /* neither KFMI_BACKEND nor kfmi_set_backend chose it */
 thread_local int t_device = -1;
 thread_local int32_t t_last_error = KFMI_SUCCESS;
 thread_local double t_ms[3] = {0, 0, 0};
@@ -63,8 +64,18 @@ extern "C" kfmi_backend_t kfmi_backend(void)
   if (t_backend < 0) {
     int b = backend_from_name(getenv("KFMI_BACKEND"));
     t_backend = b >= 0 ? b : KFMI_BK_TASK_MID;
+    t_backend_implicit = b < 0;
   }
   return (kfmi_backend_t) t_backend;
+}
+
+/* The backend an index of K-steps is uploaded for: the selected one, except
+ * that the implicit default (task-mid, K <= 2) becomes coop-grp for K = 4
+ * indexes, the one layout those run on at speed. */
+int backend_for(uint32_t K)
+{
+  const int b = kfmi_backend();
+  return (t_backend_implicit && K == 4) ? (int) KFMI_BK_COOP_GRP : b;
 }
 
 extern "C" uint32_t kfmi_backend_tag(kfmi_backend_t b)
@@ -79,6 +90,7 @@ extern "C" int32_t kfmi_set_backend(const char* name)
   int b = backend_from_name(name);
   if (b < 0) return KFMI_E_BAD_ARGUMENT;
   t_backend = b;
+  t_backend_implicit = false;
   return KFMI_SUCCESS;
 }
 
@@ -1117,7 +1129,7 @@ extern "C" int32_t transferCPUtoGPU(void* index, void* queries, void* results)
   DevCtx* ctx = nullptr;
   int32_t err = ctx_for(dev, &ctx);
   if (err) return err;
-  const int backend = kfmi_backend();
+  const int backend = f ? backend_for(f->steps) : kfmi_backend();
   if (f && (!f->dev || f->dev->backend != backend || f->dev->device != dev)) {
     err = upload_index(f, backend, dev, ctx);
     if (err) return err;

@@ -162,3 +162,30 @@ def test_grp_locate_against_bruteforce(kfmi_mod):
     for i in range(q.shape[0]):
         L, R = int(res[2 * i]), int(res[2 * i + 1])
         assert list(pos[off[i]:off[i + 1]]) == [int(x) for x in sa[L:R]], i
+
+
+@pytest.mark.gpu
+def test_k4_index_under_the_implicit_default_backend(kfmi_mod, oracle_mod, tmp_path):
+    """No KFMI_BACKEND, no kfmi_set_backend: a K = 4 index is uploaded for
+    coop-grp (the default task-mid has no K = 4 geometry).  Fresh process, so
+    the thread's backend is still the implicit one."""
+    t = _text(100_003, 12)
+    q = _reads(t, 2000, 100, 12)
+    np.save(tmp_path / "q.npy", q)
+    (tmp_path / "t.bin").write_bytes(t.tobytes())
+    code = f"""
+import sys, numpy as np
+sys.path.insert(0, {str(util.PKG)!r})
+import kstep_fmi as K
+K.load(); K.set_device(0)
+i4 = K.Index.build(open({str(tmp_path / "t.bin")!r}, "rb").read(), k=4, d=64)
+q = np.load({str(tmp_path / "q.npy")!r})
+np.save({str(tmp_path / "got.npy")!r}, K.search_array(i4, q))
+print(K.get_backend())
+"""
+    env = {k: v for k, v in __import__("os").environ.items() if k != "KFMI_BACKEND"}
+    p = subprocess.run([__import__("sys").executable, "-c", code], capture_output=True, text=True, env=env, timeout=120)
+    assert p.returncode == 0, p.stderr[-2000:]
+    i4 = kfmi_mod.Index.build(t.tobytes(), k=4, d=64)
+    want, _ = oracle_mod.search(i4.image(), q)
+    assert np.array_equal(np.load(tmp_path / "got.npy"), want)
