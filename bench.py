@@ -474,6 +474,13 @@ def kstep4_leg(D, text: bytes, reads: np.ndarray, res: np.ndarray, idx2, steps: 
                            "achieved_GBs": round(bytes_alg / (lfm / 1e3) / 1e9, 1),
                            "frac": round(bytes_alg / (lfm / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
                            "note": "rank 0's launch"}
+        if D.world == 1:
+            # opt-in jump start on the K = 4 index: the first 16 bases
+            # (4 K-steps, most with L and R in different blocks) from a 34 GB table
+            wall, lf1, tot1 = time_backend(i4, q, r, "coop-grp+ftab16", steps, 5)
+            out["coop-grp+ftab16"] = {"mqps": round(reads.shape[0] * steps / wall / 1e6, 2), "lf_ms": round(lf1, 3),
+                                      "results_equal_k2": bool(np.array_equal(r.array(), res)),
+                                      "device_bytes_incl_ftab": i4.device_bytes() + 8 * 4 ** 16}
         q.close()
         r.close()
         q = r = None
