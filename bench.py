@@ -381,7 +381,7 @@ def config1_leg(backend: str, thr: int, steps: int = 5) -> dict:
 
 
 def config5_leg(D, idx, text: bytes, backend: str, qlen: int, nq: int, steps: int, warmup: int, ac: bool,
-                oracle_idx=None) -> dict:
+                oracle_idx=None, ingest: bool = False) -> dict:
     """BASELINE config #5's read shape on every rank: this rank's shard of nq
     reads of qlen bases (seed 20 + rank; 10M x 150 bp = one eighth of the
     80M x 150 bp batch at N = 8), searched on the resident index; timed like
@@ -418,10 +418,19 @@ def config5_leg(D, idx, text: bytes, backend: str, qlen: int, nq: int, steps: in
     total = D.sum(float(nq))
     q.close()
     r.close()
-    return {"what": f"config #5 shape: {nq // 1_000_000}M x {qlen} bp reads per GPU (seed 20 + rank), "
-                    f"{D.world} GPU(s), index replicated",
-            "mqps": round(total * steps / el / 1e6, 2), "ms_per_step": round(el / steps * 1e3, 4),
-            "lf_ms_per_rank": lfs, "oracle_sample_ok_per_rank": oks, "oracle_sample_per_rank": int(sel.size)}
+    out = {"what": f"config #5 shape: {nq // 1_000_000}M x {qlen} bp reads per GPU (seed 20 + rank), "
+                   f"{D.world} GPU(s), index replicated",
+           "mqps": round(total * steps / el / 1e6, 2), "ms_per_step": round(el / steps * 1e3, 4),
+           "lf_ms_per_rank": lfs, "oracle_sample_ok_per_rank": oks, "oracle_sample_per_rank": int(sel.size)}
+    if ingest:
+        # this rank's shard as a FASTA file -> results (host parser and device parser)
+        try:
+            ing = ingest_leg(idx, reads, res, D.world)
+        except Exception as e:          # auxiliary (e.g. TMPDIR full): report, never abort the bench
+            ing = {"error": repr(e)}
+            os.environ.pop("KFMI_LOAD_MMAP", None)
+        out["ingest_file_per_rank"] = D.gather(ing)
+    return out
 
 
 def kstep4_leg(D, text: bytes, reads: np.ndarray, res: np.ndarray, idx2, steps: int, pinned_md5: str | None,
@@ -640,7 +649,7 @@ def main():
         try:
             c5 = config5_leg(D, idx, text, a.backend, a.config5_qlen, a.config5_queries, a.steps, 5,
                              a.backend in ("task-ac", "coop-ac", "task-ac128", "coop-ac128", "task-ac-mid",
-                                           "coop-ac-mid"))
+                                           "coop-ac-mid"), ingest=a.ingest)
             log(f"rank {D.rank}: config #5 leg {c5}")
         except K.KfmiError as e:
             c5 = {"error": str(e)}
