@@ -27,6 +27,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <algorithm>
+#include <mutex>
 #include <vector>
 
 #include "../kfmi_internal.h"
@@ -644,6 +645,8 @@ extern "C" int32_t kfmi_build_index_gpu(const char* text, uint64_t n, uint32_t k
 extern "C" int32_t kfmi_host_entries(kfmi_fmi_t* f)
 {
   if (!f) return KFMI_E_BAD_ARGUMENT;
+  static std::mutex mu;   /* two threads asking for the same handle's image fetch it once */
+  std::lock_guard<std::mutex> lk(mu);
   if (f->h_index) return KFMI_SUCCESS;
   if (!f->d_entries) return KFMI_E_BAD_ARGUMENT;
   const uint64_t body = 4ull * f->entry_words * f->nentries;

@@ -508,7 +508,7 @@ bool is_coop(int backend)
  * cnt_{E-1} + rows of each code in the last block, $ rows excluded.  Used for
  * the padding entry that keeps R/d == nentries in bounds when (n+1) % d == 0
  * (reference defect B5: it reads past the end there). */
-static void end_counters(const kfmi_fmi_t* f, uint32_t* out)
+static bool end_counters(const kfmi_fmi_t* f, uint32_t* out)
 {
   const uint32_t nc = 1u << (2 * f->steps), nb = f->nbitmaps;
   const uint32_t last = f->nentries - 1;
@@ -519,11 +519,10 @@ static void end_counters(const kfmi_fmi_t* f, uint32_t* out)
   } else {   /* entries only in HBM: fetch the last one */
     dev_last.assign(f->entry_words, 0u);
     int cur = 0;
-    (void) hipGetDevice(&cur);
-    (void) hipSetDevice(f->d_entries_dev);
-    (void) hipMemcpy(dev_last.data(), f->d_entries + (uint64_t) last * f->entry_words, 4ull * f->entry_words,
-                     hipMemcpyDeviceToHost);
-    (void) hipSetDevice(cur);
+    if (hipGetDevice(&cur) != hipSuccess || hipSetDevice(f->d_entries_dev) != hipSuccess) return false;
+    const hipError_t ce = hipMemcpy(dev_last.data(), f->d_entries + (uint64_t) last * f->entry_words,
+                                    4ull * f->entry_words, hipMemcpyDeviceToHost);
+    if (hipSetDevice(cur) != hipSuccess || ce != hipSuccess) return false;
     e = dev_last.data();
   }
   const uint32_t o = f->bwtsize - last * f->chunk;  /* rows of the last block, in (0, d] */
@@ -544,6 +543,7 @@ static void end_counters(const kfmi_fmi_t* f, uint32_t* out)
       if (f->modposdollarBWT[s] == last && f->dollarBaseBWT[s] == c && f->bwtsize > f->dollarPositionBWT[s]) pop--;
     out[c] = e[2 * nb * f->steps + c] + pop;
   }
+  return true;
 }
 
 /* Host image of the entries for a layout, converting tags as needed.
@@ -796,7 +796,7 @@ int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx, kfmi_dev_
     /* entries + 2 padding entries (B5 guard; AC may look at b+1 of the sentinel) */
     di->ent_bytes = body + 4ull * ew * 2;
     if (hipMalloc((void**) &di->ent, di->ent_bytes) != hipSuccess) return fail(KFMI_E_DEVICE_ALLOC);
-    if (lay == LAY_INTER) end_counters(src, pad.data() + 2 * f->nbitmaps * f->steps);
+    if (lay == LAY_INTER && !end_counters(src, pad.data() + 2 * f->nbitmaps * f->steps)) return fail(KFMI_E_KERNEL);
     if (upload_entries(di->ent, src, body, ctx->st) != hipSuccess ||
         hipMemcpyAsync((uint8_t*) di->ent + body, pad.data(), 4ull * ew * 2, hipMemcpyHostToDevice, ctx->st) !=
             hipSuccess ||
@@ -809,7 +809,7 @@ int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx, kfmi_dev_
     const uint32_t ngrp = nc < 16 ? 1u : nc / 16;
     const uint32_t lw = (uint32_t) pow2ceil((int) (2 * f->nbitmaps * f->steps + (nc < 16 ? nc : 16)));
     const uint64_t nlines = (uint64_t) (src->nentries + 1) * ngrp;
-    end_counters(src, pad.data() + 2 * f->nbitmaps * f->steps);
+    if (!end_counters(src, pad.data() + 2 * f->nbitmaps * f->steps)) return fail(KFMI_E_KERNEL);
     /* entries that already live on this device (built here, no host image) are
      * read in place; otherwise one staging copy as stored (no interleave pass) */
     const bool in_place = !src->h_index && src->d_entries && src->d_entries_dev == dev;
@@ -856,7 +856,7 @@ int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx, kfmi_dev_
     const uint32_t nl = nreal + 1;
     const uint32_t lw = (uint32_t) pow2ceil((int) (2 * 2 * f->nbitmaps * f->steps + nc));
     std::vector<uint32_t> endc(nc), ext(2 * nc);
-    end_counters(src, endc.data());
+    if (!end_counters(src, endc.data())) return fail(KFMI_E_KERNEL);
     const uint64_t n1 = f->bwtsize;                                   /* n + 1 */
     const uint64_t mid_last = (uint64_t) E * f->chunk;               /* midpoint of line nreal-1 when E is odd */
     const uint64_t mid_pad = (uint64_t) nreal * 2 * f->chunk + f->chunk;
@@ -900,7 +900,7 @@ int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx, kfmi_dev_
     const uint32_t pw = (uint32_t) pow2ceil((int) (2 * f->nbitmaps * f->steps + nc / 2));
     const int S = sb_shift_for((int) f->chunk);
     const uint64_t nsb = ((uint64_t) ne + (1u << S) - 1) >> S;
-    end_counters(src, pad.data() + 2 * f->nbitmaps * f->steps);
+    if (!end_counters(src, pad.data() + 2 * f->nbitmaps * f->steps)) return fail(KFMI_E_KERNEL);
     di->ent_bytes = 4ull * pw * (ne + 1);
     di->sb_bytes = 4ull * nc * nsb;
     if (hipMalloc((void**) &tmp, 4ull * ew * ne) != hipSuccess) return fail(KFMI_E_DEVICE_ALLOC);
