@@ -100,18 +100,18 @@ __device__ __forceinline__ uint32_t coop_lf(const IdxArgs& ix, const uint8_t* sl
         if constexpr (G::LAY == LAY_MIDAC) all += __popc(sel);
       }
     }
-  } else {   // K > 2: one 32-row word spans PW / 4 chunks
+  } else {   // K > 2: the block's BMW plane words (a 32-row word may straddle chunks at K = 3)
+    uint32_t pl[G::BMW];
+#pragma unroll
+    for (int k = 0; k < C::BC; ++k) {
+      const uint4 v = *reinterpret_cast<const uint4*>(slot + 16 * k);
+      pl[4 * k] = v.x; pl[4 * k + 1] = v.y; pl[4 * k + 2] = v.z; pl[4 * k + 3] = v.w;
+    }
 #pragma unroll
     for (int w = 0; w < G::NB; ++w) {
-      uint32_t pl[G::PW];
-#pragma unroll
-      for (int k = 0; k < G::PW / 4; ++k) {
-        const uint4 v = *reinterpret_cast<const uint4*>(slot + 16 * (w * (G::PW / 4) + k));
-        pl[4 * k] = v.x; pl[4 * k + 1] = v.y; pl[4 * k + 2] = v.z; pl[4 * k + 3] = v.w;
-      }
       uint32_t m = row_mask(o - 32 * w);
       if constexpr (G::TWO_SIDED) m = e ? ~m : m;
-      pop += __popc(m & select_rows<G::K>(pl, sx));
+      pop += __popc(m & select_rows<G::K>(&pl[w * G::PW], sx));
     }
   }
   uint32_t cnt;
@@ -147,7 +147,8 @@ __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, 
                                                                     uint32_t* __restrict__ res)
 {
   using C = CoopCfg<G>;
-  constexpr int CW = MAXW > 0 ? MAXW : 1;
+  constexpr int RW = MAXW > 0 ? MAXW : 1;                                   // 16 bases per word
+  constexpr int CW = MAXW > 0 && G::K == 3 ? k3_words<RW>() : RW;           // SPW K-steps per word
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
@@ -163,6 +164,7 @@ __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, 
   uint32_t cw[CW];
   uint32_t rc = 0;
   if constexpr (MAXW > 0) {
+    uint32_t raw[RW];
     const uint32_t rpr = coop_stage_rows<G>(m);
 #pragma unroll 1
     for (uint32_t h = 0; h < 64u / rpr; ++h) {
@@ -173,15 +175,20 @@ __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, 
       for (uint32_t i = lane; i < n16; i += 64) reinterpret_cast<uint4*>(wl)[i] = src[i];
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       if ((uint32_t) lane / rpr == h) {   // K-step stream of bases 0 .. m-rem-1; the last rem apart
-        row_codes<MAXW>(wl, (uint64_t) (lane % rpr) * m, m - ix.rem, cw);
+        row_codes<MAXW>(wl, (uint64_t) (lane % rpr) * m, m - ix.rem, raw);
         rc = rem_code(wl + (uint64_t) (lane % rpr) * m + m - ix.rem, ix.rem);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
     if (q >= num) {
 #pragma unroll
-      for (int i = 0; i < CW; ++i) cw[i] = 0;
+      for (int i = 0; i < RW; ++i) raw[i] = 0;
       rc = 0;
+    }
+    if constexpr (G::K == 3) recut30<RW>(raw, cw);
+    else {
+#pragma unroll
+      for (int i = 0; i < CW; ++i) cw[i] = raw[i];
     }
   }
   uint32_t L = 0, R = ix.bwtsize;

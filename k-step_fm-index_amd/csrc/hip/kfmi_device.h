@@ -206,6 +206,24 @@ __device__ __forceinline__ uint32_t rem_code(const uint8_t* __restrict__ p, uint
   return c;
 }
 
+// K = 3: a K-step is 6 bits, so the pack kernel's words hold 5 steps (30 bits,
+// SPW = 5) while the fused packers produce 16 bases per word; recut30 re-cuts
+// the stream into 30-bit words with compile-time shifts (registers only).
+template <int MAXW>
+__host__ __device__ constexpr int k3_words() { return (MAXW * 32 + 29) / 30; }
+
+template <int MAXW>
+__device__ __forceinline__ void recut30(const uint32_t (&in)[MAXW], uint32_t (&out)[k3_words<MAXW>()])
+{
+#pragma unroll
+  for (int j = 0; j < k3_words<MAXW>(); ++j) {
+    const int bit = 30 * j, w = bit >> 5, sh = bit & 31;
+    const uint32_t lo = w < MAXW ? in[w] : 0u;
+    const uint32_t hi = w + 1 < MAXW ? in[w + 1] : 0u;
+    out[j] = (sh ? ((lo >> sh) | (hi << (32 - sh))) : lo) & 0x3FFFFFFFu;
+  }
+}
+
 // Fused query packing for a 256-thread block, one query per thread: each
 // wave copies its rows HBM -> LDS with coalesced 16-byte loads, RPR rows per
 // round, and the lanes owning those rows convert them from LDS (a lane reading

@@ -230,6 +230,7 @@ extern "C" int32_t kfmi_load_queries_gpu(const char* fn, uint32_t sizequery, uin
   if (hipMalloc((void**) &dq->ascii, ((abytes + 3) & ~3ull) + 16) != hipSuccess ||
       hipMalloc((void**) &dq->packed, 4ull * (dq->nwords + 1) * (num ? num : 1)) != hipSuccess)
     return fail(KFMI_E_DEVICE_ALLOC);
+  dq->packed_rows = dq->nwords + 1;
   if (num) {
     if (starts.alloc(8 * num) != hipSuccess) return fail(KFMI_E_DEVICE_ALLOC);
     unsigned long long fb = ~0ull;

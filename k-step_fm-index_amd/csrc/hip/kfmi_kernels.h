@@ -30,14 +30,20 @@ __global__ __launch_bounds__(256) void task_kernel(IdxArgs ix, const uint32_t* _
                                                    uint32_t steps, uint32_t nwords, uint32_t* __restrict__ res)
 {
   constexpr int SPW = G::SPW;
-  constexpr int CW = MAXW > 0 ? MAXW : 1;
+  constexpr int CW = MAXW > 0 ? (G::K == 3 ? k3_words<(MAXW > 0 ? MAXW : 1)>() : MAXW) : 1;
   static_assert(MAXW == 0 || QPT == 1, "fused packing: one query per thread");
   const uint64_t base = (uint64_t) blockIdx.x * (256 * QPT) + threadIdx.x;
   uint32_t cw[QPT][CW];
   uint32_t rc = 0;
   if constexpr (MAXW > 0) {
     extern __shared__ __attribute__((aligned(16))) uint8_t stage[];
-    stage_query_codes<MAXW>(ascii, num, m, stage, cw[0], ix.rem, rc);   /* whole block, before any exit */
+    if constexpr (G::K == 3) {   /* 16 bases per word -> 5 K-steps per word */
+      uint32_t raw[MAXW];
+      stage_query_codes<MAXW>(ascii, num, m, stage, raw, ix.rem, rc);   /* whole block, before any exit */
+      recut30<MAXW>(raw, cw[0]);
+    } else {
+      stage_query_codes<MAXW>(ascii, num, m, stage, cw[0], ix.rem, rc);   /* whole block, before any exit */
+    }
   }
   if (base >= num) return;
   uint64_t q[QPT];

@@ -67,6 +67,7 @@ struct kfmi_dev_queries {
   /* m = size = rem + K * steps: the last rem (< K) bases of a read are resolved
    * by one remainder-table lookup before its K-steps (query_geometry) */
   uint32_t size = 0, K = 0, steps = 0, nwords = 0, rem = 0;
+  uint32_t packed_rows = 0;    /* rows allocated in `packed` (>= nwords + 1) */
 };
 
 namespace kfmi {
@@ -90,7 +91,7 @@ uint32_t ftab_bases(void);
 /* backends and kernel dispatch (kfmi_search.hip) */
 bool is_coop(int backend);
 int backend_for(uint32_t K);   /* the selected backend, or coop-grp for K = 4 under the implicit default */
-int fused_maxw(int backend, uint32_t nwords);
+int fused_maxw(int backend, uint32_t bases);   /* bases = K * steps of the batch */
 hipError_t dispatch(Op op, uint32_t K, uint32_t nb, int lay, const SearchLaunch& a,
                     unsigned long long* d_total = nullptr);
 IdxArgs idx_args(const kfmi_dev_index* di);

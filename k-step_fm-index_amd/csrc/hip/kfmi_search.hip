@@ -70,12 +70,12 @@ extern "C" kfmi_backend_t kfmi_backend(void)
 }
 
 /* The backend an index of K-steps is uploaded for: the selected one, except
- * that the implicit default (task-mid, K <= 2) becomes coop-grp for K = 4
+ * that the implicit default (task-mid, K <= 2) becomes coop-grp for K = 3, 4
  * indexes, the one layout those run on at speed. */
 int backend_for(uint32_t K)
 {
   const int b = kfmi_backend();
-  return (t_backend_implicit && K == 4) ? (int) KFMI_BK_COOP_GRP : b;
+  return (t_backend_implicit && (K == 3 || K == 4)) ? (int) KFMI_BK_COOP_GRP : b;
 }
 
 extern "C" uint32_t kfmi_backend_tag(kfmi_backend_t b)
@@ -338,12 +338,14 @@ __global__ __launch_bounds__(256) void build_ac128_kernel(const uint32_t* __rest
 
 /* Code registers the task kernel needs to pack a query itself (0: use the
  * pack kernel).  KFMI_FUSED=0 forces the separate pack launch. */
-int fused_maxw(int backend, uint32_t nwords)
+/* Fused packing keeps 16 bases per register word (MAXW words): 8 words up to
+ * 128 K-step bases, 16 up to 256, else the pack kernel. */
+int fused_maxw(int backend, uint32_t bases)
 {
   (void) backend;   /* task and coop kernels both pack in-kernel (m <= 256 fits either's LDS staging) */
   const char* e = getenv("KFMI_FUSED");
   if (e && !atoi(e)) return 0;
-  return nwords <= 8 ? 8 : (nwords <= 16 ? 16 : 0);
+  return bases <= 128 ? 8 : (bases <= 256 ? 16 : 0);
 }
 
 static bool nb_supported(uint32_t nb)
@@ -366,6 +368,7 @@ KFMI_FOR_NB(KFMI_EXTERN, 2, LAY_AC128)
 KFMI_FOR_NB(KFMI_EXTERN, 1, LAY_MIDAC)
 KFMI_FOR_NB(KFMI_EXTERN, 2, LAY_MIDAC)
 KFMI_EXTERN(4, 2, LAY_GRP)
+KFMI_EXTERN(3, 2, LAY_GRP)
 
 hipError_t dispatch(Op op, uint32_t K, uint32_t nb, int lay, const SearchLaunch& a, unsigned long long* d_total)
 {
@@ -384,6 +387,7 @@ hipError_t dispatch(Op op, uint32_t K, uint32_t nb, int lay, const SearchLaunch&
   KFMI_FOR_NB(KFMI_CASE, 1, LAY_MIDAC)
   KFMI_FOR_NB(KFMI_CASE, 2, LAY_MIDAC)
   KFMI_CASE(4, 2, LAY_GRP)
+  KFMI_CASE(3, 2, LAY_GRP)
 #undef KFMI_CASE
   return hipErrorInvalidValue;
 }
@@ -394,9 +398,9 @@ bool is_coop(int backend);
  * kernel needs 16-byte-aligned chunks, CoopCfg::OK). */
 static bool geometry_supported(int backend, uint32_t K, uint32_t nb, int lay)
 {
-  if (lay == LAY_GRP) {   /* instantiated for K = 4, d = 64 only (K <= 2 has the MID128 lines) */
-    if (K != 4 || nb != 2) return false;
-    return !is_coop(backend) || CoopCfg<Geo<4, 2, LAY_GRP>>::OK;
+  if (lay == LAY_GRP) {   /* instantiated for K = 3, 4 with d = 64 (K <= 2 has the MID128 lines) */
+    if ((K != 3 && K != 4) || nb != 2) return false;
+    return !is_coop(backend) || (K == 4 ? CoopCfg<Geo<4, 2, LAY_GRP>>::OK : CoopCfg<Geo<3, 2, LAY_GRP>>::OK);
   }
   if (!nb_supported(nb) || (K != 1 && K != 2)) return false;
   if (!is_coop(backend)) return true;
@@ -469,14 +473,17 @@ static hipError_t dispatch_build_ac128(uint32_t K, uint32_t nb, const uint32_t* 
 static hipError_t dispatch_build_grp(uint32_t K, uint32_t nb, uint32_t tag, const uint32_t* ent, uint64_t nent,
                                      const uint32_t* pad, uint64_t nlines, uint32_t* lines, hipStream_t st)
 {
-  if (K != 4 || nb != 2 || (tag != 100 && tag != 101)) return hipErrorInvalidValue;
+  if ((K != 3 && K != 4) || nb != 2 || (tag != 100 && tag != 101)) return hipErrorInvalidValue;
   PlanePerm perm;
   for (uint32_t w = 0; w < nb; ++w)
     for (uint32_t s = 0; s < K; ++s)
       for (uint32_t t = 0; t < 2; ++t)
         perm.p[kfmi_plane_index(101, K, nb, s, t, w)] = kfmi_plane_index(tag, K, nb, s, t, w);
-  hipLaunchKernelGGL((build_grp_kernel<4, 2>), dim3((uint32_t) ((nlines + 255) / 256)), dim3(256), 0, st, ent, nent, pad,
-                     perm, nlines, lines);
+  const dim3 grid((uint32_t) ((nlines + 255) / 256));
+  if (K == 4)
+    hipLaunchKernelGGL((build_grp_kernel<4, 2>), grid, dim3(256), 0, st, ent, nent, pad, perm, nlines, lines);
+  else
+    hipLaunchKernelGGL((build_grp_kernel<3, 2>), grid, dim3(256), 0, st, ent, nent, pad, perm, nlines, lines);
   return hipGetLastError();
 }
 
@@ -1078,6 +1085,7 @@ int32_t upload_queries(kfmi_qrys_t* q, uint32_t K, int dev, DevCtx* ctx)
     free_dev_queries(dq);
     return KFMI_E_DEVICE_ALLOC;
   }
+  dq->packed_rows = dq->nwords + 1;
   if (abytes && (h2d(dq->ascii, q->h_queries, abytes, ctx->st) != hipSuccess ||
                  hipStreamSynchronize(ctx->st) != hipSuccess)) {
     free_dev_queries(dq);
@@ -1100,6 +1108,9 @@ hipError_t launch_pack(const kfmi_dev_queries* dq, hipStream_t st)
                        dq->size, dq->steps, dq->nwords, tq, dq->packed, dq->rem);
   else if (dq->K == 4)
     hipLaunchKernelGGL((pack_queries_kernel<4>), dim3((uint32_t) blocks), dim3(256), lds, st, dq->ascii, dq->num,
+                       dq->size, dq->steps, dq->nwords, tq, dq->packed, dq->rem);
+  else if (dq->K == 3)
+    hipLaunchKernelGGL((pack_queries_kernel<3>), dim3((uint32_t) blocks), dim3(256), lds, st, dq->ascii, dq->num,
                        dq->size, dq->steps, dq->nwords, tq, dq->packed, dq->rem);
   else
     hipLaunchKernelGGL((pack_queries_kernel<2>), dim3((uint32_t) blocks), dim3(256), lds, st, dq->ascii, dq->num,
@@ -1140,6 +1151,15 @@ extern "C" int32_t transferCPUtoGPU(void* index, void* queries, void* results)
       if (!q->dev) return KFMI_E_NOT_ON_DEVICE;
       if (q->dev->device != dev) return KFMI_E_BAD_ARGUMENT;
       query_geometry(q->dev, f->steps);
+      kfmi_dev_queries* dq = q->dev;
+      if (dq->nwords + 1 > dq->packed_rows) {   /* K = 3 packs 15 bases per word: a few more rows */
+        (void) hipFree(dq->packed);
+        dq->packed = nullptr;
+        dq->packed_rows = 0;
+        if (hipMalloc((void**) &dq->packed, 4ull * (dq->nwords + 1) * (dq->num ? dq->num : 1)) != hipSuccess)
+          return KFMI_E_DEVICE_ALLOC;
+        dq->packed_rows = dq->nwords + 1;
+      }
     } else {
       err = upload_queries(q, f->steps, dev, ctx);
       if (err) return err;
@@ -1166,7 +1186,7 @@ extern "C" int32_t transferCPUtoGPU(void* index, void* queries, void* results)
 static bool reorder_wanted(const kfmi_dev_index* di, const kfmi_dev_queries* dq, int maxw, bool ftab)
 {
   const char* e = getenv("KFMI_REORDER");
-  return e && atoi(e) && !is_coop(di->backend) && maxw == 8 && !ftab && dq->num > 0 &&
+  return e && atoi(e) && !is_coop(di->backend) && maxw == 8 && !ftab && di->K != 3 && dq->num > 0 &&
          dq->num < 0xFFFFFFFFull;
 }
 
@@ -1219,7 +1239,7 @@ int32_t search_enqueue(kfmi_dev_index* di, kfmi_dev_queries* dq, uint32_t* d_res
   a.qp = dq->packed;
   a.ascii = dq->ascii;
   a.m = dq->size;
-  a.maxw = fused_maxw(di->backend, dq->nwords);
+  a.maxw = fused_maxw(di->backend, dq->K * dq->steps);
   a.num = dq->num;
   a.steps = dq->steps;
   a.nwords = dq->nwords;

@@ -321,7 +321,9 @@ extern "C" int32_t kfmi_search_stream(void* index, const char* ascii, uint64_t n
    * previous chunks -- on a box whose host packs slower than the link carries
    * ASCII, part of the batch goes as ASCII while the host packs the rest. */
   const char* hp = getenv("KFMI_STREAM_HOSTPACK");
-  const int mode = hp ? atoi(hp) : 2;
+  /* K = 3: the host packer writes 16 bases per word, the K = 3 kernels read 5
+   * K-steps per word -- every chunk goes as ASCII (packed in the kernel) */
+  const int mode = K == 3 ? 0 : (hp ? atoi(hp) : 2);
   const bool any_pack = mode != 0, any_ascii = mode != 1;
   const uint64_t def_chunk = any_pack ? (1ull << 19) : (1ull << 16);   /* profiles/r01/e2e_sweep*.jsonl */
   if (chunk == 0) {
@@ -419,7 +421,7 @@ extern "C" int32_t kfmi_search_stream(void* index, const char* ascii, uint64_t n
     a.qp = s.dq.packed;
     a.ascii = s.dq.ascii;
     a.m = size;
-    a.maxw = host_pack ? 0 : fused_maxw(di->backend, nwords);
+    a.maxw = host_pack ? 0 : fused_maxw(di->backend, K * steps);
     a.num = s.n;
     a.steps = steps;
     a.nwords = nwords;
