@@ -505,6 +505,28 @@ def kstep4_leg(D, text: bytes, reads: np.ndarray, res: np.ndarray, idx2, steps: 
     return out
 
 
+def kstep3_leg(text: bytes, reads: np.ndarray, res: np.ndarray, steps: int) -> dict:
+    """The main leg's reads on a K = 3 index (LAY_GRP, 4 lines per block; 100 %
+    3 = 1 base from the remainder table, then 33 K-steps), one GPU."""
+    t = time.perf_counter()
+    i3 = K.Index.build(text, k=3, d=64, gpu=True, host_image=False)
+    out = {"what": "coop-grp: K=3, d=64 index (LAY_GRP lines), wave64 cooperative LF, the main leg's reads",
+           "build_s": round(time.perf_counter() - t, 2)}
+    q = K.Queries.from_array(reads)
+    r = K.Results.alloc(reads.shape[0])
+    try:
+        wall, lf, tot = time_backend(i3, q, r, "coop-grp", steps, 5)
+        out.update({"mqps": round(reads.shape[0] * steps / wall / 1e6, 2), "lf_ms": round(lf, 3),
+                    "device_index_bytes": i3.device_bytes(),
+                    "results_equal_k2": bool(np.array_equal(r.array(), res))})
+    finally:
+        q.close()
+        r.close()
+        i3.free_gpu()
+        i3.close()
+    return out
+
+
 def time_backend(idx, q, r, backend, steps, warmup):
     """`backend` may carry "+ftabN": the Bowtie-style jump-start table of N bases."""
     name, _, opt = backend.partition("+")
@@ -687,6 +709,12 @@ def main():
         extra["config5"] = c5
     if k4 is not None:
         extra["kstep4"] = k4
+    if a.kstep4 and a.k == 2 and a.d == 64 and D.world == 1:
+        try:
+            extra["kstep3"] = kstep3_leg(text, reads, res, a.steps)
+            log(f"K=3 leg {extra['kstep3']}")
+        except K.KfmiError as e:
+            extra["kstep3"] = {"error": str(e)}
     if ingest is not None:
         extra["ingest_file"] = ingest          # rank 0's; every rank's is under "ranks"
     cpu = None
