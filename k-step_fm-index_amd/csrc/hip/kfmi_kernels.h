@@ -398,6 +398,15 @@ static hipError_t launch_locate(const SearchLaunch& a)
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
     cus = 256;
   uint64_t blocks = (a.total + 255) / 256;
+  if constexpr (locate_coop_ok<G>()) {   /* MID lines: one round trip per step (KFMI_LOCATE_COOP=0: per-lane walk) */
+    const char* e = getenv("KFMI_LOCATE_COOP");
+    if (!e || atoi(e)) {
+      if (blocks > (uint64_t) cus * 4) blocks = (uint64_t) cus * 4;   /* 33-34 KB of LDS per workgroup */
+      hipLaunchKernelGGL((locate_coop_kernel<G>), dim3((uint32_t) blocks), dim3(256), 0, a.st, a.ix, a.sa, a.sa_log2,
+                         a.owner, a.total, a.pos);
+      return hipGetLastError();
+    }
+  }
   if (blocks > (uint64_t) cus * 8) blocks = (uint64_t) cus * 8;
   hipLaunchKernelGGL((locate_kernel<G>), dim3((uint32_t) blocks), dim3(256), 0, a.st, a.ix, a.sa, a.sa_log2, a.owner,
                      a.total, a.pos);

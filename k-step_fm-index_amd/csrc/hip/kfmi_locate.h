@@ -94,6 +94,104 @@ __global__ __launch_bounds__(256) void locate_kernel(IdxArgs ix, const uint32_t*
   }
 }
 
+// ---------------------------------------------------------------------------
+// MID128 lines: one round trip per walk step.  A row's K-mer code sits in its
+// line's planes and the counter it then needs in the same line, so the
+// per-lane walk above pays a line load plus a dependent L2 hit per step.
+// Here each wave stages the whole line of every stepping lane HBM -> LDS with
+// cooperative 16-byte global_load_lds (TPR lanes per line, one round = 1 KiB,
+// as in the coop search kernel) and every lane takes its step from LDS.
+// ---------------------------------------------------------------------------
+template <class G>
+__host__ __device__ constexpr bool locate_coop_ok()
+{
+  return G::LAY == LAY_MID && G::EW * 4 >= 16 && G::EW * 4 <= 128;
+}
+
+// LF_K of row X from its MID line in LDS (the same arithmetic as lf_row on LAY_MID)
+template <class G>
+__device__ __forceinline__ uint32_t lf_row_line(const IdxArgs& ix, const uint8_t* line, uint32_t X)
+{
+  const uint32_t* L = reinterpret_cast<const uint32_t*>(line);
+  const uint32_t b = X / (uint32_t) G::D;
+  const uint32_t o = X - b * (uint32_t) G::D;
+  const bool e = (b & 1u) == 0;                     // even block: backward from the midpoint
+  const uint32_t* pl = L + (b & 1u) * G::BMW;
+  const uint32_t* pw = pl + (o >> 5) * G::PW;
+  const uint32_t bit = 31u - (o & 31u);
+  uint32_t c = 0;
+#pragma unroll
+  for (int p = 0; p < G::PW; ++p) c |= ((pw[p] >> bit) & 1u) << p;
+  uint32_t sx[2 * G::K];
+  plane_xor<G::K>(c, sx);
+  uint32_t pop = 0;
+#pragma unroll
+  for (int w = 0; w < G::NB; ++w) {
+    uint32_t m = row_mask((int) o - 32 * w);
+    m = e ? ~m : m;
+    pop += __popc(m & select_rows<G::K>(&pl[w * G::PW], sx));
+  }
+  return finish<G>(ix, L[G::MIDCNT + c], pop, b, c, X, e);
+}
+
+template <class G>
+__global__ __launch_bounds__(256) void locate_coop_kernel(IdxArgs ix, const uint32_t* __restrict__ sa,
+                                                          uint32_t rate_log2, const uint32_t* __restrict__ rows,
+                                                          uint64_t total, uint32_t* __restrict__ pos)
+{
+  constexpr int LB = G::EW * 4;     // line bytes
+  constexpr int TPR = LB / 16;      // lanes per line
+  constexpr int RPR = 64 / TPR;     // lines per 1 KiB round
+  static_assert(locate_coop_ok<G>(), "MID lines of 16..128 bytes");
+  __shared__ __attribute__((aligned(16))) uint8_t lds[4 * 64 * LB];
+  __shared__ uint32_t tabs[4 * 64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint8_t* wl = lds + wave * 64 * LB;
+  uint32_t* tab = tabs + wave * 64;
+  const uint8_t* base = reinterpret_cast<const uint8_t*>(ix.ent);
+  const uint32_t mask = (1u << rate_log2) - 1u;
+  const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
+  uint64_t i = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x;
+  bool act = i < total;
+  uint32_t r = act ? rows[i] : 0u;
+  uint32_t r_next = (act && i + stride < total) ? rows[i + stride] : 0u;
+  uint32_t steps = 0;
+  const int g = lane / TPR, k = lane % TPR;
+  while (__ballot(act)) {   // wave-uniform: until every lane of the wave has no slot left
+    const bool smp = act && (r & mask) == 0u;
+    int ds = -1;   /* r = D_s (SA = s): the walk cannot step past it */
+#pragma unroll
+    for (int s = G::K - 1; s >= 0; --s)
+      if (r == ix.dl.dpos[s]) ds = s;
+    const bool step = act && !smp && ds < 0;
+    uint32_t p = 0;
+    if (smp) p = sa[r >> rate_log2];
+    tab[lane] = step ? r / (uint32_t) (2 * G::D) : 0xFFFFFFFFu;   // this lane's MID line, or none
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int rr = 0; rr < 64 / RPR; ++rr) {
+      const uint32_t li = tab[rr * RPR + g];
+      if (li != 0xFFFFFFFFu)
+        __builtin_amdgcn_global_load_lds((const void*) (base + (uint64_t) li * LB + 16 * k),
+                                         (__attribute__((address_space(3))) void*) (wl + rr * 1024), 16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t nr = step ? lf_row_line<G>(ix, wl + lane * LB, r) : 0u;
+    if (smp || (act && ds >= 0)) {
+      pos[i] = (smp ? p : (uint32_t) ds) + steps;
+      i += stride;
+      act = i < total;
+      r = r_next;
+      r_next = (act && i + stride < total) ? rows[i + stride] : 0u;
+      steps = 0;
+    } else if (act) {
+      r = nr;
+      steps += G::K;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // LDS reads done before the next round overwrites
+  }
+}
+
 }  // namespace kfmi
 
 #endif  // KFMI_LOCATE_H_

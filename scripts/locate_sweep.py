@@ -28,7 +28,7 @@ def main():
     p.add_argument("--rates", default="1,4,16,32,64")
     p.add_argument("--backends", default="task-mid,task-ac")
     p.add_argument("--steps", type=int, default=3)
-    p.add_argument("--regs", default="0,1", help="KFMI_LOC_REGS values (one-round-trip walk step)")
+    p.add_argument("--coop", default="0,1", help="KFMI_LOCATE_COOP values (MID lines staged through LDS)")
     a = p.parse_args()
     K.load()
     K.set_device(0)
@@ -42,8 +42,8 @@ def main():
         t = time.perf_counter()
         idx = K.Index.build(text, k=2, d=64, gpu=True, sa_rate=rate)
         build_s = time.perf_counter() - t
-        for b, regs in [(b, g) for b in a.backends.split(",") for g in a.regs.split(",")]:
-            os.environ["KFMI_LOC_REGS"] = regs
+        for b, regs in [(b, g) for b in a.backends.split(",") for g in a.coop.split(",")]:
+            os.environ["KFMI_LOCATE_COOP"] = regs
             K.set_backend(b)
             K.transfer_to_gpu(idx, q, r)
             K.search(idx, q, r)
@@ -60,7 +60,8 @@ def main():
             p0 = pos[off[smp].astype(np.int64)].astype(np.int64)
             ok = bool(np.array_equal(t8[p0[:, None] + np.arange(a.qlen)[None, :]], reads[smp]))
             ms = float(np.median(kms))
-            out = {"rate": rate, "backend": b, "regs": int(regs), "positions": int(loc.total()), "kernel_ms": round(ms, 3),
+            import hashlib
+            out = {"rate": rate, "backend": b, "coop": int(regs), "pos_md5": hashlib.md5(pos.tobytes()).hexdigest(), "positions": int(loc.total()), "kernel_ms": round(ms, 3),
                    "Mpos_per_s": round(loc.total() / ms / 1e3, 1), "sa_bytes": int(idx.sa()[1].nbytes),
                    "build_s": round(build_s, 2), "positions_start_reads": ok}
             print(json.dumps(out), flush=True)
