@@ -81,6 +81,8 @@ struct DevCtx {
 int32_t ctx_for(int dev, DevCtx** out);   /* selects `dev`, creates its stream once */
 /* The calling thread's three timing events on device `dev` (current device). */
 hipEvent_t* thread_events(int dev);
+/* The calling thread's search stream on device `dev` (current device). */
+hipStream_t thread_stream(int dev);
 
 /* per calling thread (kfmi_search.hip) */
 extern thread_local int t_device;

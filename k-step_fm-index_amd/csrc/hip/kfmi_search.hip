@@ -166,18 +166,45 @@ int32_t ctx_for(int dev, DevCtx** out)
   return KFMI_SUCCESS;
 }
 
-/* Per thread and device, so that concurrent searches on one device do not
- * overwrite each other's timing (never destroyed: a handful per thread). */
+/* Per calling thread and device: a search stream and three timing events.
+ * Searches from different threads therefore run concurrently (small,
+ * latency-bound batches overlap on the device); uploads stay on the shared
+ * per-device stream and complete before they return.  Released when the
+ * thread exits. */
+struct ThreadRes {
+  hipStream_t st[64] = {};
+  hipEvent_t ev[64][3] = {};
+  ~ThreadRes()
+  {
+    for (int d = 0; d < 64; ++d) {
+      if (!st[d] && !ev[d][0] && !ev[d][1] && !ev[d][2]) continue;
+      if (hipSetDevice(d) != hipSuccess) continue;
+      if (st[d]) (void) hipStreamDestroy(st[d]);
+      for (hipEvent_t& e : ev[d])
+        if (e) (void) hipEventDestroy(e);
+    }
+  }
+};
+static thread_local ThreadRes t_res;
+
 hipEvent_t* thread_events(int dev)
 {
-  static thread_local hipEvent_t ev[64][3];
   if (dev < 0 || dev >= 64) return nullptr;
+  hipEvent_t* ev = t_res.ev[dev];
   for (int i = 0; i < 3; ++i)
-    if (!ev[dev][i] && hipEventCreate(&ev[dev][i]) != hipSuccess) {
-      ev[dev][i] = nullptr;
+    if (!ev[i] && hipEventCreate(&ev[i]) != hipSuccess) {
+      ev[i] = nullptr;
       return nullptr;
     }
-  return ev[dev];
+  return ev;
+}
+
+hipStream_t thread_stream(int dev)
+{
+  if (dev < 0 || dev >= 64) return nullptr;
+  if (!t_res.st[dev] && hipStreamCreateWithFlags(&t_res.st[dev], hipStreamNonBlocking) != hipSuccess)
+    t_res.st[dev] = nullptr;
+  return t_res.st[dev];
 }
 
 /* ------------------------------------------------------------------------ */
@@ -1286,9 +1313,10 @@ extern "C" int32_t kfmi_search(void* index, void* queries, void* results)
   DevCtx* ctx = nullptr;
   int32_t err = ctx_for(di->device, &ctx);
   hipEvent_t* ev = err ? nullptr : thread_events(di->device);
-  if (!err && !ev) err = KFMI_E_NO_DEVICE;
-  if (!err) err = search_enqueue(di, q->dev, r->d_results, ctx->st, ev, ftab_bases());
-  if (!err) err = search_finish(ctx->st, ev, t_ms);
+  hipStream_t st = err ? nullptr : thread_stream(di->device);
+  if (!err && (!ev || !st)) err = KFMI_E_NO_DEVICE;
+  if (!err) err = search_enqueue(di, q->dev, r->d_results, st, ev, ftab_bases());
+  if (!err) err = search_finish(st, ev, t_ms);
   return err;
 }
 

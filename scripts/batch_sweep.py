@@ -42,4 +42,30 @@ for k, backends in ((2, ("task-mid", "coop-mid")), (4, ("coop-grp",))):
                               "mqps": round(n / wall / 1e6, 1)}), flush=True)
             q.close()
             r.close()
+        # several host threads, each its own small batches (per-thread streams)
+        import threading
+        for n in (1_000, 16_000, 64_000):
+            for nt in (1, 2, 4, 8):
+                qs = [K.Queries.from_array(np.ascontiguousarray(reads[j * n:(j + 1) * n])) for j in range(nt)]
+                rs = [K.Results.alloc(n) for _ in range(nt)]
+                for j in range(nt):
+                    K.transfer_to_gpu(idx[k], qs[j], rs[j])
+                calls = max(20, min(400, 4_000_000 // n))
+
+                def work(j):
+                    K.set_device(0)
+                    K.set_backend(b)
+                    for _ in range(calls):
+                        K.search(idx[k], qs[j], rs[j])
+                th = [threading.Thread(target=work, args=(j,)) for j in range(nt)]
+                t0 = time.perf_counter()
+                for x in th:
+                    x.start()
+                for x in th:
+                    x.join()
+                wall = time.perf_counter() - t0
+                print(json.dumps({"k": k, "backend": b, "reads_per_batch": n, "threads": nt, "calls_per_thread": calls,
+                                  "mqps": round(nt * calls * n / wall / 1e6, 1)}), flush=True)
+                for x in qs + rs:
+                    x.close()
         idx[k].free_gpu()
