@@ -116,6 +116,12 @@ struct IdxArgs {
   // bases m-1 .. m-rem at bits 0-1 ..), the start of their K-steps; null = rem 0
   const uint2* __restrict__ rtab;
   uint32_t rem;
+  // task kernels: per-lane index gathers issued as 4 exec-masked groups of 16
+  // lanes (4: every task kernel; 2: the fused m <= 128 kernel only; 1: none).
+  // A wave instruction whose 64 lanes hit 64 pages of a table beyond the
+  // translation reach (~3.5 GB) stalls on translation; 16 pages per
+  // instruction do not (profiles/r02/gather_mask_r2ag.jsonl)
+  uint32_t split;
 };
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));

@@ -24,7 +24,40 @@ namespace kfmi {
 /*            in MAXW registers (fused packing, no pack launch, no qp).     */
 /* ------------------------------------------------------------------------ */
 
-template <class G, int QPT, int MAXW>
+
+/* Both ends' blocks of one step: block(L), and block(R) only when it differs. */
+template <class G, bool NT, int QPT>
+__device__ __forceinline__ void fetch_ends(const IdxArgs& ix, const uint32_t (&L)[QPT], const uint32_t (&R)[QPT],
+                                           const uint32_t (&c)[QPT], Blk<G> (&kl)[QPT], Blk<G> (&kr)[QPT])
+{
+#pragma unroll
+  for (int i = 0; i < QPT; ++i) fetch_block<G, NT>(ix, L[i] / (uint32_t) G::D, c[i], kl[i]);
+#pragma unroll
+  for (int i = 0; i < QPT; ++i) {
+    const uint32_t br = R[i] / (uint32_t) G::D;
+    if (br != kl[i].b) fetch_block<G, NT>(ix, br, c[i], kr[i]);
+    else kr[i] = kl[i];
+  }
+}
+
+/* SPLIT > 1: the same loads as SPLIT exec-masked groups of 64/SPLIT lanes, so
+ * one wave instruction touches at most 64/SPLIT pages (IdxArgs::split). */
+template <class G, bool NT, int QPT, int SPLIT>
+__device__ __forceinline__ void fetch_ends_split(const IdxArgs& ix, const uint32_t (&L)[QPT],
+                                                 const uint32_t (&R)[QPT], const uint32_t (&c)[QPT],
+                                                 Blk<G> (&kl)[QPT], Blk<G> (&kr)[QPT])
+{
+  if constexpr (SPLIT == 1) {
+    fetch_ends<G, NT, QPT>(ix, L, R, c, kl, kr);
+  } else {
+    const int grp = (int) (threadIdx.x & 63) / (64 / SPLIT);
+#pragma unroll
+    for (int g = 0; g < SPLIT; ++g)
+      if (grp == g) fetch_ends<G, NT, QPT>(ix, L, R, c, kl, kr);
+  }
+}
+
+template <class G, int QPT, int MAXW, int SPLIT = 1>
 __global__ __launch_bounds__(256) void task_kernel(IdxArgs ix, const uint32_t* __restrict__ qp,
                                                    const uint8_t* __restrict__ ascii, uint32_t m, uint64_t num,
                                                    uint32_t steps, uint32_t nwords, uint32_t* __restrict__ res)
@@ -98,25 +131,10 @@ __global__ __launch_bounds__(256) void task_kernel(IdxArgs ix, const uint32_t* _
       for (int i = 0; i < QPT; ++i) c[i] = (word[i] >> (2 * G::K * j)) & (uint32_t) (G::NC - 1);
       if constexpr (G::SMALL) {
         Blk<G> kl[QPT], kr[QPT];
-        if (w * SPW + j >= ix.nt_from) {   /* wave-uniform: deep steps stream non-temporally */
-#pragma unroll
-          for (int i = 0; i < QPT; ++i) fetch_block<G, true>(ix, L[i] / (uint32_t) G::D, c[i], kl[i]);
-#pragma unroll
-          for (int i = 0; i < QPT; ++i) {
-            const uint32_t br = R[i] / (uint32_t) G::D;
-            if (br != kl[i].b) fetch_block<G, true>(ix, br, c[i], kr[i]);
-            else kr[i] = kl[i];
-          }
-        } else {
-#pragma unroll
-          for (int i = 0; i < QPT; ++i) fetch_block<G>(ix, L[i] / (uint32_t) G::D, c[i], kl[i]);
-#pragma unroll
-          for (int i = 0; i < QPT; ++i) {
-            const uint32_t br = R[i] / (uint32_t) G::D;
-            if (br != kl[i].b) fetch_block<G>(ix, br, c[i], kr[i]);
-            else kr[i] = kl[i];
-          }
-        }
+        if (w * SPW + j >= ix.nt_from)   /* wave-uniform: deep steps stream non-temporally */
+          fetch_ends_split<G, true, QPT, SPLIT>(ix, L, R, c, kl, kr);
+        else
+          fetch_ends_split<G, false, QPT, SPLIT>(ix, L, R, c, kl, kr);
 #pragma unroll
         for (int i = 0; i < QPT; ++i) {
           uint32_t sx[2 * G::K];
@@ -341,8 +359,8 @@ static inline int task_qpt(void)
   return v == 2 ? 2 : 1;
 }
 
-template <class G>
-static hipError_t launch_task(const SearchLaunch& a)
+template <class G, int SPLIT>
+static void launch_task_split(const SearchLaunch& a)
 {
   if (a.maxw) {
     const uint64_t blocks = (a.num + 255) / 256;
@@ -350,20 +368,33 @@ static hipError_t launch_task(const SearchLaunch& a)
     const char* pe = getenv("KFMI_LDS_PAD");
     const size_t lds = 4 * (size_t) stage_slot_bytes(a.m) + (pe ? (size_t) atoi(pe) : 0);
     if (a.maxw == 8)
-      hipLaunchKernelGGL((task_kernel<G, 1, 8>), dim3((uint32_t) blocks), dim3(256), lds, a.st, a.ix, a.qp, a.ascii,
-                         a.m, a.num, a.steps, a.nwords, a.res);
-    else
-      hipLaunchKernelGGL((task_kernel<G, 1, 16>), dim3((uint32_t) blocks), dim3(256), lds, a.st, a.ix, a.qp,
+      hipLaunchKernelGGL((task_kernel<G, 1, 8, SPLIT>), dim3((uint32_t) blocks), dim3(256), lds, a.st, a.ix, a.qp,
                          a.ascii, a.m, a.num, a.steps, a.nwords, a.res);
-  } else if (task_qpt() == 2) {
+    else
+      hipLaunchKernelGGL((task_kernel<G, 1, 16, SPLIT>), dim3((uint32_t) blocks), dim3(256), lds, a.st, a.ix, a.qp,
+                         a.ascii, a.m, a.num, a.steps, a.nwords, a.res);
+  } else if (SPLIT == 1 && task_qpt() == 2) {
     const uint64_t blocks = (a.num + 511) / 512;
     hipLaunchKernelGGL((task_kernel<G, 2, 0>), dim3((uint32_t) blocks), dim3(256), 0, a.st, a.ix, a.qp, a.ascii,
                        a.m, a.num, a.steps, a.nwords, a.res);
   } else {
     const uint64_t blocks = (a.num + 255) / 256;
-    hipLaunchKernelGGL((task_kernel<G, 1, 0>), dim3((uint32_t) blocks), dim3(256), 0, a.st, a.ix, a.qp, a.ascii,
-                       a.m, a.num, a.steps, a.nwords, a.res);
+    hipLaunchKernelGGL((task_kernel<G, 1, 0, SPLIT>), dim3((uint32_t) blocks), dim3(256), 0, a.st, a.ix, a.qp,
+                       a.ascii, a.m, a.num, a.steps, a.nwords, a.res);
   }
+}
+
+template <class G>
+static hipError_t launch_task(const SearchLaunch& a)
+{
+  /* the split only exists for the one-line-per-block path (d <= 128 at K=2) */
+  if constexpr (G::SMALL) {
+    if (a.ix.split == 4 || (a.ix.split == 2 && a.maxw == 8)) {
+      launch_task_split<G, 4>(a);
+      return hipGetLastError();
+    }
+  }
+  launch_task_split<G, 1>(a);
   return hipGetLastError();
 }
 

@@ -979,6 +979,28 @@ int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx, kfmi_dev_
   return KFMI_SUCCESS;
 }
 
+/* Gather split for the per-lane (task) kernels (IdxArgs::split): 4 = every
+ * task kernel issues its index gathers as 4 exec-masked groups of 16 lanes;
+ * 2 = only the fused kernel for reads of <= 128 bases; 1 = none.
+ *  - tables over 3.5 GB: 4.  Past the translation reach the per-instruction
+ *    page cliff costs up to 2.7x (task-grp 96 GB: 17.6 -> 6.8 ms at 100 bp,
+ *    25.1 -> 9.1 at 150 bp; task-ac128 6.4 GB: 18.1 -> 10.0, 26.1 -> 15.5);
+ *  - 2-3.5 GB, one line per LF (MID128 / MIDAC): 2 (task-mid 9.53 -> 9.45 at
+ *    100 bp, but 14.41 -> 14.83 ms with the 16-word kernel at 150 bp);
+ *  - 2-3.5 GB, other layouts: 4 (task-ac 12.87 -> 11.81 at 100 bp,
+ *    18.93 -> 17.94 at 150 bp; task-packed 14.0 -> 13.3).
+ * profiles/r02/sweep_split_r2ah.jsonl, sweep_split150_r2aj.jsonl.  The ftab
+ * lookup (one gather per read) is never split: that measured slower.
+ * KFMI_SPLIT=1|4 forces it. */
+static uint32_t split_for(uint64_t table_bytes, int layout)
+{
+  const char* e = getenv("KFMI_SPLIT");
+  if (e && *e) return atoi(e) == 4 ? 4u : 1u;
+  if (table_bytes > 3500000000ull) return 4u;
+  if (table_bytes > 2000000000ull) return (layout == LAY_MID || layout == LAY_MIDAC) ? 2u : 4u;
+  return 1u;
+}
+
 IdxArgs idx_args(const kfmi_dev_index* di)
 {
   IdxArgs ix;
@@ -995,6 +1017,7 @@ IdxArgs idx_args(const kfmi_dev_index* di)
   ix.ac_tail_b0 = di->ac_tail_b0;
   ix.rtab = nullptr;
   ix.rem = 0;
+  ix.split = split_for(di->ent_bytes + di->sb_bytes, di->layout);
   return ix;
 }
 

@@ -11,6 +11,9 @@
  *   coop   : TPR lanes read one line cooperatively, 16 B each
  *   chain  : dependent chains (next address = f(loaded data)), 1 or 2 chains
  *            per lane -- the LF kernel's shape
+ *   mask<G>: as indep / chain1, but each wave issues every gather as G
+ *            instructions with 64/G active lanes (fewer distinct pages per
+ *            instruction -- the translation-reach question)
  * Addresses come from a per-lane xorshift generator (no index array traffic).
  */
 #include <hip/hip_runtime.h>
@@ -103,6 +106,67 @@ __global__ __launch_bounds__(256) void k_chain(const uint4* __restrict__ t, uint
   if (acc == 0x12345678u) sink[0] = acc;
 }
 
+
+/* indep / chain with every gather issued as G exec-masked instructions of
+ * 64/G lanes each: the same requests, at most 64/G distinct pages per
+ * instruction */
+template <int LB, int G>
+__global__ __launch_bounds__(256) void k_masked(const uint4* __restrict__ t, uint64_t nlines, uint64_t per_thread,
+                                                uint32_t* __restrict__ sink)
+{
+  constexpr int V = LB / 16;
+  const int grp = (threadIdx.x & 63) / (64 / G);
+  uint64_t s = 0x9E3779B97F4A7C15ull ^ ((uint64_t) blockIdx.x * 256 + threadIdx.x) * 0xBF58476D1CE4E5B9ull;
+  uint32_t acc = 0;
+  for (uint64_t i = 0; i < per_thread; i += 4) {
+    uint4 v[4][V];
+    uint64_t l[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) l[j] = pick(xs(s), nlines);
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if (grp == g) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int k = 0; k < V; ++k) v[j][k] = t[l[j] * V + k];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int k = 0; k < V; ++k) acc ^= v[j][k].x ^ v[j][k].w;
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
+template <int LB, int G>
+__global__ __launch_bounds__(256) void k_chain_masked(const uint4* __restrict__ t, uint64_t nlines, uint32_t steps,
+                                                      uint32_t* __restrict__ sink)
+{
+  constexpr int V = LB / 16;
+  const int grp = (threadIdx.x & 63) / (64 / G);
+  uint64_t s = 0x9E3779B97F4A7C15ull ^ ((uint64_t) blockIdx.x * 256 + threadIdx.x) * 0xBF58476D1CE4E5B9ull;
+  uint64_t l = pick(xs(s), nlines);
+  uint32_t acc = 0;
+  for (uint32_t i = 0; i < steps; ++i) {
+    uint4 v[V];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if (grp == g) {
+#pragma unroll
+        for (int k = 0; k < V; ++k) v[k] = t[l * V + k];
+      }
+    }
+    uint32_t x = 0;
+#pragma unroll
+    for (int k = 0; k < V; ++k) x ^= v[k].x ^ v[k].y;
+    acc ^= x;
+    l = pick(xs(s) ^ ((uint64_t) x << 32), nlines);
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
 static float timed(hipEvent_t a, hipEvent_t b)
 {
   float ms;
@@ -168,6 +232,22 @@ int main(int argc, char** argv)
            ms, nlines / ms / 1e6, nlines * lb / ms / 1e6);
     fflush(stdout);
   };
+  if (getenv("PROBE_MASK")) {
+    const uint64_t pt = (lines_target / threads + 3) & ~3ull;
+    const uint32_t st = (uint32_t) (lines_target / threads);
+    run("indep_mask1", 64, [&] { hipLaunchKernelGGL((k_masked<64, 1>), grid, blk, 0, 0, t, bytes / 64, pt, sink); }, (double) pt * threads);
+    run("indep_mask2", 64, [&] { hipLaunchKernelGGL((k_masked<64, 2>), grid, blk, 0, 0, t, bytes / 64, pt, sink); }, (double) pt * threads);
+    run("indep_mask4", 64, [&] { hipLaunchKernelGGL((k_masked<64, 4>), grid, blk, 0, 0, t, bytes / 64, pt, sink); }, (double) pt * threads);
+    run("indep_mask8", 64, [&] { hipLaunchKernelGGL((k_masked<64, 8>), grid, blk, 0, 0, t, bytes / 64, pt, sink); }, (double) pt * threads);
+    run("indep_mask16", 64, [&] { hipLaunchKernelGGL((k_masked<64, 16>), grid, blk, 0, 0, t, bytes / 64, pt, sink); }, (double) pt * threads);
+    run("chain_mask1", 64, [&] { hipLaunchKernelGGL((k_chain_masked<64, 1>), grid, blk, 0, 0, t, bytes / 64, st, sink); }, (double) st * threads);
+    run("chain_mask4", 64, [&] { hipLaunchKernelGGL((k_chain_masked<64, 4>), grid, blk, 0, 0, t, bytes / 64, st, sink); }, (double) st * threads);
+    run("chain_mask8", 64, [&] { hipLaunchKernelGGL((k_chain_masked<64, 8>), grid, blk, 0, 0, t, bytes / 64, st, sink); }, (double) st * threads);
+    run("indep_mask8", 128, [&] { hipLaunchKernelGGL((k_masked<128, 8>), grid, blk, 0, 0, t, bytes / 128, pt, sink); }, (double) pt * threads);
+    run("coop", 128, [&] { const uint64_t pg128 = (lines_target / (threads / 8) + 3) & ~3ull; hipLaunchKernelGGL((k_coop<128>), grid, blk, 0, 0, t, bytes / 128, pg128, sink); }, (double) ((lines_target / (threads / 8) + 3) & ~3ull) * (threads / 8));
+    if (strcmp(mode, "vmm")) CHECK(hipFree(t));
+    return 0;
+  }
   {
     const uint64_t pt = (lines_target / threads + 3) & ~3ull;
     run("indep", 32, [&] { hipLaunchKernelGGL((k_indep<32>), grid, blk, 0, 0, t, bytes / 32, pt, sink); }, (double) pt * threads);

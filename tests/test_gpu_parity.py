@@ -311,3 +311,36 @@ def test_ac_tail_blocks(gpu, oracle_mod, n, tail):
             for b in ACMID + ("task-ac128", "coop-ac128"):
                 if coop_supported(b, k, d):
                     assert np.array_equal(gpu.search_array(idx, q, b), want), (n, tail, k, d, m, b, defined)
+
+
+@pytest.mark.parametrize("backend", ["task-mid", "task", "task-packed", "task-ac", "task-ac128", "task-ac-mid"])
+def test_split_gathers_equal_oracle(gpu, oracle_mod, random_index, backend, monkeypatch):
+    """KFMI_SPLIT=4 (per-lane gathers as 4 exec-masked groups of 16 lanes, the
+    default for index tables over 2 GB) forced on small indexes:
+    the same results as the oracle, incl. partial last waves (n % 64 != 0),
+    reads with m % K != 0 (remainder table), fused and pack-kernel reads, and
+    the ftab jump start.  d = 192 has no split path (lf_stream) and must be
+    unaffected."""
+    text, idxs = random_index
+    monkeypatch.setenv("KFMI_SPLIT", "4")
+    for k, d in ((2, 64), (1, 64), (1, 32), (2, 128), (2, 192)):
+        idx = idxs[(k, d)]
+        if not coop_supported(backend, k, d):
+            continue
+        ref_img = idx.alt_counters()[0].image() if backend in ALT else idx.image()
+        lens = [(100, 20011), (150, 3001), (2 * k, 999), (300, 517)]
+        if backend not in ALT:
+            lens.append((101, 1203))
+        for m, n in lens:
+            q = _reads(text, n, m, seed=m * 11 + k)
+            # m % K != 0: the true interval, i.e. the K = 1 oracle's
+            want, _ = oracle_mod.search(ref_img if m % k == 0 else idxs[(1, 64)].image(), q)
+            got = gpu.search_array(idx, q, backend)
+            assert np.array_equal(got, want), (backend, k, d, m)
+        if d == 64:
+            monkeypatch.setenv("KFMI_FTAB", str(4 * k))
+            q = _reads(text, 5003, 100, seed=17 + k)
+            want, _ = oracle_mod.search(ref_img, q)
+            got = gpu.search_array(idx, q, backend)
+            monkeypatch.delenv("KFMI_FTAB")
+            assert np.array_equal(got, want), (backend, k, d, "ftab")

@@ -77,13 +77,18 @@ def k4(kfmi_mod):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("split", ["1", "4"])
 @pytest.mark.parametrize("backend", GRP)
-def test_grp_matches_oracle_and_k2(kfmi_mod, oracle_mod, k4, backend):
+def test_grp_matches_oracle_and_k2(kfmi_mod, oracle_mod, k4, backend, split, monkeypatch):
+    """split 4: per-lane gathers as 4 exec-masked groups (the default for the
+    96 GB GRP table at 3 Gbase; the coop kernel ignores it)."""
     K = kfmi_mod
+    monkeypatch.setenv("KFMI_SPLIT", split)
     t, i4, i2 = k4
-    for m, n in ((100, 20_000), (16, 4_000), (4, 2_000), (256, 1_000), (300, 1_000), (8, 500)):
+    for m, n in ((100, 20_000), (16, 4_000), (4, 2_000), (256, 1_000), (300, 1_000), (8, 500), (102, 1_001),
+                 (150, 777)):
         q = _reads(t, n, m, m + 1)
-        want, _ = oracle_mod.search(i4.image(), q)
+        want, _ = oracle_mod.search(i4.image() if m % 4 == 0 else i2.image(), q)   # m % 4 = 2: remainder table
         got = K.search_array(i4, q, backend)
         assert np.array_equal(got, want), (backend, m, int(np.flatnonzero(got != want)[0]))
         assert np.array_equal(got, K.search_array(i2, q, "task-mid")), (backend, m)
