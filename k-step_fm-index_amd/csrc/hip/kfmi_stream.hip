@@ -20,14 +20,22 @@ namespace kfmi {
 
 /* ------------------------------------------------------------------------ */
 /* streamed search from host memory: query H2D, packing, LF  */
-/* and result D2H of successive chunks overlap on NSLOT HIP streams.  By    */
+/* and result D2H of successive chunks overlap on a few HIP streams.  By   */
 /* default the host packs each chunk to 2-bit code words (qpack.c) while    */
 /* the GPU works on the previous ones, so PCIe carries 4 bytes per 16 bases */
 /* (KFMI_STREAM_HOSTPACK=0: ASCII H2D and packing on the device).  Pinned   */
 /* ASCII is DMA'd directly; pageable goes through pinned staging.           */
 /* ------------------------------------------------------------------------ */
 
-constexpr int NSLOT = 3;
+/* slots in flight: enough that the host keeps packing while ASCII chunks
+ * queue on the link (KFMI_STREAM_SLOTS, 2..8, default 6) */
+constexpr int NSLOT_MAX = 8;
+static int stream_slots(void)
+{
+  const char* e = getenv("KFMI_STREAM_SLOTS");
+  const int v = e ? atoi(e) : 6;
+  return v < 2 ? 2 : v > NSLOT_MAX ? NSLOT_MAX : v;
+}
 
 struct StreamSlot {
   hipStream_t st = nullptr;
@@ -46,7 +54,7 @@ struct StreamSlot {
 
 struct StreamPool {
   bool init = false;
-  StreamSlot slot[NSLOT];
+  StreamSlot slot[NSLOT_MAX];
   /* adaptive transfer mode: measured costs in ms per byte, kept across calls
    * (0 = not measured yet).  Host: EMA of packing / staging time per ASCII
    * byte.  Link: the fastest H2D seen per byte sent (the events bracketing a
@@ -319,7 +327,11 @@ extern "C" int32_t kfmi_search_stream(void* index, const char* ascii, uint64_t n
    * adaptive: per chunk, whichever mode a two-resource model (host thread
    * pool, PCIe link) says finishes first, with per-read costs measured on the
    * previous chunks -- on a box whose host packs slower than the link carries
-   * ASCII, part of the batch goes as ASCII while the host packs the rest. */
+   * ASCII, part of the batch goes as ASCII while the host packs the rest.
+   * (A batch-level balance -- pack the share that equalises host and link
+   * time -- measured no better than packing everything: host packing and the
+   * DMA of pinned ASCII draw on the same host DRAM bandwidth, so the two
+   * "resources" are not independent; profiles/r02/e2e_modes_r2al.jsonl.) */
   const char* hp = getenv("KFMI_STREAM_HOSTPACK");
   /* K = 3: the host packer writes 16 bases per word, the K = 3 kernels read 5
    * K-steps per word -- every chunk goes as ASCII (packed in the kernel) */
@@ -338,15 +350,17 @@ extern "C" int32_t kfmi_search_stream(void* index, const char* ascii, uint64_t n
   std::lock_guard<std::mutex> lk(g_pool_mu[di->device]);
   StreamPool& pool = g_pool[di->device];
   pool.init = true;
-  for (StreamSlot& s : pool.slot) {
+  const int nslot = stream_slots();
+  for (int k = 0; k < nslot; ++k) {
+    StreamSlot& s = pool.slot[k];
     err = slot_reserve(s, chunk, size, nwords, !pin_in && any_ascii, !pin_out, any_pack);
     if (err) return err;
     s.busy = false;
   }
   /* cost model: pool.r_* per byte (see StreamPool) -> ms per read */
   const double abytes = (double) size, pbytes = 4.0 * nwords;
-  double t_host = 0, t_link = 0;                      /* model clocks of this call */
   uint64_t npacked = 0;
+  double t_host = 0, t_link = 0;                      /* model clocks of this call */
   auto ema = [](double& v, double x) { v = v > 0 ? 0.6 * v + 0.4 * x : x; };
   auto keep_min = [](double& v, double x) { v = (v > 0 && v < x) ? v : x; };
   const auto t0 = std::chrono::steady_clock::now();
@@ -376,7 +390,7 @@ extern "C" int32_t kfmi_search_stream(void* index, const char* ascii, uint64_t n
   };
   const uint64_t nchunks = (num + chunk - 1) / chunk;
   for (uint64_t i = 0; i < nchunks && status == KFMI_SUCCESS; ++i) {
-    StreamSlot& s = pool.slot[i % NSLOT];
+    StreamSlot& s = pool.slot[i % nslot];
     retire(s);
     if (status) break;
     s.q0 = i * chunk;
@@ -441,7 +455,7 @@ extern "C" int32_t kfmi_search_stream(void* index, const char* ascii, uint64_t n
     }
     s.busy = true;
   }
-  for (StreamSlot& s : pool.slot) retire(s);
+  for (int k = 0; k < nslot; ++k) retire(pool.slot[k]);
   const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   t_ms[0] = ms;
   t_ms[1] = host_ms;   /* host packing or staging copies */

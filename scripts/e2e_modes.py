@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Streamed (host -> host) search: per-chunk transfer mode (KFMI_STREAM_HOSTPACK
-0 = ASCII, 1 = host-packed, 2 = adaptive) x host packing ISA, pinned and
+0 = ASCII, 1 = host-packed, 2 = adaptive)
+x stream slots (E2E_SLOTS, E2E_MODES comma lists) x host packing ISA, pinned and
 pageable input, 3 Gbase / 10M x 100 bp (dev tool; not the bench contract).
 One JSON line per measurement on stdout."""
 from __future__ import annotations
@@ -36,8 +37,10 @@ for isa in ("avx2", "avx512"):
     t = time.perf_counter()
     K.pack_queries(reads[:2_000_000])
     p1 = 2_000_000 * 100 / (time.perf_counter() - t) / 1e9
-    for kind, src, dst in (("pinned", pin, pout), ("pageable", reads, None)):
-        modes = ("1", "2", "0")
+    for kind, src, dst, slots in [(k, s, d, n) for k, s, d in (("pinned", pin, pout), ("pageable", reads, None))
+                                  for n in os.environ.get("E2E_SLOTS", "6").split(",")]:
+        os.environ["KFMI_STREAM_SLOTS"] = slots
+        modes = tuple(os.environ.get("E2E_MODES", "1,2,0").split(","))
         ms = {m: [] for m in modes}
         frac = {}
         ok = {}
@@ -57,4 +60,5 @@ for isa in ("avx2", "avx512"):
             print(json.dumps({"isa": isa, "pack_1thread_GBs": round(p1, 2), "mode": m, "input": kind,
                               "ms": round(med, 3), "ms_all": [round(x, 2) for x in ms[m]],
                               "mqps": round(reads.shape[0] / med * 1e3 / 1e6, 1),
-                              "hostpacked_fraction": round(frac[m], 3), "equal": ok[m]}), flush=True)
+                              "hostpacked_fraction": round(frac[m], 3), "equal": ok[m], "slots": int(slots)}),
+                  flush=True)

@@ -1,5 +1,5 @@
 """Streamed search from host memory (kfmi_search_stream): chunked
-H2D / pack + LF / D2H overlap on three HIP streams, with the reads packed on the
+H2D / pack + LF / D2H overlap on a few HIP streams (KFMI_STREAM_SLOTS), with the reads packed on the
 host (default) or on the device, must return exactly what the
 resident-batch path (kfmi_search) and the CPU oracle return, for ragged chunk
 sizes and for pinned and pageable host buffers."""
@@ -47,6 +47,19 @@ def test_stream_equals_batch_and_oracle(setup, oracle_mod, backend, chunk, hostp
     if chunk == 1_000 and backend == "task-mid":
         ores, _ = oracle_mod.search(idx.image(), reads, 8)
         assert np.array_equal(got, ores)
+
+
+@pytest.mark.parametrize("slots", ["2", "3", "8"])
+@pytest.mark.parametrize("hostpack", ["3", "2"])
+def test_stream_slot_counts(setup, hostpack, slots, monkeypatch):
+    """Any number of chunks in flight (2..8 slots; default 6), also after a
+    call with more slots left the extra ones idle."""
+    K, idx, reads = setup
+    monkeypatch.setenv("KFMI_STREAM_HOSTPACK", hostpack)
+    want = K.search_array(idx, reads, "task-mid")
+    monkeypatch.setenv("KFMI_STREAM_SLOTS", slots)
+    for chunk in (997, 0):
+        assert np.array_equal(K.search_stream(idx, reads, chunk=chunk), want), (slots, chunk)
 
 
 @pytest.mark.parametrize("hostpack", ["1", "0", "2", "3"])
