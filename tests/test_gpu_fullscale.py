@@ -103,3 +103,32 @@ def test_3g_backend_full_scale(gpu, g3, reads, backend, tmp_path):
     got = gpu.search_array(idx, reads["q150"], backend)
     assert np.array_equal(got, want), (backend, int(np.flatnonzero(got != want)[0]))
     idx.free_gpu()
+
+
+@pytest.mark.parametrize("split", ["", "1"])
+def test_3g_kstep4_full_scale(gpu, g3, reads, split, tmp_path, monkeypatch):
+    """K = 4 on the same 3 Gbase text (LAY_GRP, 96 GB of lines, device-resident
+    build): the same suffix-array intervals, so the q1M results file md5 and
+    the q10M results equal the K = 2 pins; 150 bp (150 % 4 = 2 bases from the
+    remainder table) equals the plain oracle.  task-grp runs with its default
+    split-issue gathers ("") and with plain issue ("1")."""
+    from kstep_fmi import synth
+    text, idx2 = g3
+    if split:
+        monkeypatch.setenv("KFMI_SPLIT", split)
+    idx2.free_gpu()
+    i4 = gpu.Index.build(text, k=4, d=64, gpu=True, host_image=False)
+    try:
+        for backend in (("task-grp", "coop-grp") if not split else ("task-grp",)):
+            res = gpu.search_array(i4, reads["q1m"], backend)
+            assert util.results_md5(gpu, res, tmp_path) == synth.MD5["res3g.q1M"], backend
+            res = gpu.search_array(i4, reads["q10m"], backend)
+            if reads["res10m"]:
+                assert np.array_equal(res, reads["res10m"]["res"]), backend
+            else:
+                assert util.results_md5(gpu, res, tmp_path) == synth.MD5["res3g.q10M"], backend
+            got = gpu.search_array(i4, reads["q150"], backend)
+            assert np.array_equal(got, reads["want150"]), (backend, int(np.flatnonzero(got != reads["want150"])[0]))
+    finally:
+        i4.free_gpu()
+        i4.close()
