@@ -806,7 +806,7 @@ def main():
                 e2e["what"] = "kfmi_search_stream: ASCII reads in host memory -> results in host memory; " \
                               "per chunk host 2-bit packing (qpack.c, KFMI_HOST_THREADS) + code-word H2D, or " \
                               "ASCII H2D + device packing, chosen from measured rates; LF / D2H of successive " \
-                              "chunks overlapped on 3 HIP streams"
+                              "chunks overlapped on KFMI_STREAM_SLOTS (default 6) HIP streams"
                 extra["end_to_end"] = e2e
                 log(f"end to end {e2e}")
                 del pin, pout

@@ -213,8 +213,9 @@ int32_t kfmi_count_blocks(void *index, void *queries, uint64_t *blocks);
  * ASCII bytes at `ascii`, results [L0,R0,L1,R1,...] into `results` (2*num
  * u32).  The index must already be on the device (transferCPUtoGPU(index,
  * NULL, NULL)).  Chunks of `chunk` queries (0: KFMI_STREAM_CHUNK, else 2^19,
- * or 2^16 when every chunk goes as ASCII) rotate over 3 HIP streams so that
- * host packing, H2D, LF and result D2H of successive chunks overlap.  Each
+ * or 2^16 when every chunk goes as ASCII) rotate over KFMI_STREAM_SLOTS
+ * (default 6) HIP streams so that host packing, H2D, LF and result D2H of
+ * successive chunks overlap.  Each
  * chunk either is packed by the host to code words (kfmi_pack_queries; PCIe
  * carries 4 bytes per 16 bases) or goes as ASCII (pinned: DMA'd directly;
  * pageable: staged through pinned buffers) and is packed on the device.  By
