@@ -92,7 +92,17 @@ class Dist:
         if self.world > 1:
             import torch.distributed as dist
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            dist.init_process_group("gloo")    # control plane only: barrier + timing max
+            # gloo's C++ layer prints "[Gloo] Rank r is connected to ..." on
+            # fd 1 while the group forms; keep stdout for rank 0's JSON line
+            sys.stdout.flush()
+            saved = os.dup(1)
+            os.dup2(2, 1)
+            try:
+                dist.init_process_group("gloo")    # control plane only: barrier + timing max
+                dist.barrier()
+            finally:
+                os.dup2(saved, 1)
+                os.close(saved)
             self.pg = dist
 
     def barrier(self):
@@ -490,6 +500,11 @@ def kstep4_leg(D, text: bytes, reads: np.ndarray, res: np.ndarray, idx2, steps: 
             out["coop-grp+ftab16"] = {"mqps": round(reads.shape[0] * steps / wall / 1e6, 2), "lf_ms": round(lf1, 3),
                                       "results_equal_k2": bool(np.array_equal(r.array(), res)),
                                       "device_bytes_incl_ftab": i4.device_bytes() + 8 * 4 ** 16}
+            # the per-lane kernel on the same 96 GB lines, with its default
+            # split-issue gathers (4 exec-masked groups of 16 lanes)
+            wall, lf1, tot1 = time_backend(i4, q, r, "task-grp", steps, 5)
+            out["task-grp"] = {"mqps": round(reads.shape[0] * steps / wall / 1e6, 2), "lf_ms": round(lf1, 3),
+                               "results_equal_k2": bool(np.array_equal(r.array(), res))}
         q.close()
         r.close()
         q = r = None
