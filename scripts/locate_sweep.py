@@ -29,6 +29,8 @@ def main():
     p.add_argument("--backends", default="task-mid,task-ac")
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--coop", default="0,1", help="KFMI_LOCATE_COOP values (MID lines staged through LDS)")
+    p.add_argument("--k", type=int, default=2)
+    p.add_argument("--env", default="", help="semicolon list of VAR=v1,v2 knobs swept for every backend")
     a = p.parse_args()
     K.load()
     K.set_device(0)
@@ -40,10 +42,16 @@ def main():
     t8 = np.frombuffer(text, dtype=np.uint8)
     for rate in [int(x) for x in a.rates.split(",")]:
         t = time.perf_counter()
-        idx = K.Index.build(text, k=2, d=64, gpu=True, sa_rate=rate)
+        idx = K.Index.build(text, k=a.k, d=64, gpu=True, sa_rate=rate, host_image=a.k < 3)
         build_s = time.perf_counter() - t
-        for b, regs in [(b, g) for b in a.backends.split(",") for g in a.coop.split(",")]:
+        knobs = [{}]
+        for spec in [x for x in a.env.split(";") if x]:
+            var, vals = spec.split("=")
+            knobs = [dict(kk, **{var: v}) for kk in knobs for v in vals.split(",")]
+        for b, regs, kn in [(b, g, kn) for b in a.backends.split(",") for g in a.coop.split(",") for kn in knobs]:
             os.environ["KFMI_LOCATE_COOP"] = regs
+            for var, v in kn.items():
+                os.environ[var] = v
             K.set_backend(b)
             K.transfer_to_gpu(idx, q, r)
             K.search(idx, q, r)
@@ -61,7 +69,7 @@ def main():
             ok = bool(np.array_equal(t8[p0[:, None] + np.arange(a.qlen)[None, :]], reads[smp]))
             ms = float(np.median(kms))
             import hashlib
-            out = {"rate": rate, "backend": b, "coop": int(regs), "pos_md5": hashlib.md5(pos.tobytes()).hexdigest(), "positions": int(loc.total()), "kernel_ms": round(ms, 3),
+            out = {"rate": rate, "backend": b, "coop": int(regs), "knobs": kn, "k": a.k, "pos_md5": hashlib.md5(pos.tobytes()).hexdigest(), "positions": int(loc.total()), "kernel_ms": round(ms, 3),
                    "Mpos_per_s": round(loc.total() / ms / 1e3, 1), "sa_bytes": int(idx.sa()[1].nbytes),
                    "build_s": round(build_s, 2), "positions_start_reads": ok}
             print(json.dumps(out), flush=True)
