@@ -341,6 +341,7 @@ struct SearchLaunch {
   const uint32_t* owner;
   uint64_t total;
   uint32_t* pos;
+  unsigned long long* slot_ctr;   /* walk slot queue, zeroed before the launch */
   /* in-call reorder: search order and row-major code words (MAXW = 8) */
   const uint32_t* perm;
   const uint32_t* pk;
@@ -420,7 +421,8 @@ static hipError_t launch_count(const SearchLaunch& a, unsigned long long* d_tota
 
 
 /* Locate: enough lanes to fill every CU (8 workgroups of 256 per CU), each
- * lane walking slot after slot. */
+ * lane walking slot after slot (the cooperative walk: from its wave's share of
+ * the slot queue). */
 template <class G>
 static hipError_t launch_locate(const SearchLaunch& a)
 {
@@ -434,7 +436,7 @@ static hipError_t launch_locate(const SearchLaunch& a)
     if (!e || atoi(e)) {
       if (blocks > (uint64_t) cus * 4) blocks = (uint64_t) cus * 4;   /* 33-34 KB of LDS per workgroup */
       hipLaunchKernelGGL((locate_coop_kernel<G>), dim3((uint32_t) blocks), dim3(256), 0, a.st, a.ix, a.sa, a.sa_log2,
-                         a.owner, a.total, a.pos);
+                         a.owner, a.total, a.pos, a.slot_ctr);
       return hipGetLastError();
     }
   }

@@ -18,8 +18,15 @@
  *
  * Work distribution: one output slot per lane at a time; a lane whose walk
  * ends takes its next slot at once instead of idling until the longest walk
- * of its wave ends.  Slots are assigned without any search: the exclusive scan
- * of min(R - L, max_occ) gives each query's first slot, the query id is written
+ * of its wave ends.  The per-lane walk takes slots i, i + stride, ...; the
+ * cooperative walk (whose waves move in lockstep rounds) takes them from one
+ * queue: each wave takes chunks of SLOT_CHUNK consecutive slots from a global
+ * counter (one atomic per chunk) and hands them to its lanes as their walks
+ * end, so no wave keeps stepping a few long walks while the queue still holds
+ * work (a fixed order leaves each lane ~38 walks of geometric length whose
+ * sums differ by hundreds of steps).  The slots' first rows are computed
+ * without any search: the exclusive scan of
+ * min(R - L, max_occ) gives each query's first slot, the query id is written
  * there and spread by an inclusive max-scan, and a coalesced pass turns it
  * into each slot's first row.
  */
@@ -55,10 +62,64 @@ __device__ __forceinline__ uint32_t lf_row(const IdxArgs& ix, uint32_t X)
   return lf_stream<G>(ix, X, c, sx);
 }
 
+// Wave-level slot queue.  `want` lanes receive the next slots of the wave's
+// chunk [cur, end), a new chunk is taken from *ctr when the chunk runs short
+// (SLOT_CHUNK >= 64 slots, so one chunk always covers the rest).  Called by
+// every lane of the wave (the caller's loop is wave-uniform).  Returns the
+// lane's slot, or ~0 when it wants none or the queue is empty; slots a wave
+// receives only grow, so once a lane is told "empty" it stays so.
+constexpr uint32_t SLOT_CHUNK = 256;
+
+__device__ __forceinline__ uint64_t uniform64(uint64_t x)
+{
+  return ((uint64_t) __builtin_amdgcn_readfirstlane((uint32_t) (x >> 32)) << 32) |
+         (uint64_t) __builtin_amdgcn_readfirstlane((uint32_t) x);
+}
+
+struct WaveSlots {
+  uint64_t cur = 0, end = 0;   // wave-uniform
+  uint64_t fixed = ~0ull;      // ctr == nullptr (KFMI_LOCATE_QUEUE=0): this lane's next slot of i, i + stride, ...
+};
+
+__device__ __forceinline__ uint64_t take_slot(bool want, WaveSlots& ws, unsigned long long* ctr, uint64_t total)
+{
+  if (!ctr) {   // fixed order (A/B reference)
+    if (ws.fixed == ~0ull) ws.fixed = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (!want) return ~0ull;
+    const uint64_t s = ws.fixed;
+    ws.fixed += (uint64_t) gridDim.x * blockDim.x;
+    return s < total ? s : ~0ull;
+  }
+  const uint64_t mask = __ballot(want);
+  const uint32_t n = (uint32_t) __popcll(mask);
+  if (n == 0) return ~0ull;
+  const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t) (mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) mask, 0u));
+  ws.cur = uniform64(ws.cur);   // the same in every lane: keep it (and the branches on it) scalar
+  ws.end = uniform64(ws.end);
+  const uint64_t have = ws.end - ws.cur;
+  uint64_t slot;
+  if (have >= n) {
+    slot = ws.cur + rank;
+    ws.cur += n;
+  } else {
+    unsigned long long base = ~0ull;   // queue already past its end: no more chunks
+    if (ws.end < total) {
+      if ((threadIdx.x & 63) == 0) base = atomicAdd(ctr, (unsigned long long) SLOT_CHUNK);
+      base = __shfl(base, 0);
+    }
+    slot = rank < have ? ws.cur + rank : (base == ~0ull ? ~0ull : base + (rank - have));
+    ws.cur = base == ~0ull ? ws.end : base + (n - have);
+    ws.end = base == ~0ull ? ws.end : base + SLOT_CHUNK;
+  }
+  return want && slot < total ? slot : ~0ull;
+}
+
 // Each lane walks slot after slot (i, i + stride, ...).  Per iteration a lane
 // either reads its row's sample (sampled row), stops at a '$' row, or takes
 // one LF_K step; the sample load and the step's line load of the other lanes
-// are in flight together, and the next slot's first row is prefetched.
+// are in flight together, and the next slot's first row is prefetched.  (Fed
+// from the slot queue of the cooperative walk below, this walk measured
+// 13-20 % slower: profiles/r02/locate_r2au.jsonl.)
 template <class G>
 __global__ __launch_bounds__(256) void locate_kernel(IdxArgs ix, const uint32_t* __restrict__ sa, uint32_t rate_log2,
                                                      const uint32_t* __restrict__ rows, uint64_t total,
@@ -137,7 +198,8 @@ __device__ __forceinline__ uint32_t lf_row_line(const IdxArgs& ix, const uint8_t
 template <class G>
 __global__ __launch_bounds__(256) void locate_coop_kernel(IdxArgs ix, const uint32_t* __restrict__ sa,
                                                           uint32_t rate_log2, const uint32_t* __restrict__ rows,
-                                                          uint64_t total, uint32_t* __restrict__ pos)
+                                                          uint64_t total, uint32_t* __restrict__ pos,
+                                                          unsigned long long* __restrict__ ctr)
 {
   constexpr int LB = G::EW * 4;     // line bytes
   constexpr int TPR = LB / 16;      // lanes per line
@@ -150,11 +212,12 @@ __global__ __launch_bounds__(256) void locate_coop_kernel(IdxArgs ix, const uint
   uint32_t* tab = tabs + wave * 64;
   const uint8_t* base = reinterpret_cast<const uint8_t*>(ix.ent);
   const uint32_t mask = (1u << rate_log2) - 1u;
-  const uint64_t stride = (uint64_t) gridDim.x * blockDim.x;
-  uint64_t i = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x;
+  WaveSlots ws;
+  uint64_t i = take_slot(true, ws, ctr, total);
+  uint32_t r = i < total ? rows[i] : 0u;
+  uint64_t i_n = take_slot(true, ws, ctr, total);
+  uint32_t r_n = i_n < total ? rows[i_n] : 0u;
   bool act = i < total;
-  uint32_t r = act ? rows[i] : 0u;
-  uint32_t r_next = (act && i + stride < total) ? rows[i + stride] : 0u;
   uint32_t steps = 0;
   const int g = lane / TPR, k = lane % TPR;
   while (__ballot(act)) {   // wave-uniform: until every lane of the wave has no slot left
@@ -177,16 +240,21 @@ __global__ __launch_bounds__(256) void locate_coop_kernel(IdxArgs ix, const uint
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint32_t nr = step ? lf_row_line<G>(ix, wl + lane * LB, r) : 0u;
-    if (smp || (act && ds >= 0)) {
+    const bool fin = smp || (act && ds >= 0);
+    if (fin) {
       pos[i] = (smp ? p : (uint32_t) ds) + steps;
-      i += stride;
+      i = i_n;
+      r = r_n;
       act = i < total;
-      r = r_next;
-      r_next = (act && i + stride < total) ? rows[i + stride] : 0u;
       steps = 0;
     } else if (act) {
       r = nr;
       steps += G::K;
+    }
+    const uint64_t got = take_slot(fin, ws, ctr, total);
+    if (fin) {
+      i_n = got;
+      r_n = got < total ? rows[got] : 0u;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // LDS reads done before the next round overwrites
   }

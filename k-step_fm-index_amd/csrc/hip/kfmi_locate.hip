@@ -179,7 +179,15 @@ static int32_t locate_on(kfmi_fmi_t* f, kfmi_dev_index* di, uint32_t* d_res, uin
   a.owner = d_own;
   a.total = total;
   a.pos = d_pos;
-  ok = hipEventRecord(ev[1], st) == hipSuccess &&
+  /* The cooperative walk takes its slots from a queue (counts are spent: word 0
+   * of d_cnt is the queue's counter) when walks are long enough for the lanes'
+   * ends to drift apart, SA rate >= 8 (rate 8: 2.3 -> 2.0-2.1 ms, rate 32:
+   * 8.5-8.9 -> 7.3-7.9 ms; rate 1, one round per slot: 0.30 -> 0.56 ms,
+   * profiles/r02/locate_r2av.jsonl); KFMI_LOCATE_QUEUE=0/1 forces it. */
+  const char* qe = getenv("KFMI_LOCATE_QUEUE");
+  const bool queue = qe ? atoi(qe) != 0 : (1u << di->sa_log2) >= 8;
+  a.slot_ctr = queue ? reinterpret_cast<unsigned long long*>(d_cnt) : nullptr;
+  ok = hipMemsetAsync(d_cnt, 0, 8, st) == hipSuccess && hipEventRecord(ev[1], st) == hipSuccess &&
        (total == 0 || dispatch(Op::Locate, di->K, di->nb, di->layout, a) == hipSuccess) &&
        hipEventRecord(ev[2], st) == hipSuccess &&
        hipMemcpyAsync(L->h_off, d_off, 8 * (num + 1), hipMemcpyDeviceToHost, st) == hipSuccess &&

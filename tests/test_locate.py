@@ -187,6 +187,27 @@ def test_locate_max_occ_repeats_and_empty(gpu):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("queue", ["0", "1"])
+def test_locate_slot_queue_forced(gpu, monkeypatch, queue):
+    # the cooperative walk's slot queue (default at SA rate >= 8) and the fixed
+    # slot order, each forced at every rate: ~3 M positions, so every wave of
+    # the grid takes several chunks of the queue and the last chunk is partial
+    monkeypatch.setenv("KFMI_LOCATE_QUEUE", queue)
+    text = b"A" * 3000 + b"C" + b"ACGT" * 700 + b"G" + _text(5000, 77)
+    sa = util.suffix_array(text + b"$")
+    q = np.frombuffer(b"AAAA" * 999 + b"ACGT" + b"TTTT" + b"CGTA", dtype=np.uint8).reshape(-1, 4)
+    for rate in (1, 8, 64):
+        idx = gpu.Index.build(text, k=2, d=64, gpu=True, sa_rate=rate)
+        for backend in ("task-mid", "coop-mid"):
+            res, off, pos = gpu.locate_array(idx, q, backend)
+            w_off, w_pos = _expected(sa, res)
+            assert int(w_off[-1]) > 2_900_000
+            assert np.array_equal(off, w_off), (queue, rate, backend)
+            assert np.array_equal(pos, w_pos), (queue, rate, backend)
+        idx.close()
+
+
+@pytest.mark.gpu
 def test_locate_errors(gpu):
     text = _text(2000, 9)
     idx = gpu.Index.build(text, k=2, d=64, gpu=True)          # no samples
