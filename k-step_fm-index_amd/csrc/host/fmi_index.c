@@ -368,7 +368,8 @@ int32_t kfmi_ac_tail(const kfmi_fmi_t *f, uint32_t *out, uint32_t *first)
   uint32_t c, nc, nbw, rem, last;
   const uint32_t *src;
   if (!f || !out || (f->tag != 100 && f->tag != 101) || !f->nentries) return KFMI_E_BAD_ARGUMENT;
-  if (kfmi_host_entries(f) != KFMI_SUCCESS) return KFMI_E_NOT_ON_DEVICE;
+  /* a device-resident index fetches its host image on demand (a cache owned by the handle) */
+  if (kfmi_host_entries((kfmi_fmi_t *) f) != KFMI_SUCCESS) return KFMI_E_NOT_ON_DEVICE;
   nc = f->ncounters;
   nbw = 2 * f->nbitmaps * f->steps;
   last = f->nentries;
