@@ -416,6 +416,17 @@ def config5_leg(D, idx, text: bytes, backend: str, qlen: int, nq: int, steps: in
     el = D.max(time.perf_counter() - t0)
     K.transfer_to_cpu(r)
     res = r.array().copy()
+    # host memory to host memory on every rank (config #5's wall
+    # time across the GPUs): this rank's reads H2D, search, results D2H on the
+    # resident index, bracketed by barriers, max over ranks
+    D.barrier()
+    t0 = time.perf_counter()
+    K.transfer_to_gpu(idx, q, r)
+    K.search(idx, q, r)
+    K.transfer_to_cpu(r)
+    D.barrier()
+    e2e = D.max(time.perf_counter() - t0)
+    e2e_eq = D.gather(bool(np.array_equal(r.array(), res)))
     sel = np.linspace(0, nq - 1, min(100_000, nq)).astype(np.int64)
     src = oracle_idx if oracle_idx is not None else idx
     img_idx = src.alt_counters()[0] if ac else src
@@ -431,7 +442,11 @@ def config5_leg(D, idx, text: bytes, backend: str, qlen: int, nq: int, steps: in
     out = {"what": f"config #5 shape: {nq // 1_000_000}M x {qlen} bp reads per GPU (seed 20 + rank), "
                    f"{D.world} GPU(s), index replicated",
            "mqps": round(total * steps / el / 1e6, 2), "ms_per_step": round(el / steps * 1e3, 4),
-           "lf_ms_per_rank": lfs, "oracle_sample_ok_per_rank": oks, "oracle_sample_per_rank": int(sel.size)}
+           "lf_ms_per_rank": lfs, "oracle_sample_ok_per_rank": oks, "oracle_sample_per_rank": int(sel.size),
+           "host_to_host": {"wall_s": round(e2e, 4), "mqps": round(total / e2e / 1e6, 2),
+                            "results_equal_per_rank": e2e_eq,
+                            "what": "every rank: its reads (pageable host memory) H2D + search + results D2H "
+                                    "on the resident index, barriers around, max over ranks"}}
     if ingest:
         # this rank's shard as a FASTA file -> results (host parser and device parser)
         try:
