@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round-2 session AY: default bench (config #5 host-to-host leg incl. the streamed path)
+# and N = 2 rehearsal on the one card.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-/root/repo}
+OUT=$R/gpurun_out
+mkdir -p $OUT
+export TMPDIR=/tmp
+cd $R
+cd /tmp
+timeout -k 10 600 python3 $R/bench.py > $OUT/bench_r2ay.json 2> $OUT/bench_r2ay.log || { tail -30 $OUT/bench_r2ay.log; exit 32; }
+cut -c1-300 $OUT/bench_r2ay.json
+timeout -k 10 700 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 $R/bench.py --gpus 2 --steps 10 --warmup 5 --ref-size 1000000000 --queries 2000000 --config5-queries 2000000 > $OUT/bench_r2ay_n2.json 2> $OUT/bench_r2ay_n2.log || { tail -30 $OUT/bench_r2ay_n2.log; exit 33; }
+cut -c1-300 $OUT/bench_r2ay_n2.json
