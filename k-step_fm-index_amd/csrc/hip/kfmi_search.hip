@@ -1122,7 +1122,7 @@ void query_geometry(kfmi_dev_queries* dq, uint32_t K)
 int32_t upload_queries(kfmi_qrys_t* q, uint32_t K, int dev, DevCtx* ctx)
 {
   if (q->size == 0 || K == 0) return KFMI_E_BAD_ARGUMENT;
-  if (64ull * q->size > 160ull * 1024) return KFMI_E_BAD_ARGUMENT;       /* pack tile must fit LDS */
+  if (64ull * q->size + 16 > 160ull * 1024) return KFMI_E_BAD_ARGUMENT;   /* pack tile (64 rows + 16 B) must fit LDS */
   kfmi_dev_queries* dq = new (std::nothrow) kfmi_dev_queries();
   if (!dq) return KFMI_E_ALLOCATING_MFASTA;
   dq->device = dev;

@@ -317,7 +317,7 @@ extern "C" int32_t kfmi_search_stream(void* index, const char* ascii, uint64_t n
   if (!f->dev) return KFMI_E_NOT_ON_DEVICE;
   kfmi_dev_index* di = f->dev;
   const uint32_t K = di->K;
-  if (size == 0 || size % K || 64ull * size > 160ull * 1024) return KFMI_E_BAD_ARGUMENT;
+  if (size == 0 || size % K || 64ull * size + 16 > 160ull * 1024) return KFMI_E_BAD_ARGUMENT;
   DevCtx* ctx = nullptr;
   int32_t err = ctx_for(di->device, &ctx);
   if (err) return err;

@@ -249,13 +249,16 @@ def test_long_reads_fused_limit_and_pack_fallback(gpu, oracle_mod, random_index,
     for k, d in ((2, 64), (1, 64)):
         idx = idxs[(k, d)]
         ref_img = idx.alt_counters()[0].image() if backend in ALT else idx.image()
-        for m in (254, 256, 258, 300, 1000):
+        for m in (254, 256, 258, 300, 1000, 2558):
             if m % k:
                 continue
-            q = _reads(text, 1500, m, seed=m * 3 + k)
+            q = _reads(text, 1500 if m < 2000 else 300, m, seed=m * 3 + k)
             want, _ = oracle_mod.search(ref_img, q)
             got = gpu.search_array(idx, q, backend)
             assert np.array_equal(got, want), (backend, k, m)
+        # the pack kernel stages 64 rows + 16 B in LDS (160 KiB): 2559 bases at most
+        with pytest.raises(gpu.KfmiError):
+            gpu.search_array(idx, _reads(text, 64, 2560, seed=7), backend)
 
 
 @pytest.mark.parametrize("backend", ["task-mid", "task", "task-ac", "task-packed", "task-ac128"])
