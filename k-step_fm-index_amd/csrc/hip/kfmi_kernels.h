@@ -434,7 +434,9 @@ static hipError_t launch_locate(const SearchLaunch& a)
   if constexpr (locate_coop_ok<G>()) {   /* MID lines: one round trip per step (KFMI_LOCATE_COOP=0: per-lane walk) */
     const char* e = getenv("KFMI_LOCATE_COOP");
     if (!e || atoi(e)) {
-      if (blocks > (uint64_t) cus * 4) blocks = (uint64_t) cus * 4;   /* 33-34 KB of LDS per workgroup */
+      /* 32 KB of LDS per workgroup: 5 fit a CU (4 measured the same within 2 %,
+       * profiles/r02/locate_r2ba.jsonl: the walk is not short of lines in flight) */
+      if (blocks > (uint64_t) cus * 5) blocks = (uint64_t) cus * 5;
       hipLaunchKernelGGL((locate_coop_kernel<G>), dim3((uint32_t) blocks), dim3(256), 0, a.st, a.ix, a.sa, a.sa_log2,
                          a.owner, a.total, a.pos, a.slot_ctr);
       return hipGetLastError();

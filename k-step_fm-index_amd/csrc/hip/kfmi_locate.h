@@ -205,11 +205,9 @@ __global__ __launch_bounds__(256) void locate_coop_kernel(IdxArgs ix, const uint
   constexpr int TPR = LB / 16;      // lanes per line
   constexpr int RPR = 64 / TPR;     // lines per 1 KiB round
   static_assert(locate_coop_ok<G>(), "MID lines of 16..128 bytes");
-  __shared__ __attribute__((aligned(16))) uint8_t lds[4 * 64 * LB];
-  __shared__ uint32_t tabs[4 * 64];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[4 * 64 * LB];   // 32 KiB at 128-B lines: 5 workgroups per CU
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   uint8_t* wl = lds + wave * 64 * LB;
-  uint32_t* tab = tabs + wave * 64;
   const uint8_t* base = reinterpret_cast<const uint8_t*>(ix.ent);
   const uint32_t mask = (1u << rate_log2) - 1u;
   WaveSlots ws;
@@ -229,11 +227,10 @@ __global__ __launch_bounds__(256) void locate_coop_kernel(IdxArgs ix, const uint
     const bool step = act && !smp && ds < 0;
     uint32_t p = 0;
     if (smp) p = sa[r >> rate_log2];
-    tab[lane] = step ? r / (uint32_t) (2 * G::D) : 0xFFFFFFFFu;   // this lane's MID line, or none
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const uint32_t mine = step ? r / (uint32_t) (2 * G::D) : 0xFFFFFFFFu;   // this lane's MID line, or none
 #pragma unroll
     for (int rr = 0; rr < 64 / RPR; ++rr) {
-      const uint32_t li = tab[rr * RPR + g];
+      const uint32_t li = __shfl(mine, rr * RPR + g);   // line of lane rr*RPR+g (no LDS table)
       if (li != 0xFFFFFFFFu)
         __builtin_amdgcn_global_load_lds((const void*) (base + (uint64_t) li * LB + 16 * k),
                                          (__attribute__((address_space(3))) void*) (wl + rr * 1024), 16, 0, 0);
