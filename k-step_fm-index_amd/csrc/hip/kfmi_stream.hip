@@ -309,18 +309,18 @@ extern "C" int32_t kfmi_stream_release(void)
   return KFMI_SUCCESS;
 }
 
-extern "C" int32_t kfmi_search_stream(void* index, const char* ascii, uint64_t num, uint32_t size,
-                                      uint32_t* results, uint64_t chunk)
+/* One device's streamed search of `num` reads (the whole batch, or one member's
+ * slice of a device group).  ms3 = {wall, host packing/staging, blocked on
+ * the GPU}; *npacked = reads sent as host-packed words. */
+static int32_t stream_on(kfmi_dev_index* di, const char* ascii, uint64_t num, uint32_t size, uint32_t* results,
+                         uint64_t chunk, uint32_t ftab, double* ms3, uint64_t* npacked_out)
 {
-  kfmi_fmi_t* f = (kfmi_fmi_t*) index;
-  if (!f || (!ascii && num) || (!results && num)) return KFMI_E_BAD_ARGUMENT;
-  if (!f->dev) return KFMI_E_NOT_ON_DEVICE;
-  kfmi_dev_index* di = f->dev;
   const uint32_t K = di->K;
-  if (size == 0 || size % K || 64ull * size + 16 > 160ull * 1024) return KFMI_E_BAD_ARGUMENT;
   DevCtx* ctx = nullptr;
   int32_t err = ctx_for(di->device, &ctx);
   if (err) return err;
+  ms3[0] = ms3[1] = ms3[2] = 0;
+  *npacked_out = 0;
   if (num == 0) return KFMI_SUCCESS;
   /* KFMI_STREAM_HOSTPACK: 1 = every chunk packed on the host, 0 = every chunk
    * sent as ASCII (packed on the device), 3 = alternate (testing), unset / 2 =
@@ -366,7 +366,7 @@ extern "C" int32_t kfmi_search_stream(void* index, const char* ascii, uint64_t n
   const auto t0 = std::chrono::steady_clock::now();
   const Op op = is_coop(di->backend) ? Op::Coop : Op::Task;
   IdxArgs ix = idx_args(di);
-  err = use_ftab(di, ctx->st, ix, ftab_bases());
+  err = use_ftab(di, ctx->st, ix, ftab);   /* the caller's setting (member threads have their own) */
   if (err) return err;
   int32_t status = KFMI_SUCCESS;
   using clk = std::chrono::steady_clock;
@@ -456,12 +456,57 @@ extern "C" int32_t kfmi_search_stream(void* index, const char* ascii, uint64_t n
     s.busy = true;
   }
   for (int k = 0; k < nslot; ++k) retire(pool.slot[k]);
-  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  t_ms[0] = ms;
-  t_ms[1] = host_ms;   /* host packing or staging copies */
-  t_ms[2] = wait_ms;   /* blocked on chunks in flight */
-  t_stream_packed_frac = num ? (double) npacked / (double) num : 0.0;
+  ms3[0] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  ms3[1] = host_ms;   /* host packing or staging copies */
+  ms3[2] = wait_ms;   /* blocked on chunks in flight */
+  *npacked_out = npacked;
   return status;
+}
+
+/* Streamed search of host reads into host results.  On a device group
+ * (KFMI_DEVICES / kfmi_set_devices, index transferred to the group) the batch
+ * is cut into one contiguous slice per member (multiples of 64 reads) and
+ * every member streams its slice on its own replica from its own host thread;
+ * the members' host packing shares the one worker pool (taking turns), their
+ * copies and kernels overlap on their devices.  Timings: the slowest member. */
+extern "C" int32_t kfmi_search_stream(void* index, const char* ascii, uint64_t num, uint32_t size,
+                                      uint32_t* results, uint64_t chunk)
+{
+  kfmi_fmi_t* f = (kfmi_fmi_t*) index;
+  if (!f || (!ascii && num) || (!results && num)) return KFMI_E_BAD_ARGUMENT;
+  GroupIndex* g = (GroupIndex*) f->grp;
+  if (!g && !f->dev) return KFMI_E_NOT_ON_DEVICE;
+  const uint32_t K = g ? g->di[0]->K : f->dev->K;
+  if (size == 0 || size % K || 64ull * size + 16 > 160ull * 1024) return KFMI_E_BAD_ARGUMENT;
+  double ms[KFMI_MAX_GROUP][3] = {};
+  uint64_t np[KFMI_MAX_GROUP] = {};
+  int32_t err = KFMI_SUCCESS;
+  const uint32_t ftab = ftab_bases();
+  if (!g) {
+    err = stream_on(f->dev, ascii, num, size, results, chunk, ftab, ms[0], &np[0]);
+  } else {
+    const int n = g->n;
+    uint64_t per = (num + n - 1) / n;
+    per = (per + 63) & ~63ull;
+    int32_t errs[KFMI_MAX_GROUP] = {};
+    std::vector<std::thread> th;
+    th.reserve(n);
+    for (int i = 0; i < n; ++i) {
+      const uint64_t a = per * i < num ? per * i : num, b = per * (i + 1) < num ? per * (i + 1) : num;
+      th.emplace_back([&, i, a, b] {
+        errs[i] = stream_on(g->di[i], ascii + a * size, b - a, size, results + 2 * a, chunk, ftab, ms[i], &np[i]);
+      });
+    }
+    for (auto& t : th) t.join();
+    for (int i = 0; i < n && !err; ++i) err = errs[i];
+    for (int i = 1; i < n; ++i) {
+      for (int k = 0; k < 3; ++k) ms[0][k] = std::max(ms[0][k], ms[i][k]);
+      np[0] += np[i];
+    }
+  }
+  for (int k = 0; k < 3; ++k) t_ms[k] = ms[0][k];
+  t_stream_packed_frac = num ? (double) np[0] / (double) num : 0.0;
+  return err;
 }
 
 }  // namespace kfmi

@@ -78,6 +78,33 @@ def test_group_equals_single_device(setup, backend, group, num):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("backend", ["task-mid", "coop-mid", "task-ac"])
+@pytest.mark.parametrize("group", [[0, 0], [0, 0, 0]])
+def test_group_streamed_search_equals_single_device(setup, backend, group):
+    """kfmi_search_stream on a device group: one slice per member, each
+    streamed on its own replica from its own host thread."""
+    K, idx, reads = setup
+    K.set_backend(backend)
+    K.set_devices([])
+    _, _, want = run_trio(K, idx, reads)
+    try:
+        K.set_devices(group)
+        K.transfer_to_gpu(idx, None, None)
+        for num in (reads.shape[0], 130, 64, 1, 0):
+            sub = np.ascontiguousarray(reads[:num])
+            got = K.search_stream(idx, sub, chunk=257)
+            assert np.array_equal(got, want[:2 * num]), (backend, group, num)
+        K.set_ftab(8)                     # the caller's per-thread setting reaches the members
+        try:
+            assert np.array_equal(K.search_stream(idx, reads), want)
+        finally:
+            K.set_ftab(0)
+    finally:
+        K.set_devices([])
+        idx.free_gpu()
+
+
+@pytest.mark.gpu
 def test_group_locate_and_mode_switch(setup):
     K, idx, reads = setup
     K.set_backend("task-mid")
