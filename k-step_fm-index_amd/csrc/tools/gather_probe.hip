@@ -14,6 +14,10 @@
  *   mask<G>: as indep / chain1, but each wave issues every gather as G
  *            instructions with 64/G active lanes (fewer distinct pages per
  *            instruction -- the translation-reach question)
+ *   PROBE_CPOL=1: the coop 128-B gather with sc0 / sc1 / nt cache-policy
+ *            bits on its loads; PROBE_ALLOC=uncached: the table allocated
+ *            uncached -- whether any load path beats the random-line
+ *            request ceiling
  * Addresses come from a per-lane xorshift generator (no index array traffic).
  */
 #include <hip/hip_runtime.h>
@@ -167,6 +171,43 @@ __global__ __launch_bounds__(256) void k_chain_masked(const uint4* __restrict__ 
   if (acc == 0x12345678u) sink[0] = acc;
 }
 
+/* coop 128-B gather with explicit cache-policy bits (PROBE_CPOL=1), through
+ * raw buffer loads (bounds-checked: an out-of-range offset reads 0, never
+ * faults).  aux: sc0 = 1, nt = 2, sc1 = 16.  The table must be < 4 GB. */
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t table_rsrc(const void* t, uint64_t bytes)
+{
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(t), (short) 0, (int) (uint32_t) bytes, 0x00020000);
+}
+
+template <int AUX>
+__global__ __launch_bounds__(256) void k_coop_pol(const uint4* __restrict__ t, uint64_t nlines, uint64_t per_group,
+                                                  uint32_t* __restrict__ sink)
+{
+  constexpr int TPR = 8;
+  const __amdgpu_buffer_rsrc_t rs = table_rsrc(t, nlines * 128);
+  const int lane = threadIdx.x & 63, k = lane % TPR;
+  uint64_t s = 0x9E3779B97F4A7C15ull ^ (((uint64_t) blockIdx.x * 256 + threadIdx.x) / TPR) * 0xBF58476D1CE4E5B9ull;
+  uint32_t acc = 0;
+  for (uint64_t i = 0; i < per_group; i += 4) {
+    v4u v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      v[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int) (uint32_t) (pick(xs(s), nlines) * 128 + 16 * k), 0, AUX);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc ^= v[j].x ^ v[j].w;
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
+/* one buffer load of the table's last 16 B: the descriptor reads real data */
+__global__ void k_rsrc_check(const uint4* __restrict__ t, uint64_t bytes, uint32_t* __restrict__ out)
+{
+  const v4u v = __builtin_amdgcn_raw_buffer_load_b128(table_rsrc(t, bytes), (int) (uint32_t) (bytes - 16), 0, 0);
+  out[0] = v.x;
+}
+
 static float timed(hipEvent_t a, hipEvent_t b)
 {
   float ms;
@@ -187,6 +228,8 @@ int main(int argc, char** argv)
   const char* mode = getenv("PROBE_ALLOC") ? getenv("PROBE_ALLOC") : "default";
   if (!strcmp(mode, "contig")) {
     CHECK(hipExtMallocWithFlags((void**) &t, bytes, hipDeviceMallocContiguous));
+  } else if (!strcmp(mode, "uncached")) {
+    CHECK(hipExtMallocWithFlags((void**) &t, bytes, hipDeviceMallocUncached));
   } else if (!strcmp(mode, "vmm")) {
     hipMemAllocationProp prop = {};
     prop.type = hipMemAllocationTypePinned;
@@ -232,6 +275,26 @@ int main(int argc, char** argv)
            ms, nlines / ms / 1e6, nlines * lb / ms / 1e6);
     fflush(stdout);
   };
+  if (getenv("PROBE_CPOL")) {
+    if (bytes >= (1ull << 32)) { fprintf(stderr, "PROBE_CPOL: table must be < 4 GB\n"); return 1; }
+    uint32_t chk = 0;
+    hipLaunchKernelGGL(k_rsrc_check, dim3(1), dim3(1), 0, 0, t, bytes, sink);
+    CHECK(hipMemcpy(&chk, sink, 4, hipMemcpyDeviceToHost));
+    printf("{\"rsrc_check\": \"0x%08x\", \"ok\": %s}\n", chk, chk == 0x5a5a5a5au ? "true" : "false");
+    const uint64_t pg = (lines_target / (threads / 8) + 3) & ~3ull;
+    const double nl = (double) pg * (threads / 8);
+    run("coop_plain", 128, [&] { hipLaunchKernelGGL((k_coop_pol<0>), grid, blk, 0, 0, t, bytes / 128, pg, sink); }, nl);
+    run("coop_sc0", 128, [&] { hipLaunchKernelGGL((k_coop_pol<1>), grid, blk, 0, 0, t, bytes / 128, pg, sink); }, nl);
+    run("coop_nt", 128, [&] { hipLaunchKernelGGL((k_coop_pol<2>), grid, blk, 0, 0, t, bytes / 128, pg, sink); }, nl);
+    run("coop_sc0_nt", 128, [&] { hipLaunchKernelGGL((k_coop_pol<3>), grid, blk, 0, 0, t, bytes / 128, pg, sink); }, nl);
+    run("coop_sc1", 128, [&] { hipLaunchKernelGGL((k_coop_pol<16>), grid, blk, 0, 0, t, bytes / 128, pg, sink); }, nl);
+    run("coop_sc0_sc1", 128, [&] { hipLaunchKernelGGL((k_coop_pol<17>), grid, blk, 0, 0, t, bytes / 128, pg, sink); }, nl);
+    run("coop_sc1_nt", 128, [&] { hipLaunchKernelGGL((k_coop_pol<18>), grid, blk, 0, 0, t, bytes / 128, pg, sink); }, nl);
+    run("coop_sc0_sc1_nt", 128, [&] { hipLaunchKernelGGL((k_coop_pol<19>), grid, blk, 0, 0, t, bytes / 128, pg, sink); }, nl);
+    run("coop_ref", 128, [&] { hipLaunchKernelGGL((k_coop<128>), grid, blk, 0, 0, t, bytes / 128, pg, sink); }, nl);
+    if (strcmp(mode, "vmm")) CHECK(hipFree(t));
+    return 0;
+  }
   if (getenv("PROBE_MASK")) {
     const uint64_t pt = (lines_target / threads + 3) & ~3ull;
     const uint32_t st = (uint32_t) (lines_target / threads);
