@@ -158,9 +158,10 @@ int32_t     kfmi_set_ftab(uint32_t bases);
  * h_results; results equal the single-device ones.  A device may be listed
  * twice (two replicas on one GPU).  n = 0 returns to single-device mode, n = 1
  * equals kfmi_set_device.  Per calling thread.  kfmi_locate works on group
- * handles (each device locates its slice); kfmi_count_blocks and
- * kfmi_search_stream stay single-device (KFMI_E_NOT_IMPLEMENTED / not on
- * device for group handles). */
+ * handles (each device locates its slice), so does kfmi_search_stream (one
+ * slice and host thread per member), and reads parsed on a device
+ * (kfmi_load_queries_gpu) reach the members device to device;
+ * kfmi_count_blocks stays single-device (KFMI_E_NOT_IMPLEMENTED). */
 int32_t     kfmi_set_devices(const int32_t *devices, int32_t n);
 /* The device list (returns its length; 0 = single-device mode). */
 int32_t     kfmi_get_devices(int32_t *devices, int32_t cap);

@@ -154,6 +154,44 @@ static int32_t each_member(int n, F fn)
   return KFMI_SUCCESS;
 }
 
+/* Reads [q0, q0 + n) of device-resident reads `src` (any device) as their own
+ * device batch on `dev`: the ASCII rows copied device to device (a local copy
+ * on src's own device, hipMemcpyPeerAsync over xGMI otherwise). */
+static int32_t slice_device_queries(const kfmi_dev_queries* src, uint64_t q0, uint64_t n, uint32_t K, int dev,
+                                    DevCtx* ctx, kfmi_dev_queries** out)
+{
+  *out = nullptr;
+  kfmi_dev_queries* dq = new (std::nothrow) kfmi_dev_queries();
+  if (!dq) return KFMI_E_ALLOCATING_MFASTA;
+  dq->device = dev;
+  dq->num = n;
+  dq->size = src->size;
+  query_geometry(dq, K);
+  const uint64_t bytes = n * (uint64_t) src->size;
+  if (hipMalloc((void**) &dq->ascii, bytes + 16) != hipSuccess ||
+      hipMalloc((void**) &dq->packed, 4ull * (dq->nwords + 1) * (n ? n : 1)) != hipSuccess) {
+    free_dev_queries(dq);
+    return KFMI_E_DEVICE_ALLOC;
+  }
+  dq->packed_rows = dq->nwords + 1;
+  if (bytes) {
+    int can = 0;
+    if (dev != src->device && hipDeviceCanAccessPeer(&can, dev, src->device) == hipSuccess && can &&
+        hipDeviceEnablePeerAccess(src->device, 0) != hipSuccess)
+      (void) hipGetLastError();   /* already enabled: fine; else the runtime stages the copy */
+    const uint8_t* from = src->ascii + q0 * src->size;
+    const hipError_t ce = dev == src->device
+                              ? hipMemcpyAsync(dq->ascii, from, bytes, hipMemcpyDeviceToDevice, ctx->st)
+                              : hipMemcpyPeerAsync(dq->ascii, dev, from, src->device, bytes, ctx->st);
+    if (ce != hipSuccess || hipStreamSynchronize(ctx->st) != hipSuccess) {
+      free_dev_queries(dq);
+      return KFMI_E_KERNEL;
+    }
+  }
+  *out = dq;
+  return KFMI_SUCCESS;
+}
+
 int32_t group_transfer(kfmi_fmi_t* f, kfmi_qrys_t* q, kfmi_res_t* r, const int* devs, int n)
 {
   const int backend = f ? backend_for(f->steps) : kfmi_backend();
@@ -207,19 +245,27 @@ int32_t group_transfer(kfmi_fmi_t* f, kfmi_qrys_t* q, kfmi_res_t* r, const int* 
   }
   if (q) {
     if (!f) return KFMI_E_BAD_ARGUMENT;
-    if (!q->h_queries && q->num) return KFMI_E_NOT_IMPLEMENTED;   /* device-parsed reads stay on their device */
+    /* reads parsed on a device (kfmi_load_queries_gpu) have no host copy: the
+     * members take their slices device to device from the parsing device, and
+     * that copy (q->dev) stays with the handle */
+    const bool parsed = !q->h_queries && q->num;
+    if (parsed && !q->dev) return KFMI_E_NOT_ON_DEVICE;
     group_free_queries(q);
-    if (q->dev) {
+    if (q->dev && !parsed) {
       free_dev_queries(q->dev);
       q->dev = nullptr;
     }
     GroupSlices* g = group_slices(q->num, devs, n);
     if (!g) return KFMI_E_ALLOCATING_MFASTA;
     q->grp = g;
-    /* every slice over its own device's PCIe link at the same time */
+    /* every slice over its own device's PCIe link (or xGMI link) at the same time */
     err = each_member(n, [&](int i) {
       DevCtx* ctx = nullptr;
       int32_t e = ctx_for(devs[i], &ctx);
+      if (!e && parsed) {
+        e = slice_device_queries(q->dev, g->q0[i], g->num[i], f->steps, devs[i], ctx, &g->dq[i]);
+        return e;
+      }
       kfmi_qrys_t sh{};
       sh.num = g->num[i];
       sh.size = q->size;

@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round-2 session BD: device-parsed reads on device groups (slices device to
+# device from the parsing device) -- group, ingest and stream tests.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-/root/repo}
+OUT=$R/gpurun_out
+mkdir -p $OUT
+export TMPDIR=/tmp
+cd $R
+timeout -k 10 500 python3 -u -m pytest tests/test_groups.py tests/test_ingest.py tests/test_stream.py -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/gpu_tests_r2bd.log 2>&1 || { tail -40 $OUT/gpu_tests_r2bd.log; exit 31; }
+tail -2 $OUT/gpu_tests_r2bd.log

@@ -187,26 +187,27 @@ def test_group_replication_setup_time(kfmi_mod):
 
 
 @pytest.mark.gpu
-def test_group_rejects_device_parsed_queries(setup, tmp_path):
-    """Reads parsed on the device (kfmi_load_queries_gpu) live on that device
-    only: a device group refuses them (KFMI_E_NOT_IMPLEMENTED) instead of
-    uploading an empty host copy; single-device mode takes them as they are."""
+@pytest.mark.parametrize("group", [[0, 0], [0, 0, 0]])
+def test_group_takes_device_parsed_queries(setup, tmp_path, group):
+    """Reads parsed on the device (kfmi_load_queries_gpu) have no host copy: a
+    device group gives every member its slice device to device from the
+    parsing device, which keeps its copy -- the same handle then still works
+    in single-device mode, and in group mode again."""
     K, idx, reads = setup
     path = tmp_path / "q.fa"
-    path.write_bytes(b"".join(b">r\n" + r.tobytes() + b"\n" for r in reads[:500]))
+    n = 2_999                                     # not a multiple of 64: a short last slice
+    path.write_bytes(b"".join(b">r\n" + r.tobytes() + b"\n" for r in reads[:n]))
     K.set_backend("task-mid")
+    want = K.search_array(idx, reads[:n])
     q = K.Queries.load_gpu(path, 100)
-    r = K.Results.alloc(500)
+    r = K.Results.alloc(n)
     try:
-        K.set_devices([0, 0])
-        with pytest.raises(K.KfmiError) as e:
+        for devs in (group, [], group):
+            K.set_devices(devs)
             K.transfer_to_gpu(idx, q, r)
-        assert e.value.code == 19
-        K.set_devices([])
-        K.transfer_to_gpu(idx, q, r)
-        K.search(idx, q, r)
-        K.transfer_to_cpu(r)
-        assert np.array_equal(r.array(), K.search_array(idx, reads[:500]))
+            K.search(idx, q, r)
+            K.transfer_to_cpu(r)
+            assert np.array_equal(r.array(), want), devs
     finally:
         K.set_devices([])
         idx.free_gpu()
