@@ -170,6 +170,41 @@ def test_grp_locate_against_bruteforce(kfmi_mod):
 
 
 @pytest.mark.gpu
+def test_k4_results_located_through_a_k2_companion(kfmi_mod):
+    """The rows of [L, R) are suffix-array ranks, the same for every K of one
+    text: K = 4 results (coop-grp) are located through a K = 2 index of the
+    same text (the cooperative MID walk, one line per step) -- positions equal
+    the brute-force suffix array and the K = 4 index's own (per-lane) walk."""
+    K = kfmi_mod
+    t = _text(50_021, 9, repeats=True)
+    text = t.tobytes()
+    sa = util.suffix_array(text + b"$")
+    i4 = K.Index.build(text, k=4, d=64, gpu=True, sa_rate=8)
+    i2 = K.Index.build(text, k=2, d=64, gpu=True, sa_rate=8)
+    q = _reads(t, 3000, 100, 6)
+    try:
+        K.set_backend("coop-grp")
+        qq, r = K.Queries.from_array(q), K.Results.alloc(q.shape[0])
+        K.transfer_to_gpu(i4, qq, r)
+        K.search(i4, qq, r)
+        own = K.locate(i4, r)
+        K.set_backend("task-mid")
+        K.transfer_to_gpu(i2, None, None)
+        loc = K.locate(i2, r)                    # K = 4 results, K = 2 walk
+        K.transfer_to_cpu(r)
+        res = r.array()
+        off, pos = loc.offsets(), loc.positions()
+        assert np.array_equal(off, own.offsets()) and np.array_equal(pos, own.positions())
+        for i in range(q.shape[0]):
+            L, R = int(res[2 * i]), int(res[2 * i + 1])
+            assert [int(x) for x in pos[off[i]:off[i + 1]]] == [int(x) for x in sa[L:R]], i
+        loc.close(); own.close(); qq.close(); r.close()
+    finally:
+        i4.free_gpu(); i2.free_gpu()
+        i4.close(); i2.close()
+
+
+@pytest.mark.gpu
 def test_k4_index_under_the_implicit_default_backend(kfmi_mod, oracle_mod, tmp_path):
     """No KFMI_BACKEND, no kfmi_set_backend: a K = 4 index is uploaded for
     coop-grp (the default task-mid has no K = 4 geometry).  Fresh process, so
