@@ -160,8 +160,8 @@ int32_t     kfmi_set_ftab(uint32_t bases);
  * equals kfmi_set_device.  Per calling thread.  kfmi_locate works on group
  * handles (each device locates its slice), so does kfmi_search_stream (one
  * slice and host thread per member), and reads parsed on a device
- * (kfmi_load_queries_gpu) reach the members device to device;
- * kfmi_count_blocks stays single-device (KFMI_E_NOT_IMPLEMENTED). */
+ * (kfmi_load_queries_gpu) reach the members device to device, and
+ * kfmi_count_blocks sums the members' slices. */
 int32_t     kfmi_set_devices(const int32_t *devices, int32_t n);
 /* The device list (returns its length; 0 = single-device mode). */
 int32_t     kfmi_get_devices(int32_t *devices, int32_t cap);

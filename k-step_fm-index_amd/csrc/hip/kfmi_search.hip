@@ -1353,15 +1353,36 @@ extern "C" void searchIndexGPU(void* index, void* queries, void* resIntervals)
   if (e) fprintf(stderr, "kstepfmi: searchIndexGPU failed: %s\n", errorCommon(e));
 }
 
+static int32_t count_on(kfmi_dev_index* di, kfmi_dev_queries* dq, uint64_t* blocks);
+
+/* Distinct d-blocks the batch's LF steps touch (SURVEY 8(d) algorithmic bytes);
+ * on a device group the sum over the members' slices. */
 extern "C" int32_t kfmi_count_blocks(void* index, void* queries, uint64_t* blocks)
 {
   kfmi_fmi_t* f = (kfmi_fmi_t*) index;
   kfmi_qrys_t* q = (kfmi_qrys_t*) queries;
   if (!f || !q || !blocks) return KFMI_E_BAD_ARGUMENT;
-  if (f->grp || q->grp) return KFMI_E_NOT_IMPLEMENTED;   /* single-device API */
+  if (f->grp || q->grp) {
+    GroupIndex* gi = (GroupIndex*) f->grp;
+    GroupSlices* gq = (GroupSlices*) q->grp;
+    if (!gi || !gq) return KFMI_E_NOT_ON_DEVICE;   /* handles moved to different modes */
+    if (gq->n != gi->n) return KFMI_E_BAD_ARGUMENT;
+    uint64_t sum = 0;
+    for (int i = 0; i < gi->n; ++i) {
+      uint64_t b = 0;
+      const int32_t e = count_on(gi->di[i], gq->dq[i], &b);
+      if (e) return e;
+      sum += b;
+    }
+    *blocks = sum;
+    return KFMI_SUCCESS;
+  }
   if (!f->dev || !q->dev) return KFMI_E_NOT_ON_DEVICE;
-  kfmi_dev_index* di = f->dev;
-  kfmi_dev_queries* dq = q->dev;
+  return count_on(f->dev, q->dev, blocks);
+}
+
+static int32_t count_on(kfmi_dev_index* di, kfmi_dev_queries* dq, uint64_t* blocks)
+{
   DevCtx* ctx = nullptr;
   int32_t err = ctx_for(di->device, &ctx);
   if (err) return err;

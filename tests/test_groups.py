@@ -112,11 +112,13 @@ def test_group_locate_and_mode_switch(setup):
     q, r, want = run_trio(K, idx, reads)
     loc1 = K.locate(idx, r)
     single_bytes = idx.device_bytes()
+    blocks1 = K.count_blocks(idx, q)
     q.close(); r.close()
     try:
         K.set_devices([0, 0, 0])
         q, r, got = run_trio(K, idx, reads)
         assert np.array_equal(got, want)
+        assert K.count_blocks(idx, q) == blocks1 > 0          # sum over the members' slices
         loc3 = K.locate(idx, r)
         assert np.array_equal(loc3.offsets(), loc1.offsets())
         assert np.array_equal(loc3.positions(), loc1.positions())
