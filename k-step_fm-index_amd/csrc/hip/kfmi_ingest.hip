@@ -110,28 +110,29 @@ __global__ __launch_bounds__(256) void fa_rows(const uint8_t* __restrict__ raw, 
                                                const uint64_t* __restrict__ starts, uint64_t num, uint32_t m,
                                                uint32_t* __restrict__ out, unsigned long long* __restrict__ first_bad)
 {
-  const uint64_t w = (uint64_t) blockIdx.x * 256 + threadIdx.x;
   const uint64_t total = num * m;
-  if (4 * w >= total) return;
-  uint32_t word = 0;
+  /* grid-stride: more than 16 GB of reads exceed the 2^32 work-items of one dispatch */
+  for (uint64_t w = (uint64_t) blockIdx.x * 256 + threadIdx.x; 4 * w < total; w += (uint64_t) gridDim.x * 256) {
+    uint32_t word = 0;
 #pragma unroll
-  for (int b = 0; b < 4; ++b) {
-    const uint64_t o = 4 * w + b;
-    if (o >= total) break;
-    const uint64_t q = o / m;
-    const uint32_t j = (uint32_t) (o - q * m);
-    const uint64_t s = starts[q] + j;
-    const uint32_t ch = s < n ? raw[s] : (uint32_t) '\n';   /* past the end: the read is short */
-    bool bad = ch == '\n';
-    if (j == m - 1 && !bad) {   /* what follows the read: '\r'* then '\n' or the end of the file */
-      uint64_t p = s + 1;
-      while (p < n && raw[p] == '\r') ++p;
-      bad = !(p >= n || raw[p] == '\n');
+    for (int b = 0; b < 4; ++b) {
+      const uint64_t o = 4 * w + b;
+      if (o >= total) break;
+      const uint64_t q = o / m;
+      const uint32_t j = (uint32_t) (o - q * m);
+      const uint64_t s = starts[q] + j;
+      const uint32_t ch = s < n ? raw[s] : (uint32_t) '\n';   /* past the end: the read is short */
+      bool bad = ch == '\n';
+      if (j == m - 1 && !bad) {   /* what follows the read: '\r'* then '\n' or the end of the file */
+        uint64_t p = s + 1;
+        while (p < n && raw[p] == '\r') ++p;
+        bad = !(p >= n || raw[p] == '\n');
+      }
+      if (bad) atomicMin(first_bad, (unsigned long long) q);
+      word |= ch << (8 * b);
     }
-    if (bad) atomicMin(first_bad, (unsigned long long) q);
-    word |= ch << (8 * b);
+    out[w] = word;
   }
-  out[w] = word;
 }
 
 /* The file into device memory at dst (n bytes), through two pinned 64 MB
@@ -239,7 +240,8 @@ extern "C" int32_t kfmi_load_queries_gpu(const char* fn, uint32_t sizequery, uin
                        num, starts.as<uint64_t>());
     ok = ok && hipGetLastError() == hipSuccess;
     const uint64_t words = (abytes + 3) / 4;
-    hipLaunchKernelGGL(fa_rows, dim3((uint32_t) ((words + 255) / 256)), dim3(256), 0, st, raw.as<uint8_t>(), n,
+    const uint64_t rb = (words + 255) / 256;
+    hipLaunchKernelGGL(fa_rows, dim3((uint32_t) (rb < (1u << 22) ? rb : (1u << 22))), dim3(256), 0, st, raw.as<uint8_t>(), n,
                        starts.as<uint64_t>(), num, sizequery, reinterpret_cast<uint32_t*>(dq->ascii),
                        bad.as<unsigned long long>());
     ok = ok && hipGetLastError() == hipSuccess &&
