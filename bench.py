@@ -71,8 +71,10 @@ def parse():
     p.add_argument("--config5-qlen", type=int, default=150)
     p.add_argument("--no-kstep4", dest="kstep4", action="store_false",
                    help="skip the K=4 (coop-grp) leg at N=1")
-    p.add_argument("--no-ingest", dest="ingest", action="store_false",
-                   help="skip the FASTA file -> loadQueries -> search -> results leg (f2)")
+    p.add_argument("--ingest", choices=("auto", "on", "off"), default="auto",
+                   help="FASTA file -> loadQueries -> search -> results legs (f2); auto: on at N <= 2 (each rank "
+                        "writes 2.6 GB of FASTA to TMPDIR and parses it on 16 host threads)")
+    p.add_argument("--no-ingest", dest="ingest", action="store_const", const="off", help="= --ingest off")
     p.add_argument("--no-md5", action="store_true")
     p.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic.json"))
     p.add_argument("--sa-rate", type=int, default=32,
@@ -133,9 +135,89 @@ class Dist:
         self.pg.all_gather_object(out, obj)
         return out
 
+    def all_ok(self, ok: bool) -> bool:
+        """True on every rank iff `ok` on every rank (one collective, every rank calls it)."""
+        if not self.pg:
+            return bool(ok)
+        import torch
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+        self.pg.all_reduce(t, op=self.pg.ReduceOp.MIN)
+        return bool(t.item())
+
     def close(self):
         if self.pg:
             self.pg.destroy_process_group()
+
+
+class Steps:
+    """A leg's local work on this rank, one step at a time: the first step that
+    raises ends the rank's local work for the leg (its error is kept), while the
+    leg itself keeps making every collective call (barrier, max, gather) in the
+    same order on every rank -- a rank that fails part-way never leaves the
+    others waiting at a barrier it skips.  Timed sections ask D.all_ok first and
+    are skipped by every rank together."""
+
+    def __init__(self):
+        self.err = None
+
+    @property
+    def ok(self) -> bool:
+        return self.err is None
+
+    def run(self, fn, *a, **kw):
+        if self.err is not None:
+            return None
+        try:
+            return fn(*a, **kw)
+        except Exception as e:          # reported in the leg's output, never fatal
+            self.err = f"{type(e).__name__}: {e}"
+            return None
+
+
+class Phases:
+    """Wall time of each bench phase on this rank, and the process's peak RSS."""
+
+    def __init__(self):
+        self.t = time.perf_counter()
+        self.rows = {}
+
+    def mark(self, name: str) -> None:
+        now = time.perf_counter()
+        self.rows[name] = round(self.rows.get(name, 0.0) + now - self.t, 2)
+        self.t = now
+
+    @staticmethod
+    def peak_rss_gb() -> float:
+        import resource
+        return round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1e6, 2)   # ru_maxrss is KiB
+
+
+def device_rows(D, dev: int) -> list:
+    """Every rank's (rank, local rank, device number, PCI bus id of that device),
+    in rank order on every rank: the bus id names the physical GPU, which device
+    numbers do not across processes (HIP_VISIBLE_DEVICES)."""
+    try:
+        bus = K.device_pci_bus_id(dev)
+    except K.KfmiError:
+        bus = None
+    return D.gather({"rank": D.rank, "local_rank": D.local, "device": dev, "pci_bus_id": bus,
+                     "host": os.uname().nodename})
+
+
+def aggregate_devices(rows: list) -> dict:
+    """Distinct physical GPUs behind the ranks (host + PCI bus id; a rank whose
+    bus id is unknown counts as its own GPU only if no other rank on its host
+    has the same device number).  shared_devices: two ranks on one GPU -- then
+    the run is a rehearsal, not a multi-GPU measurement."""
+    keys = []
+    for r in rows:
+        keys.append((r.get("host"), r["pci_bus_id"]) if r.get("pci_bus_id") else (r.get("host"), f"dev{r['device']}"))
+    per = {}
+    for k in keys:
+        per[k] = per.get(k, 0) + 1
+    distinct = len(per)
+    return {"distinct_devices": distinct, "shared_devices": distinct < len(rows),
+            "ranks_per_device": sorted(per.values(), reverse=True)}
 
 
 def cuda_sync(dev: int):
@@ -243,7 +325,7 @@ def ingest_leg(idx, reads: np.ndarray, res: np.ndarray, world: int) -> dict:
     out["mqps_file_to_results"] = round(n / tot / 1e6, 2)
     out["load_GB_per_s"] = round(out["file_bytes"] / out["load_s_parallel"] / 1e9, 2)
     out["results_equal"] = bool(np.array_equal(r2.array(), res))
-    out["host_threads"] = int(os.environ.get("KFMI_HOST_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    out["host_threads"] = K.host_threads()
     qp.close()
     r2.close()
     return out
@@ -397,89 +479,114 @@ def config5_leg(D, idx, text: bytes, backend: str, qlen: int, nq: int, steps: in
     80M x 150 bp batch at N = 8), searched on the resident index; timed like
     the main leg (barrier + synchronize, max over ranks), then an evenly spread
     100 K-read sample of every rank checked against the CPU oracle (on
-    `oracle_idx`'s image when given: another index of the same text)."""
+    `oracle_idx`'s image when given: another index of the same text).  Every
+    rank makes the same collective calls whatever fails locally (Steps)."""
     from oracle import oracle
-    reads = synth.gather_reads(text, synth.read_starts(len(text), nq, qlen, seed=20 + D.rank), qlen)
-    q = K.Queries.from_array(reads)
-    r = K.Results.alloc(nq)
-    K.set_backend(backend)
-    K.transfer_to_gpu(idx, q, r)
-    for _ in range(warmup):
-        K.search(idx, q, r)
-    D.barrier()
+    S = Steps()
+    h = {}
+
+    def setup():
+        h["reads"] = synth.gather_reads(text, synth.read_starts(len(text), nq, qlen, seed=20 + D.rank), qlen)
+        h["q"] = K.Queries.from_array(h["reads"])
+        h["r"] = K.Results.alloc(nq)
+        K.set_backend(backend)
+        K.transfer_to_gpu(idx, h["q"], h["r"])
+        for _ in range(warmup):
+            K.search(idx, h["q"], h["r"])
+
+    def timed(lf):
+        for _ in range(steps):
+            K.search(idx, h["q"], h["r"])
+            lf.append(K.last_timing()["lf_ms"])
+
+    def fetch():
+        K.transfer_to_cpu(h["r"])
+        h["res"] = h["r"].array().copy()
+
+    def host_to_host():
+        K.transfer_to_gpu(idx, h["q"], h["r"])
+        K.search(idx, h["q"], h["r"])
+        K.transfer_to_cpu(h["r"])
+
+    S.run(setup)
+    out = {"what": f"config #5 shape: {nq // 1_000_000}M x {qlen} bp reads per GPU (seed 20 + rank), "
+                   f"{D.world} GPU(s), index replicated"}
     lf = []
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        K.search(idx, q, r)
-        lf.append(K.last_timing()["lf_ms"])
-    D.barrier()
-    el = D.max(time.perf_counter() - t0)
-    K.transfer_to_cpu(r)
-    res = r.array().copy()
+    if D.all_ok(S.ok):
+        D.barrier()
+        t0 = time.perf_counter()
+        S.run(timed, lf)
+        D.barrier()
+        el = D.max(time.perf_counter() - t0)
+        S.run(fetch)
+        total = D.sum(float(nq))
+        out.update({"mqps": round(total * steps / el / 1e6, 2), "ms_per_step": round(el / steps * 1e3, 4),
+                    "lf_ms_per_rank": D.gather(round(float(np.mean(lf)), 4) if lf else None)})
     # host memory to host memory on every rank (SURVEY 8(d): config #5's wall
     # time across the GPUs): this rank's reads H2D, search, results D2H on the
     # resident index, bracketed by barriers, max over ranks
-    D.barrier()
-    t0 = time.perf_counter()
-    K.transfer_to_gpu(idx, q, r)
-    K.search(idx, q, r)
-    K.transfer_to_cpu(r)
-    D.barrier()
-    e2e = D.max(time.perf_counter() - t0)
-    e2e_eq = D.gather(bool(np.array_equal(r.array(), res)))
-    # the same through kfmi_search_stream (chunks packed to 2-bit words on the
-    # host, H2D / LF / D2H overlapped): one warm-up call, then one timed call
-    # (every rank makes the same collective calls whether or not its calls fail)
-    outb = np.empty(2 * nq, dtype=np.uint32)
-    err = None
-    try:
-        K.search_stream(idx, reads, out=outb)
-    except K.KfmiError as e:
-        err = str(e)
-    D.barrier()
-    t0 = time.perf_counter()
-    if err is None:
+    if D.all_ok(S.ok):
+        D.barrier()
+        t0 = time.perf_counter()
+        S.run(host_to_host)
+        D.barrier()
+        e2e = D.max(time.perf_counter() - t0)
+        e2e_eq = D.gather(S.ok and bool(np.array_equal(h["r"].array(), h["res"])))
+        out["host_to_host"] = {"wall_s": round(e2e, 4), "mqps": round(D.sum(float(nq)) / e2e / 1e6, 2),
+                               "results_equal_per_rank": e2e_eq,
+                               "what": "every rank: its reads (pageable host memory) H2D + search + results D2H "
+                                       "on the resident index, barriers around, max over ranks"}
+        # the same through kfmi_search_stream (chunks packed to 2-bit words on the
+        # host, H2D / LF / D2H overlapped): one warm-up call, then one timed call
+        outb = np.empty(2 * nq, dtype=np.uint32)
+        err = None
         try:
-            K.search_stream(idx, reads, out=outb)
+            K.search_stream(idx, h["reads"], out=outb)
         except K.KfmiError as e:
             err = str(e)
-    D.barrier()
-    sw = D.max(time.perf_counter() - t0)
-    errs = D.gather(err)
-    st_eq = D.gather(err is None and bool(np.array_equal(outb, res)))
-    if any(errs):
-        st = {"error_per_rank": errs}
-    else:
-        st = {"wall_s": round(sw, 4), "mqps": round(D.sum(float(nq)) / sw / 1e6, 2), "results_equal_per_rank": st_eq}
-    sel = np.linspace(0, nq - 1, min(100_000, nq)).astype(np.int64)
-    src = oracle_idx if oracle_idx is not None else idx
-    img_idx = src.alt_counters()[0] if ac else src
-    want, _ = oracle.search(img_idx.image(), reads[sel], nthreads=max(1, cpu_effective() // D.world))
-    ok = bool(np.array_equal(want.reshape(-1, 2), res.reshape(-1, 2)[sel]))
-    if ac:
-        img_idx.close()
-    oks = D.gather(ok)
-    lfs = D.gather(round(float(np.mean(lf)), 4))
-    total = D.sum(float(nq))
-    q.close()
-    r.close()
-    out = {"what": f"config #5 shape: {nq // 1_000_000}M x {qlen} bp reads per GPU (seed 20 + rank), "
-                   f"{D.world} GPU(s), index replicated",
-           "mqps": round(total * steps / el / 1e6, 2), "ms_per_step": round(el / steps * 1e3, 4),
-           "lf_ms_per_rank": lfs, "oracle_sample_ok_per_rank": oks, "oracle_sample_per_rank": int(sel.size),
-           "host_to_host": {"wall_s": round(e2e, 4), "mqps": round(total / e2e / 1e6, 2),
-                            "results_equal_per_rank": e2e_eq,
-                            "what": "every rank: its reads (pageable host memory) H2D + search + results D2H "
-                                    "on the resident index, barriers around, max over ranks",
-                            "streamed": st}}
+        D.barrier()
+        t0 = time.perf_counter()
+        if err is None:
+            try:
+                K.search_stream(idx, h["reads"], out=outb)
+            except K.KfmiError as e:
+                err = str(e)
+        D.barrier()
+        sw = D.max(time.perf_counter() - t0)
+        errs = D.gather(err)
+        st_eq = D.gather(err is None and bool(np.array_equal(outb, h["res"])))
+        if any(errs):
+            out["host_to_host"]["streamed"] = {"error_per_rank": errs}
+        else:
+            out["host_to_host"]["streamed"] = {"wall_s": round(sw, 4), "mqps": round(D.sum(float(nq)) / sw / 1e6, 2),
+                                               "results_equal_per_rank": st_eq,
+                                               "host_threads": K.host_threads()}
+        del outb
+
+    def parity():
+        sel = np.linspace(0, nq - 1, min(100_000, nq)).astype(np.int64)
+        src = oracle_idx if oracle_idx is not None else idx
+        img_idx = src.alt_counters()[0] if ac else src
+        want, _ = oracle.search(img_idx.image(), h["reads"][sel], nthreads=max(1, cpu_effective() // D.world))
+        if ac:
+            img_idx.close()
+        h["n_sample"] = int(sel.size)
+        return bool(np.array_equal(want.reshape(-1, 2), h["res"].reshape(-1, 2)[sel]))
+
+    ok = S.run(parity)
+    out["oracle_sample_ok_per_rank"] = D.gather(ok if S.ok else None)
+    out["oracle_sample_per_rank"] = h.get("n_sample", 0)
+    for k in ("q", "r"):
+        if k in h:
+            h[k].close()
     if ingest:
         # this rank's shard as a FASTA file -> results (host parser and device parser)
-        try:
-            ing = ingest_leg(idx, reads, res, D.world)
-        except Exception as e:          # auxiliary (e.g. TMPDIR full): report, never abort the bench
-            ing = {"error": repr(e)}
-            os.environ.pop("KFMI_LOAD_MMAP", None)
-        out["ingest_file_per_rank"] = D.gather(ing)
+        ing = S.run(ingest_leg, idx, h["reads"], h["res"], D.world) if S.ok else None
+        os.environ.pop("KFMI_LOAD_MMAP", None)
+        out["ingest_file_per_rank"] = D.gather(ing if ing is not None else {"error": S.err})
+    errs = D.gather(S.err)
+    if any(errs):
+        out["error_per_rank"] = errs
     return out
 
 
@@ -493,47 +600,63 @@ def kstep4_leg(D, text: bytes, reads: np.ndarray, res: np.ndarray, idx2, steps: 
     ranks).  The intervals do not depend on K, so every rank's results must
     equal its K = 2 results (rank 0: and the pinned md5).  Config #5's read
     shape runs on it too (150 % 4 = 2: the last two bases of each read from the
-    remainder table, then 37 K-steps), oracle-sampled against the K = 2 image."""
+    remainder table, then 37 K-steps), oracle-sampled against the K = 2 image.
+    Every rank makes the same collective calls whatever fails locally (Steps)."""
     out = {"what": "coop-grp: K=4, d=64 index (LAY_GRP lines, device_index_bytes), wave64 cooperative LF, "
                    "the main leg's reads on every rank"}
-    t = time.perf_counter()
-    i4 = K.Index.build(text, k=4, d=64, gpu=True, host_image=False)
-    build_s = time.perf_counter() - t
-    q = K.Queries.from_array(reads)
-    r = K.Results.alloc(reads.shape[0])
-    try:
+    S = Steps()
+    h = {}
+
+    def setup():
+        t = time.perf_counter()
+        h["i4"] = K.Index.build(text, k=4, d=64, gpu=True, host_image=False)
+        h["build_s"] = time.perf_counter() - t
+        h["q"] = K.Queries.from_array(reads)
+        h["r"] = K.Results.alloc(reads.shape[0])
         t = time.perf_counter()
         K.set_backend("coop-grp")
-        K.transfer_to_gpu(i4, q, r)
-        upload_s = time.perf_counter() - t
+        K.transfer_to_gpu(h["i4"], h["q"], h["r"])
+        h["upload_s"] = time.perf_counter() - t
         for _ in range(5):
-            K.search(i4, q, r)
-        D.barrier()
-        lf = []
-        t0 = time.perf_counter()
+            K.search(h["i4"], h["q"], h["r"])
+
+    def timed(lf):
         for _ in range(steps):
-            K.search(i4, q, r)
+            K.search(h["i4"], h["q"], h["r"])
             lf.append(K.last_timing()["lf_ms"])
+
+    def fetch():
+        K.transfer_to_cpu(h["r"])
+        return h["r"].array().copy()
+
+    S.run(setup)
+    got = None
+    if D.all_ok(S.ok):
+        lf = []
+        D.barrier()
+        t0 = time.perf_counter()
+        S.run(timed, lf)
         D.barrier()
         el = D.max(time.perf_counter() - t0)
-        K.transfer_to_cpu(r)
-        got = r.array().copy()
+        got = S.run(fetch)
         total = D.sum(float(reads.shape[0]))
+        lfm = float(np.mean(lf)) if lf else float("nan")
         out.update({"mqps": round(total * steps / el / 1e6, 2), "ms_per_step": round(el / steps * 1e3, 4),
-                    "lf_ms": round(float(np.mean(lf)), 3), "lf_ms_per_rank": D.gather(round(float(np.mean(lf)), 4)),
-                    "device_index_bytes": i4.device_bytes(),
-                    "build_s_max": round(D.max(build_s), 2), "upload_s_max": round(D.max(upload_s), 2),
-                    "results_equal_k2_per_rank": D.gather(bool(np.array_equal(got, res)))})
-        if pinned_md5 and D.rank == 0:
+                    "lf_ms": round(lfm, 3), "lf_ms_per_rank": D.gather(round(lfm, 4) if lf else None),
+                    "device_index_bytes": h["i4"].device_bytes(),
+                    "build_s_max": round(D.max(h["build_s"]), 2), "upload_s_max": round(D.max(h["upload_s"]), 2),
+                    "results_equal_k2_per_rank": D.gather(got is not None and bool(np.array_equal(got, res)))})
+        if pinned_md5 and D.rank == 0 and got is not None:
             out["results_md5_pinned"] = synth.results_md5(got) == pinned_md5
-        blocks = K.count_blocks(i4, q)
-        bytes_alg = blocks * (4 * 64 // 4 + 4)              # SURVEY 8(d): K*d/4 + 4 B per distinct block
-        lfm = float(np.mean(lf))
-        out["roofline"] = {"distinct_blocks": blocks, "bytes_per_block": 68, "bytes_per_launch": bytes_alg,
-                           "achieved_GBs": round(bytes_alg / (lfm / 1e3) / 1e9, 1),
-                           "frac": round(bytes_alg / (lfm / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-                           "note": "rank 0's launch"}
-        if D.world == 1:
+        blocks = S.run(K.count_blocks, h["i4"], h["q"])
+        if blocks is not None and lf:
+            bytes_alg = blocks * (4 * 64 // 4 + 4)              # SURVEY 8(d): K*d/4 + 4 B per distinct block
+            out["roofline"] = {"distinct_blocks": blocks, "bytes_per_block": 68, "bytes_per_launch": bytes_alg,
+                               "achieved_GBs": round(bytes_alg / (lfm / 1e3) / 1e9, 1),
+                               "frac": round(bytes_alg / (lfm / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                               "note": "rank 0's launch"}
+        if D.world == 1 and S.ok:
+            i4, q, r = h["i4"], h["q"], h["r"]
             # opt-in jump start (DESIGN 5a) on the K = 4 index: the first 16 bases
             # (4 K-steps, most with L and R in different blocks) from a 34 GB table
             wall, lf1, tot1 = time_backend(i4, q, r, "coop-grp+ftab16", steps, 5)
@@ -545,18 +668,22 @@ def kstep4_leg(D, text: bytes, reads: np.ndarray, res: np.ndarray, idx2, steps: 
             wall, lf1, tot1 = time_backend(i4, q, r, "task-grp", steps, 5)
             out["task-grp"] = {"mqps": round(reads.shape[0] * steps / wall / 1e6, 2), "lf_ms": round(lf1, 3),
                                "results_equal_k2": bool(np.array_equal(r.array(), res))}
-        q.close()
-        r.close()
-        q = r = None
-        if c5_queries > 0:
-            out["config5"] = config5_leg(D, i4, text, "coop-grp", c5_qlen, c5_queries, steps, 5, False,
+    for k in ("q", "r"):
+        if k in h:
+            h[k].close()
+    if c5_queries > 0:
+        if D.all_ok(S.ok):
+            out["config5"] = config5_leg(D, h["i4"], text, "coop-grp", c5_qlen, c5_queries, steps, 5, False,
                                          oracle_idx=idx2)
-    finally:
-        if q is not None:
-            q.close()
-            r.close()
-        i4.free_gpu()
-        i4.close()
+    if "i4" in h:
+        try:
+            h["i4"].free_gpu()
+            h["i4"].close()
+        except K.KfmiError as e:
+            S.err = S.err or str(e)
+    errs = D.gather(S.err)
+    if any(errs):
+        out["error_per_rank"] = errs
     return out
 
 
@@ -606,10 +733,14 @@ def time_backend(idx, q, r, backend, steps, warmup):
 def main():
     a = parse()
     D = Dist(a.gpus)
+    ph = Phases()
     K.load()
     ndev = K.device_count()
     if ndev < 1:
         raise SystemExit("bench.py: no HIP device visible")
+    # one rank per GPU: local rank r on device r.  With fewer devices than local
+    # ranks (a rehearsal on one card) ranks wrap onto shared devices -- detected
+    # below from the PCI bus ids and reported, never claimed as N GPUs
     dev = D.local % ndev
     K.set_device(dev)
     try:
@@ -618,15 +749,24 @@ def main():
             torch.cuda.set_device(dev)
     except Exception:
         pass
+    dev_rows = device_rows(D, dev)
+    dev_agg = aggregate_devices(dev_rows)
+    if dev_agg["shared_devices"] and D.rank == 0:
+        log(f"WARNING: {D.world} ranks on {dev_agg['distinct_devices']} distinct GPU(s) -- a rehearsal, "
+            "not a multi-GPU measurement (n_gpus reports distinct devices, no scaling claim)")
+    ingest_on = a.ingest == "on" or (a.ingest == "auto" and D.world <= 2)
+    ph.mark("init")
 
     # ---- inputs: reference text, index replica, this rank's reads ----------
     t = time.perf_counter()
     text = make_text(a.ref_size)
     log(f"rank {D.rank}: text {len(text)} bases in {time.perf_counter() - t:.1f}s")
+    ph.mark("text")
     t = time.perf_counter()
     idx = K.Index.build(text, k=a.k, d=a.d, gpu=True, sa_rate=a.sa_rate)
     build_s = time.perf_counter() - t
     log(f"rank {D.rank}: GPU index build {build_s:.1f}s")
+    ph.mark("index_build")
     pinned = (a.ref_size == 3_000_000_000 and a.k == 2 and a.d == 64)
     index_md5_ok = None
     if pinned and D.rank == 0 and not a.no_md5:
@@ -638,6 +778,7 @@ def main():
     reads = synth.gather_reads(text, starts, a.qlen)
     del starts
     log(f"rank {D.rank}: {reads.shape[0]} reads in {time.perf_counter() - t:.1f}s")
+    ph.mark("reads")
 
     q = K.Queries.from_array(reads)
     r = K.Results.alloc(reads.shape[0])
@@ -663,6 +804,7 @@ def main():
     cuda_sync(dev)
     D.barrier()
     elapsed = time.perf_counter() - t0
+    ph.mark("upload_warmup_timed")
     elapsed_max = D.max(elapsed)
     total_queries = D.sum(float(reads.shape[0]))
     ms_per_step = elapsed_max / a.steps * 1e3
@@ -692,6 +834,7 @@ def main():
         if ac:
             img_idx.close()
         log(f"rank {D.rank}: oracle sample {ns_par} reads parity_ok={parity_ok} ({time.perf_counter() - t:.1f}s)")
+    ph.mark("parity")
 
     # ---- roofline: algorithmic bytes of the LF kernel ------------------------
     blocks = K.count_blocks(idx, q)
@@ -707,8 +850,12 @@ def main():
     bytes_io = reads.shape[0] * (q_in + 8)
     lf_avg_ms = float(np.mean(lf_ms))
     achieved = bytes_alg / (lf_avg_ms / 1e3) / 1e9
-    # HBM bytes per launch from the committed PMC profile of the same config
-    # (scripts/traffic_from_pmc.py: TCC_EA0_RDREQ x line bytes, gfx950-corrected)
+    # fabric read requests per launch from the committed PMC profile of the same
+    # config (scripts/traffic_from_pmc.py: TCC_EA0_RDREQ, one request per random
+    # line of up to 128 B on gfx950).  These count every L2 miss, Infinity-Cache
+    # hits included (MI355X_MICROARCH.md HBM section), so requests x 128 B is an
+    # UPPER BOUND on HBM bytes, not HBM bytes: roofline.traffic stays null unless
+    # the profile carries a counter that excludes Infinity-Cache hits.
     traffic, traffic_src, rdreq = None, None, None
     tj = Path(a.traffic_json)
     if tj.exists() and D.world == 1:   # a one-GPU PMC profile says nothing about N > 1 runs
@@ -716,39 +863,37 @@ def main():
             tr = json.loads(tj.read_text())
             if (tr.get("backend") == a.backend and tr.get("queries") == a.queries and tr.get("ref_size") == a.ref_size
                     and tr.get("qlen", 100) == a.qlen and tr.get("k", 2) == a.k and tr.get("d", 64) == a.d):
-                traffic, traffic_src = tr.get("hbm_bytes_per_launch"), tr.get("source")
+                traffic, traffic_src = tr.get("hbm_bytes_per_launch_excl_infinity_cache"), tr.get("source")
                 rdreq = tr.get("rdreq_per_launch")
         except Exception:
             traffic = None
-
+    ph.mark("count_blocks")
+    # ---- auxiliary legs: each makes the same collective calls on every rank
+    # whatever fails locally (Steps), so one failing rank never hangs the rest
     c5 = None
     if a.config5_queries > 0:
-        try:
-            c5 = config5_leg(D, idx, text, a.backend, a.config5_qlen, a.config5_queries, a.steps, 5,
-                             a.backend in ("task-ac", "coop-ac", "task-ac128", "coop-ac128", "task-ac-mid",
-                                           "coop-ac-mid"), ingest=a.ingest)
-            log(f"rank {D.rank}: config #5 leg {c5}")
-        except K.KfmiError as e:
-            c5 = {"error": str(e)}
+        c5 = config5_leg(D, idx, text, a.backend, a.config5_qlen, a.config5_queries, a.steps, 5,
+                         a.backend in ("task-ac", "coop-ac", "task-ac128", "coop-ac128", "task-ac-mid",
+                                       "coop-ac-mid"), ingest=ingest_on)
+        log(f"rank {D.rank}: config #5 leg {c5}")
+        ph.mark("config5")
     ingest = None
-    if a.ingest:
-        try:
-            ingest = ingest_leg(idx, reads, res, D.world)
-            log(f"rank {D.rank}: ingest {ingest}")
-        except Exception as e:          # auxiliary leg (e.g. TMPDIR full): report, never abort the bench
-            ingest = {"error": repr(e)}
-            os.environ.pop("KFMI_LOAD_MMAP", None)
+    if ingest_on:
+        S = Steps()
+        ingest = S.run(ingest_leg, idx, reads, res, D.world) or {"error": S.err}
+        os.environ.pop("KFMI_LOAD_MMAP", None)
+        log(f"rank {D.rank}: ingest {ingest}")
+        ph.mark("ingest")
     k4 = None
     if a.kstep4 and a.k == 2 and a.d == 64:
         # ---- K = 4 on every rank's reads (LAY_GRP, coop kernel) --------------
-        try:
-            k4 = kstep4_leg(D, text, reads, res, idx, a.steps,
-                            synth.MD5["res3g.q10M"] if (pinned and a.qlen == 100 and a.queries == 10_000_000)
-                            else None, a.config5_qlen, a.config5_queries)
-            log(f"rank {D.rank}: K=4 leg {k4}")
-        except K.KfmiError as e:
-            k4 = {"error": str(e)}
-    rank_rows = D.gather({"ingest": ingest, "rank": D.rank, "device": dev, "queries": int(reads.shape[0]),
+        k4 = kstep4_leg(D, text, reads, res, idx, a.steps,
+                        synth.MD5["res3g.q10M"] if (pinned and a.qlen == 100 and a.queries == 10_000_000)
+                        else None, a.config5_qlen, a.config5_queries)
+        log(f"rank {D.rank}: K=4 leg {k4}")
+        ph.mark("kstep4")
+    rank_rows = D.gather({"ingest": ingest, "rank": D.rank, "device": dev,
+                          "pci_bus_id": dev_rows[D.rank]["pci_bus_id"], "queries": int(reads.shape[0]),
                           "lf_ms": round(float(np.mean(lf_ms)), 4), "step_ms": round(float(np.mean(tot_ms)), 4),
                           "elapsed_s": round(elapsed, 4), "distinct_blocks": int(blocks),
                           "parity_ok": parity_ok, "parity_sample": int(ns_par),
@@ -756,6 +901,7 @@ def main():
     ranks = aggregate_ranks(rank_rows)
 
     extra = {}
+    ph.mark("gather")
     probe = probe_leg() if D.world == 1 and D.rank == 0 else None
     if probe:
         extra["line_request_probe"] = probe
@@ -818,19 +964,24 @@ def main():
         # once and fanned out device-to-device; here one card listed n times ----
         try:
             K.set_backend(a.backend)
-            reps = {}
+            reps, parts = {}, {}
             for nrep in (1, 2, 4):
                 K.set_devices([dev] * nrep if nrep > 1 else [])
                 idx.free_gpu()
                 t = time.perf_counter()
                 K.transfer_to_gpu(idx, None, None)
                 reps[str(nrep)] = round(time.perf_counter() - t, 3)
+                if nrep > 1:
+                    lt = K.last_timing()
+                    parts[str(nrep)] = {"members_streams_events_ms": round(lt["pack_ms"], 2),
+                                        "fan_out_ms": round(lt["lf_ms"], 2),
+                                        "first_member_upload_ms": round(lt["total_ms"] - lt["pack_ms"] - lt["lf_ms"], 2)}
             K.set_devices([])
             idx.free_gpu()
-            extra["group_replication"] = {"setup_s_by_replicas": reps,
+            extra["group_replication"] = {"setup_s_by_replicas": reps, "breakdown_by_replicas": parts,
                                           "what": "transferCPUtoGPU(index) for a device group of n replicas "
                                                   "on this card: host upload + relayout on the first, "
-                                                  "hipMemcpyPeerAsync to the others"}
+                                                  "hipMemcpyPeerAsync to the others (kfmi_last_timing split)"}
             log(f"group replication {extra['group_replication']}")
         except Exception as e:
             K.set_devices([])
@@ -916,18 +1067,29 @@ def main():
         extra["cpu_port_1thread"] = {"value": round(n1 / (time.perf_counter() - t) / 1e6, 4),
                                      "unit": "Mqueries/s", "cores": 1, "sample": f"first {n1} reads"}
         log(f"cpu baseline {cpu}")
+    ph.mark("rank0_n1_legs_and_cpu_baseline")
+    # per-rank phase wall times and peak host RSS (the N = 8 budget: DESIGN.md 7)
+    ph_rows = D.gather({"rank": D.rank, "phases_s": ph.rows, "peak_rss_gb": Phases.peak_rss_gb()})
+    phases = {"per_rank": ph_rows,
+              "max_over_ranks_s": {k: max(r["phases_s"].get(k, 0.0) for r in ph_rows) for k in ph.rows},
+              "wall_s_max": round(max(sum(r["phases_s"].values()) for r in ph_rows), 1),
+              "peak_rss_gb_max": max(r["peak_rss_gb"] for r in ph_rows),
+              "host_threads_per_rank": K.host_threads(),
+              "ingest_legs": ingest_on}
 
     if D.rank == 0:
         line = {
             "metric": f"Mqueries/s ({a.qlen} bp reads, {a.ref_size / 1e9:g} Gbase index)",
             "value": round(value, 3),
             "unit": "Mqueries/s",
-            "n_gpus": D.world,
+            # distinct physical GPUs (PCI bus ids), not ranks: a one-card rehearsal
+            # with two ranks reports 1 and makes no scaling claim
+            "n_gpus": dev_agg["distinct_devices"],
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": None if dev_agg["shared_devices"] else "weak",
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic: seeded uniform-ACGT reference + exact-substring reads (SURVEY App. C recipe, md5-pinned)",
@@ -935,7 +1097,11 @@ def main():
                                    f"{a.ref_size / 1e9:g} Gbase index, {a.queries // 1_000_000}M x {a.qlen} bp reads per GPU",
                        "backend": a.backend, "k": a.k, "d": a.d, "ref_size": a.ref_size,
                        "queries_per_gpu": a.queries, "qlen": a.qlen,
-                       "parallelism": f"query-sharded dp{D.world}, index replicated per GPU, no collective"},
+                       "parallelism": f"query-sharded dp{D.world}, index replicated per GPU, no collective"
+                                      + (f" (REHEARSAL: {D.world} ranks on {dev_agg['distinct_devices']} GPU(s))"
+                                         if dev_agg["shared_devices"] else "")},
+            "ranks_launched": D.world,
+            "devices": dict(dev_agg, per_rank=dev_rows),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": "LF kernel (task/coop search), HIP-event average over the timed steps",
@@ -945,11 +1111,13 @@ def main():
                          "lf_ms": round(lf_avg_ms, 4), "pack_ms": round(float(np.mean(pack_ms)), 4),
                          "naive_bytes_per_launch": 2 * (a.qlen // a.k) * b_lf * a.queries,
                          "traffic_source": traffic_src,
-                         "traffic_GBs": round(traffic / (lf_avg_ms / 1e3) / 1e9, 1) if traffic else None,
-                         "traffic_frac": round(traffic / (lf_avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
                          # every LF is a random 128-B line: the binding limit is the rate of random line
-                         # requests, calibrated by gather_probe on the same 3 GB table size
-                         # (profiles/r01/gather_probe_table_size.txt, per-lane 64-B lines)
+                         # requests at the L2/fabric boundary, calibrated by gather_probe on the same 3 GB
+                         # table size.  Requests x 128 B includes Infinity-Cache hits: an upper bound on HBM
+                         # bytes, compared with the probe's request ceiling, never with the HBM peak
+                         "fabric_read_requests_per_launch": rdreq,
+                         "fabric_request_bytes_upper_bound": rdreq * 128 if rdreq else None,
+                         "line_requests_per_query": round(rdreq / a.queries, 2) if rdreq else None,
                          "line_requests_G_per_s": round(rdreq / (lf_avg_ms / 1e3) / 1e9, 2) if rdreq else None,
                          "line_request_ceiling_G_per_s": probe["best_G_lines_per_s"] if probe else PROBE_CEILING_GLINES,
                          "line_request_ceiling_source": "gather_probe on this box, this run" if probe else
@@ -963,6 +1131,7 @@ def main():
             "ranks": ranks,
             "setup_s": {"gpu_index_build": round(build_s, 2), "h2d": round(upload_s, 2), "d2h": round(d2h_s, 3)},
             "device_index_bytes": dev_index_bytes,
+            "phases": phases,
             "variants": extra,
         }
         print(json.dumps(line), flush=True)

@@ -138,6 +138,11 @@ const char *kfmi_get_backend(void);
  * Default: KFMI_DEVICE, else 0. */
 int32_t     kfmi_set_device(int32_t device);
 int32_t     kfmi_device_count(void);
+/* PCI bus id ("0000:75:00.0") of HIP device `device`, NUL-terminated in buf
+ * (len >= 13): names the physical GPU, which device numbers do not across
+ * processes with different HIP_VISIBLE_DEVICES (not in the reference, which
+ * has one compile-time DEVICE). */
+int32_t     kfmi_device_pci_bus_id(int32_t device, char *buf, int32_t len);
 /* Status of the last searchIndexGPU() on this thread. */
 int32_t     kfmi_last_error(void);
 /* searchIndexGPU with a status return. */
@@ -149,6 +154,8 @@ int32_t     kfmi_search(void *index, void *queries, void *results);
  * (default; KFMI_FTAB sets it process-wide), at most 16, a multiple of K to
  * take effect; per calling thread like the backend. */
 int32_t     kfmi_set_ftab(uint32_t bases);
+/* Every entry point leaves the caller's current HIP device as it found it
+ * (hipGetDevice before == after), whichever devices it used inside. */
 /* Device groups (runtime multi-GPU behind the same handles; the reference
  * picks one GPU at compile time with -DDEVICE, Coop-2Step.cu:256).  With two
  * or more devices listed -- here or in KFMI_DEVICES=0,1,... -- transferCPUtoGPU
@@ -243,6 +250,11 @@ int32_t kfmi_load_queries_gpu(const char *fn, uint32_t sizequery, uint64_t numqu
  * the read's bit string (fmIndexCPUBaseline.c:200-226 order; K-independent).
  * kfmi_search_stream uses it to send 4 bytes per 16 bases over PCIe. */
 int32_t kfmi_pack_queries(const char *ascii, uint64_t num, uint32_t size, uint32_t *words);
+/* Host threads of the parallel host paths (loadQueries, the streamed search's
+ * packers, the device loader's reads): KFMI_HOST_THREADS, else this process's
+ * CPUs (affinity mask capped by the cgroup quota) divided among the ranks on
+ * this host (LOCAL_WORLD_SIZE), 2 to 16. */
+int32_t kfmi_host_threads(void);
 /* Pinned (page-locked) host memory for query/result buffers. */
 int32_t kfmi_host_alloc(uint64_t bytes, void **p);
 int32_t kfmi_host_free(void *p);

@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "../kfmi_internal.h"
+#include "kfmi_devguard.h"
 
 namespace {
 
@@ -614,6 +615,7 @@ extern "C" int32_t kfmi_build_index_gpu_sa(const char* text, uint64_t n, uint32_
 {
   if (sa_rate && !kfmi_sa_rate_ok(sa_rate)) return KFMI_E_BAD_ARGUMENT;
   if (kfmi_device_count() < 1) return KFMI_E_NO_DEVICE;
+  kfmi::DeviceGuard dg;
   int32_t e = build_gpu(text, n, k, d, sa_rate, kfmi_current_device(), true, (kfmi_fmi_t**) index);
   if (e == KFMI_E_NOT_IMPLEMENTED) {
     fprintf(stderr, "kstepfmi build: text of %llu bases exceeds one dispatch per base (2^32 - 256), "
@@ -635,43 +637,48 @@ extern "C" int32_t kfmi_build_index_gpu(const char* text, uint64_t n, uint32_t k
 {
   if (want_host_image) return kfmi_build_index_gpu_sa(text, n, k, d, 0, index);
   if (kfmi_device_count() < 1) return KFMI_E_NO_DEVICE;
+  kfmi::DeviceGuard dg;
   int32_t e = build_gpu(text, n, k, d, 0, kfmi_current_device(), false, (kfmi_fmi_t**) index);
   if (e == KFMI_E_NOT_IMPLEMENTED) return kfmi_build_index_gpu_sa(text, n, k, d, 0, index);   /* host builder */
   return e;
 }
 
 /* The host image of an index whose entries are only in HBM: fetched once (one
- * D2H), then kept beside the device copy. */
+ * D2H) into a new buffer, then kept beside the device copy.  Nothing a reader
+ * may hold moves: the header-only image it replaces is retired (freed by
+ * freeIndex), and h_index is published with release order after the bytes
+ * are in place, so a thread that sees it non-null sees the whole image. */
 extern "C" int32_t kfmi_host_entries(kfmi_fmi_t* f)
 {
   if (!f) return KFMI_E_BAD_ARGUMENT;
+  if (__atomic_load_n(&f->h_index, __ATOMIC_ACQUIRE)) return KFMI_SUCCESS;
   static std::mutex mu;   /* two threads asking for the same handle's image fetch it once */
   std::lock_guard<std::mutex> lk(mu);
-  if (f->h_index) return KFMI_SUCCESS;
+  if (__atomic_load_n(&f->h_index, __ATOMIC_ACQUIRE)) return KFMI_SUCCESS;
   if (!f->d_entries) return KFMI_E_BAD_ARGUMENT;
   const uint64_t body = 4ull * f->entry_words * f->nentries;
-  uint8_t* img = (uint8_t*) realloc(f->image, f->header_bytes + body + 64);
+  uint8_t* img = (uint8_t*) malloc(f->header_bytes + body + 64);
   if (!img) return KFMI_E_ALLOCATING_FMI;
-  f->image = img;
-  int cur = 0;
-  (void) hipGetDevice(&cur);
+  memcpy(img, f->image, f->header_bytes);
+  memset(img + f->header_bytes + body, 0, 64);
+  kfmi::DeviceGuard dg;
   if (hipSetDevice(f->d_entries_dev) != hipSuccess ||
       hipMemcpy(img + f->header_bytes, f->d_entries, body, hipMemcpyDeviceToHost) != hipSuccess) {
-    (void) hipSetDevice(cur);
+    free(img);
     return KFMI_E_KERNEL;
   }
-  (void) hipSetDevice(cur);
-  f->h_index = (uint32_t*) (img + f->header_bytes);
+  free(f->image_retired);   /* never set twice: h_index is published once */
+  f->image_retired = f->image;
+  f->image = img;
+  __atomic_store_n(&f->h_index, (uint32_t*) (img + f->header_bytes), __ATOMIC_RELEASE);
   return KFMI_SUCCESS;
 }
 
 extern "C" void kfmi_free_dev_entries(kfmi_fmi_t* f)
 {
   if (!f || !f->d_entries) return;
-  int cur = 0;
-  (void) hipGetDevice(&cur);
+  kfmi::DeviceGuard dg;
   (void) hipSetDevice(f->d_entries_dev);
   (void) hipFree(f->d_entries);
-  (void) hipSetDevice(cur);
   f->d_entries = nullptr;
 }

@@ -3,6 +3,7 @@
  * several GPUs (SURVEY 8(b) device selection, 8(e) query slicing).
  */
 #include <stdlib.h>
+#include <chrono>
 #include <new>
 #include <thread>
 #include <vector>
@@ -201,6 +202,10 @@ int32_t group_transfer(kfmi_fmi_t* f, kfmi_qrys_t* q, kfmi_res_t* r, const int* 
     bool same = g && g->backend == backend && g->n == n;
     for (int i = 0; same && i < n; ++i) same = g->dev[i] == devs[i];
     if (!same) {
+      using clk = std::chrono::steady_clock;
+      auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
+      const auto t0 = clk::now();
+      double setup_ms = 0;
       group_free_index(f);
       g = new (std::nothrow) GroupIndex();
       if (!g) return KFMI_E_ALLOCATING_FMI;
@@ -214,12 +219,15 @@ int32_t group_transfer(kfmi_fmi_t* f, kfmi_qrys_t* q, kfmi_res_t* r, const int* 
       for (int i = 0; i < n && !err; ++i) {
         g->dev[i] = devs[i];
         DevCtx* ctx = nullptr;
+        const auto ts = clk::now();
         err = ctx_for(devs[i], &ctx);
         if (!err && hipStreamCreateWithFlags(&g->st[i], hipStreamNonBlocking) != hipSuccess) err = KFMI_E_NO_DEVICE;
         for (int k = 0; k < 3 && !err; ++k)
           if (hipEventCreate(&g->ev[i][k]) != hipSuccess) err = KFMI_E_NO_DEVICE;
+        setup_ms += ms_since(ts);
         if (!err && i == 0) err = upload_index(f, backend, devs[0], ctx, &g->di[0]);
       }
+      const auto tf = clk::now();
       for (int i = 1; i < n && !err; ++i) {
         int can = 0;
         (void) hipSetDevice(devs[i]);
@@ -237,6 +245,12 @@ int32_t group_transfer(kfmi_fmi_t* f, kfmi_qrys_t* q, kfmi_res_t* r, const int* 
         group_free_index(f);
         return err;
       }
+      /* kfmi_last_timing after a group upload: total = the index setup, pack =
+       * the members' stream + event creation, lf = the replica fan-out
+       * (allocations + device-to-device copies of members 1..n-1) */
+      t_ms[0] = ms_since(t0);
+      t_ms[1] = setup_ms;
+      t_ms[2] = ms_since(tf);
     }
     if (f->dev) {   /* one mode per handle: the single-device copy goes */
       free_dev_index(f->dev);

@@ -176,6 +176,7 @@ extern "C" int32_t kfmi_load_queries_gpu(const char* fn, uint32_t sizequery, uin
   if (!fn || !queries || sizequery == 0) return KFMI_E_BAD_ARGUMENT;
   if (64ull * sizequery + 16 > 160ull * 1024) return KFMI_E_BAD_ARGUMENT;   /* as upload_queries */
   *queries = nullptr;
+  DeviceGuard dg;
   const int dev = kfmi_current_device();
   DevCtx* ctx = nullptr;
   int32_t err = ctx_for(dev, &ctx);
@@ -241,7 +242,7 @@ extern "C" int32_t kfmi_load_queries_gpu(const char* fn, uint32_t sizequery, uin
     ok = ok && hipGetLastError() == hipSuccess;
     const uint64_t words = (abytes + 3) / 4;
     const uint64_t rb = (words + 255) / 256;
-    hipLaunchKernelGGL(fa_rows, dim3((uint32_t) (rb < (1u << 22) ? rb : (1u << 22))), dim3(256), 0, st, raw.as<uint8_t>(), n,
+    hipLaunchKernelGGL(fa_rows, dim3(grid_blocks(rb, 1u << 22)), dim3(256), 0, st, raw.as<uint8_t>(), n,
                        starts.as<uint64_t>(), num, sizequery, reinterpret_cast<uint32_t*>(dq->ascii),
                        bad.as<unsigned long long>());
     ok = ok && hipGetLastError() == hipSuccess &&

@@ -12,6 +12,7 @@
 #include <stdlib.h>
 
 #include "kfmi_device.h"
+#include "kfmi_grid.h"
 #include "kfmi_coop.h"
 #include "kfmi_locate.h"
 
@@ -436,15 +437,14 @@ static hipError_t launch_locate(const SearchLaunch& a)
     if (!e || atoi(e)) {
       /* 32 KB of LDS per workgroup: 5 fit a CU (4 measured the same within 2 %,
        * profiles/r02/locate_r2ba.jsonl: the walk is not short of lines in flight) */
-      if (blocks > (uint64_t) cus * 5) blocks = (uint64_t) cus * 5;
-      hipLaunchKernelGGL((locate_coop_kernel<G>), dim3((uint32_t) blocks), dim3(256), 0, a.st, a.ix, a.sa, a.sa_log2,
+      hipLaunchKernelGGL((locate_coop_kernel<G>), dim3(grid_blocks(blocks, (uint64_t) cus * 5)), dim3(256), 0, a.st, a.ix,
+                         a.sa, a.sa_log2,
                          a.owner, a.total, a.pos, a.slot_ctr);
       return hipGetLastError();
     }
   }
-  if (blocks > (uint64_t) cus * 8) blocks = (uint64_t) cus * 8;
-  hipLaunchKernelGGL((locate_kernel<G>), dim3((uint32_t) blocks), dim3(256), 0, a.st, a.ix, a.sa, a.sa_log2, a.owner,
-                     a.total, a.pos);
+  hipLaunchKernelGGL((locate_kernel<G>), dim3(grid_blocks(blocks, (uint64_t) cus * 8)), dim3(256), 0, a.st, a.ix, a.sa,
+                     a.sa_log2, a.owner, a.total, a.pos);
   return hipGetLastError();
 }
 
@@ -452,7 +452,7 @@ template <class G>
 static hipError_t launch_ftab(const SearchLaunch& a)
 {
   const uint64_t blocks = (a.ftab_n + 255) / 256;
-  hipLaunchKernelGGL((ftab_build_kernel<G>), dim3((uint32_t) (blocks < (1u << 20) ? blocks : (1u << 20))), dim3(256), 0,
+  hipLaunchKernelGGL((ftab_build_kernel<G>), dim3(grid_blocks(blocks, 1u << 20)), dim3(256), 0,
                      a.st, a.ix, a.ftab_steps, a.ftab_n, a.ftab_out);
   return hipGetLastError();
 }

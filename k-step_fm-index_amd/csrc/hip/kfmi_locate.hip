@@ -69,7 +69,7 @@ static __global__ __launch_bounds__(256) void loc_rows_kernel(const uint32_t* __
 extern "C" int32_t kfmi_locations_free(void** locations)
 {
   kfmi_locations* L = locations ? (kfmi_locations*) *locations : nullptr;
-  if (L) {
+  if (L) {   /* host memory only */
     free(L->h_off);
     free(L->h_pos);
     delete L;
@@ -164,7 +164,7 @@ static int32_t locate_on(kfmi_fmi_t* f, kfmi_dev_index* di, uint32_t* d_res, uin
             hipSuccess)
       return done(KFMI_E_KERNEL);
     const uint64_t rb = (total + 255) / 256;
-    hipLaunchKernelGGL(loc_rows_kernel, dim3((uint32_t) (rb < (1u << 20) ? rb : (1u << 20))), dim3(256), 0, st,
+    hipLaunchKernelGGL(loc_rows_kernel, dim3(grid_blocks(rb, 1u << 20)), dim3(256), 0, st,
                        d_res, d_off, total, d_own);   /* owner -> first row of each slot, in place */
     if (hipGetLastError() != hipSuccess) return done(KFMI_E_KERNEL);
   }
@@ -211,6 +211,23 @@ extern "C" int32_t kfmi_locate(void* index, void* results, uint32_t max_occ, voi
   *locations = nullptr;
   if (!f || !r) return KFMI_E_BAD_ARGUMENT;
   if (!f->h_sa || !f->sa_rate) return KFMI_E_BAD_ARGUMENT;   /* index built without SA samples */
+  DeviceGuard dg;
+  /* the handle's lock shared; exclusive when a device copy still needs this
+   * index's samples (locate_on uploads them into the copy) */
+  std::shared_mutex& mu = index_lock(f);
+  std::shared_lock<std::shared_mutex> sl(mu);
+  std::unique_lock<std::shared_mutex> ul;
+  auto stale = [&] {
+    const GroupIndex* g = (const GroupIndex*) f->grp;
+    if (!g) return f->dev && (!f->dev->sa || f->dev->sa_gen != f->sa_gen);
+    for (int i = 0; i < g->n; ++i)
+      if (!g->di[i]->sa || g->di[i]->sa_gen != f->sa_gen) return true;
+    return false;
+  };
+  if (stale()) {
+    sl.unlock();
+    ul = std::unique_lock<std::shared_mutex>(mu);
+  }
   if (!f->grp && !r->grp) {
     if (!f->dev || !r->d_results) return KFMI_E_NOT_ON_DEVICE;
     if (r->d_device != f->dev->device) return KFMI_E_BAD_ARGUMENT;

@@ -11,8 +11,10 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <mutex>
+#include <shared_mutex>
 
 #include "../kfmi_internal.h"
+#include "kfmi_devguard.h"
 #include "kfmi_kernels.h"
 
 #define HIP_OK(x)                                                                   \
@@ -72,6 +74,14 @@ struct kfmi_dev_queries {
 
 namespace kfmi {
 
+/* Guards the device copies of one index handle (f->dev, f->grp): searches,
+ * locates, block counts and streamed searches hold it shared for as long as
+ * they use the device copy; an upload that replaces it (another backend or
+ * device, a new device group) or freeIndexGPU holds it exclusively, so a
+ * search running on another thread never sees its tables freed.  Striped by
+ * handle address. */
+std::shared_mutex& index_lock(const void* f);
+
 /* One non-blocking stream per device, shared by the threads that use it (their
  * work is serialised on it).  Timing events are per calling thread. */
 struct DevCtx {
@@ -98,6 +108,10 @@ hipError_t dispatch(Op op, uint32_t K, uint32_t nb, int lay, const SearchLaunch&
                     unsigned long long* d_total = nullptr);
 IdxArgs idx_args(const kfmi_dev_index* di);
 int32_t use_ftab(kfmi_dev_index* di, hipStream_t st, IdxArgs& ix, uint32_t bases);
+/* reads with m % K = rem != 0: layouts that take the remainder
+ * table, and the table of an index (built on first use; clears the ftab) */
+bool rem_supported(int layout);
+int32_t use_rtab(kfmi_dev_index* di, hipStream_t st, IdxArgs& ix, uint32_t rem);
 hipError_t launch_pack(const kfmi_dev_queries* dq, hipStream_t st);
 
 /* uploads (kfmi_search.hip) */

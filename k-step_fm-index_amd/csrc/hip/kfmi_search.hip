@@ -121,6 +121,26 @@ extern "C" int32_t kfmi_set_device(int32_t device)
   return KFMI_SUCCESS;
 }
 
+/* The physical GPU behind a device number: HIP_VISIBLE_DEVICES renumbers the
+ * devices per process, the PCI bus id does not (bench.py's ranks compare it). */
+extern "C" int32_t kfmi_device_pci_bus_id(int32_t device, char* buf, int32_t len)
+{
+  if (!buf || len < 13) return KFMI_E_BAD_ARGUMENT;
+  if (device < 0 || device >= kfmi_device_count()) return KFMI_E_NO_DEVICE;
+  if (hipDeviceGetPCIBusId(buf, len, device) != hipSuccess) {
+    (void) hipGetLastError();
+    return KFMI_E_NO_DEVICE;
+  }
+  return KFMI_SUCCESS;
+}
+
+std::shared_mutex& index_lock(const void* f)
+{
+  static std::shared_mutex stripes[64];
+  const uintptr_t h = (uintptr_t) f;
+  return stripes[(h >> 6 ^ h >> 12) & 63];
+}
+
 extern "C" void kfmi_set_last_error(int32_t e) { t_last_error = e; }
 
 extern "C" int32_t kfmi_set_ftab(uint32_t bases)
@@ -538,6 +558,13 @@ bool is_coop(int backend)
 /* host helpers for the device layouts                                      */
 /* ------------------------------------------------------------------------ */
 
+/* The host entries, or null while they live only in HBM; acquire pairs with
+ * the release in kfmi_host_entries (another thread may be fetching them). */
+static inline const uint32_t* host_index(const kfmi_fmi_t* f)
+{
+  return __atomic_load_n(&f->h_index, __ATOMIC_ACQUIRE);
+}
+
 /* Counters at row n+1 (one past the last row) from a tag-100/101 index:
  * cnt_{E-1} + rows of each code in the last block, $ rows excluded.  Used for
  * the padding entry that keeps R/d == nentries in bounds when (n+1) % d == 0
@@ -548,15 +575,15 @@ static bool end_counters(const kfmi_fmi_t* f, uint32_t* out)
   const uint32_t last = f->nentries - 1;
   std::vector<uint32_t> dev_last;
   const uint32_t* e;
-  if (f->h_index) {
-    e = f->h_index + (uint64_t) last * f->entry_words;
+  if (const uint32_t* hi = host_index(f)) {
+    e = hi + (uint64_t) last * f->entry_words;
   } else {   /* entries only in HBM: fetch the last one */
     dev_last.assign(f->entry_words, 0u);
-    int cur = 0;
-    if (hipGetDevice(&cur) != hipSuccess || hipSetDevice(f->d_entries_dev) != hipSuccess) return false;
+    DeviceGuard dg;
+    if (hipSetDevice(f->d_entries_dev) != hipSuccess) return false;
     const hipError_t ce = hipMemcpy(dev_last.data(), f->d_entries + (uint64_t) last * f->entry_words,
                                     4ull * f->entry_words, hipMemcpyDeviceToHost);
-    if (hipSetDevice(cur) != hipSuccess || ce != hipSuccess) return false;
+    if (ce != hipSuccess) return false;
     e = dev_last.data();
   }
   const uint32_t o = f->bwtsize - last * f->chunk;  /* rows of the last block, in (0, d] */
@@ -729,7 +756,7 @@ __global__ __launch_bounds__(256) void interleave_entries_kernel(uint32_t* __res
  * or device to device when they only live in HBM (built there). */
 static hipError_t entries_in(void* dst, const kfmi_fmi_t* src, uint64_t body, hipStream_t st)
 {
-  if (src->h_index) return h2d(dst, src->h_index, body, st);
+  if (const uint32_t* hi = host_index(src)) return h2d(dst, hi, body, st);
   if (!src->d_entries) return hipErrorInvalidValue;
   int cur = 0;
   hipError_t e = hipGetDevice(&cur);
@@ -753,7 +780,7 @@ static hipError_t upload_entries(void* dst, const kfmi_fmi_t* src, uint64_t body
   hipError_t e = entries_in(dst, src, body, st);
   const uint64_t nent = body / (4ull * ew), nbatch = (nent + IL_LDS_WORDS / ew - 1) / (IL_LDS_WORDS / ew);
   if (e == hipSuccess && nent) {
-    hipLaunchKernelGGL(interleave_entries_kernel, dim3((uint32_t) (nbatch < (1u << 16) ? nbatch : (1u << 16))),
+    hipLaunchKernelGGL(interleave_entries_kernel, dim3(grid_blocks(nbatch, 1u << 16)),
                        dim3(256), 0, st, (uint32_t*) dst, nent, ew, perm);
     e = hipGetLastError();
   }
@@ -846,7 +873,7 @@ int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx, kfmi_dev_
     if (!end_counters(src, pad.data() + 2 * f->nbitmaps * f->steps)) return fail(KFMI_E_KERNEL);
     /* entries that already live on this device (built here, no host image) are
      * read in place; otherwise one staging copy as stored (no interleave pass) */
-    const bool in_place = !src->h_index && src->d_entries && src->d_entries_dev == dev;
+    const bool in_place = !host_index(src) && src->d_entries && src->d_entries_dev == dev;
     uint32_t *tmp = nullptr, *d_pad = nullptr;
     di->ent_bytes = 4ull * lw * nlines;
     if ((!in_place && hipMalloc((void**) &tmp, body + 16) != hipSuccess) ||
@@ -1029,12 +1056,12 @@ IdxArgs idx_args(const kfmi_dev_index* di)
  * AltCounters-semantics backends keep rejecting such reads (their intervals
  * differ from the true ones where the reference's sentinel counts, and the
  * reference defines no result here).  The ftab is not combined with it. */
-static bool rem_supported(int layout)
+bool rem_supported(int layout)
 {
   return layout == LAY_INTER || layout == LAY_PACKED || layout == LAY_MID || layout == LAY_GRP;
 }
 
-static int32_t use_rtab(kfmi_dev_index* di, hipStream_t st, IdxArgs& ix, uint32_t rem)
+int32_t use_rtab(kfmi_dev_index* di, hipStream_t st, IdxArgs& ix, uint32_t rem)
 {
   ix.rtab = nullptr;
   ix.rem = 0;
@@ -1180,10 +1207,14 @@ extern "C" int32_t transferCPUtoGPU(void* index, void* queries, void* results)
   kfmi_fmi_t* f = (kfmi_fmi_t*) index;
   kfmi_qrys_t* q = (kfmi_qrys_t*) queries;
   kfmi_res_t* r = (kfmi_res_t*) results;
+  DeviceGuard dg;
   int devs[KFMI_MAX_GROUP];
   const int ng = group_devices(devs);
-  if (ng > 1) return group_transfer(f, q, r, devs, ng);
-  if (f) group_free_index(f);   /* one mode per handle */
+  if (ng > 1) {
+    std::unique_lock<std::shared_mutex> lk;
+    if (f) lk = std::unique_lock<std::shared_mutex>(index_lock(f));
+    return group_transfer(f, q, r, devs, ng);
+  }
   if (q) group_free_queries(q);
   if (r) group_free_results(r);
   const int dev = kfmi_current_device();
@@ -1191,9 +1222,24 @@ extern "C" int32_t transferCPUtoGPU(void* index, void* queries, void* results)
   int32_t err = ctx_for(dev, &ctx);
   if (err) return err;
   const int backend = f ? backend_for(f->steps) : kfmi_backend();
-  if (f && (!f->dev || f->dev->backend != backend || f->dev->device != dev)) {
-    err = upload_index(f, backend, dev, ctx);
-    if (err) return err;
+  if (f) {
+    /* the index's device copy is replaced only under the handle's exclusive
+     * lock (searches on other threads hold it shared); when it already fits,
+     * nothing waits */
+    auto fits = [&] { return !f->grp && f->dev && f->dev->backend == backend && f->dev->device == dev; };
+    bool ok;
+    {
+      std::shared_lock<std::shared_mutex> sl(index_lock(f));
+      ok = fits();
+    }
+    if (!ok) {
+      std::unique_lock<std::shared_mutex> ul(index_lock(f));
+      if (!fits()) {
+        group_free_index(f);   /* one mode per handle */
+        err = upload_index(f, backend, dev, ctx);
+        if (err) return err;
+      }
+    }
   }
   if (q) {
     if (!f) return KFMI_E_BAD_ARGUMENT;
@@ -1329,6 +1375,8 @@ extern "C" int32_t kfmi_search(void* index, void* queries, void* results)
   kfmi_res_t* r = (kfmi_res_t*) results;
   if (!f || !q || !r) return KFMI_E_BAD_ARGUMENT;
   if (q->num != r->num) return KFMI_E_BAD_ARGUMENT;
+  DeviceGuard dg;
+  std::shared_lock<std::shared_mutex> lk(index_lock(f));
   if (f->grp || q->grp || r->grp) return group_search(f, q, r);
   if (!f->dev || !q->dev || !r->d_results) return KFMI_E_NOT_ON_DEVICE;
   kfmi_dev_index* di = f->dev;
@@ -1362,6 +1410,8 @@ extern "C" int32_t kfmi_count_blocks(void* index, void* queries, uint64_t* block
   kfmi_fmi_t* f = (kfmi_fmi_t*) index;
   kfmi_qrys_t* q = (kfmi_qrys_t*) queries;
   if (!f || !q || !blocks) return KFMI_E_BAD_ARGUMENT;
+  DeviceGuard dg;
+  std::shared_lock<std::shared_mutex> lk(index_lock(f));
   if (f->grp || q->grp) {
     GroupIndex* gi = (GroupIndex*) f->grp;
     GroupSlices* gq = (GroupSlices*) q->grp;
@@ -1418,6 +1468,7 @@ static int32_t count_on(kfmi_dev_index* di, kfmi_dev_queries* dq, uint64_t* bloc
 extern "C" int32_t transferGPUtoCPU(void* results)
 {
   kfmi_res_t* r = (kfmi_res_t*) results;
+  DeviceGuard dg;
   if (r && r->grp) return group_to_host(r);
   if (!r || !r->d_results) return KFMI_E_NOT_ON_DEVICE;
   DevCtx* ctx = nullptr;
@@ -1432,8 +1483,11 @@ extern "C" int32_t transferGPUtoCPU(void* results)
 extern "C" int32_t freeIndexGPU(void** index)
 {
   kfmi_fmi_t* f = index ? (kfmi_fmi_t*) *index : nullptr;
-  if (f) group_free_index(f);
-  if (f && f->dev) {
+  if (!f) return KFMI_SUCCESS;
+  DeviceGuard dg;
+  std::unique_lock<std::shared_mutex> lk(index_lock(f));
+  group_free_index(f);
+  if (f->dev) {
     free_dev_index(f->dev);
     f->dev = nullptr;
   }
@@ -1442,6 +1496,7 @@ extern "C" int32_t freeIndexGPU(void** index)
 
 extern "C" int32_t freeQueriesGPU(void** queries)
 {
+  DeviceGuard dg;
   kfmi_qrys_t* q = queries ? (kfmi_qrys_t*) *queries : nullptr;
   if (q) group_free_queries(q);
   if (q && q->dev) {
@@ -1453,6 +1508,7 @@ extern "C" int32_t freeQueriesGPU(void** queries)
 
 extern "C" int32_t freeResultsGPU(void** results)
 {
+  DeviceGuard dg;
   kfmi_res_t* r = results ? (kfmi_res_t*) *results : nullptr;
   if (r) group_free_results(r);
   if (r && r->d_results) {
@@ -1466,7 +1522,9 @@ extern "C" int32_t freeResultsGPU(void** results)
 extern "C" uint64_t kfmi_device_index_bytes(void* index)
 {
   kfmi_fmi_t* f = (kfmi_fmi_t*) index;
-  if (f && f->grp) {   /* all replicas of a device group */
+  if (!f) return 0;
+  std::shared_lock<std::shared_mutex> lk(index_lock(f));
+  if (f->grp) {   /* all replicas of a device group */
     const GroupIndex* g = (const GroupIndex*) f->grp;
     uint64_t b = 0;
     for (int i = 0; i < g->n; ++i) b += g->di[i]->ent_bytes + g->di[i]->sb_bytes + g->di[i]->sa_bytes;

@@ -61,15 +61,18 @@ struct StreamPool {
    * copy also count time queued behind other slots' copies). */
   double r_pack = 0, r_stage = 0, r_xa = 0, r_xp = 0;
 };
-static StreamPool g_pool[64];
+/* One pool per (device, group member): a single-device search uses member 0;
+ * the members of a device group stream from pools of their own, so two
+ * replicas listed on one GPU overlap like replicas on two GPUs do. */
+static StreamPool g_pool[64][KFMI_MAX_GROUP];
 static thread_local double t_stream_packed_frac = 0;   /* share of the last streamed batch packed on the host */
-/* one streamed search per device at a time; searches on different devices (one
- * host thread each) and every other entry point run concurrently with it */
-static std::mutex g_pool_mu[64];
+/* one streamed search per pool at a time; searches on other pools (one host
+ * thread each) and every other entry point run concurrently with it */
+static std::mutex g_pool_mu[64][KFMI_MAX_GROUP];
 
-static void pool_free(int dev)
+static void pool_free(int dev, int member)
 {
-  StreamPool& p = g_pool[dev];
+  StreamPool& p = g_pool[dev][member];
   if (!p.init) return;
   (void) hipSetDevice(dev);
   for (StreamSlot& s : p.slot) {
@@ -143,7 +146,8 @@ bool host_pinned(const void* p)
 
 /* Persistent host workers for the streamed search (a chunk every few hundred
  * microseconds: spawning threads per chunk would cost as much as the work).
- * KFMI_HOST_THREADS (default min(16, cores)) threads including the caller. */
+ * kfmi_host_threads() threads including the caller (KFMI_HOST_THREADS, else
+ * the process's CPU share split among this host's ranks, common.c). */
 class HostPool {
  public:
   static HostPool& get()
@@ -179,10 +183,7 @@ class HostPool {
  private:
   HostPool()
   {
-    const char* e = getenv("KFMI_HOST_THREADS");
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    int v = e ? atoi(e) : (int) std::min(16u, hw);
-    v = std::max(1, std::min(v, 64));
+    const int v = kfmi_host_threads();
     for (int i = 0; i + 1 < v; ++i) th_.emplace_back([this] { loop(); });
   }
   ~HostPool()
@@ -271,13 +272,13 @@ bool par_pread(int fd, void* dst, uint64_t off, uint64_t bytes)
 }
 
 /* ASCII rows -> word-major code words of one chunk, over the host workers */
-static void par_pack(const char* src, uint64_t n, uint32_t size, uint32_t* out)
+static void par_pack(const char* src, uint64_t n, uint32_t size, uint32_t rem, uint32_t* out)
 {
   HostPool& hp = HostPool::get();
   const int parts = n < 4096 ? 1 : hp.size();
   hp.run(parts, [&](int t) {
     const uint64_t r0 = n * t / parts, r1 = n * (t + 1) / parts;
-    kfmi_pack_rows((const uint8_t*) src + r0 * size, r1 - r0, size, out + r0, n);
+    kfmi_pack_rows_rem((const uint8_t*) src + r0 * size, r1 - r0, size, rem, out + r0, n);
   });
 }
 
@@ -287,6 +288,7 @@ extern "C" int32_t kfmi_host_alloc(uint64_t bytes, void** p)
 {
   if (!p) return KFMI_E_BAD_ARGUMENT;
   *p = nullptr;
+  DeviceGuard dg;
   if (hipSetDevice(kfmi_current_device()) != hipSuccess) return KFMI_E_NO_DEVICE;
   if (hipHostMalloc(p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return KFMI_E_ALLOCATING_MFASTA;
   return KFMI_SUCCESS;
@@ -302,18 +304,20 @@ extern "C" int32_t kfmi_host_free(void* p)
  * pools belong to the devices the searched indexes live on). */
 extern "C" int32_t kfmi_stream_release(void)
 {
-  for (int dev = 0; dev < 64; ++dev) {
-    std::lock_guard<std::mutex> lk(g_pool_mu[dev]);
-    pool_free(dev);
-  }
+  DeviceGuard dg;
+  for (int dev = 0; dev < 64; ++dev)
+    for (int m = 0; m < KFMI_MAX_GROUP; ++m) {
+      std::lock_guard<std::mutex> lk(g_pool_mu[dev][m]);
+      pool_free(dev, m);
+    }
   return KFMI_SUCCESS;
 }
 
 /* One device's streamed search of `num` reads (the whole batch, or one member's
  * slice of a device group).  ms3 = {wall, host packing/staging, blocked on
  * the GPU}; *npacked = reads sent as host-packed words. */
-static int32_t stream_on(kfmi_dev_index* di, const char* ascii, uint64_t num, uint32_t size, uint32_t* results,
-                         uint64_t chunk, uint32_t ftab, double* ms3, uint64_t* npacked_out)
+static int32_t stream_on(kfmi_dev_index* di, int member, const char* ascii, uint64_t num, uint32_t size,
+                         uint32_t* results, uint64_t chunk, uint32_t ftab, double* ms3, uint64_t* npacked_out)
 {
   const uint32_t K = di->K;
   DevCtx* ctx = nullptr;
@@ -344,21 +348,27 @@ static int32_t stream_on(kfmi_dev_index* di, const char* ascii, uint64_t num, ui
   }
   if (chunk == 0) chunk = def_chunk;
   if (chunk > num) chunk = num;
-  const uint32_t steps = size / K, spw = 32 / (2 * K), nwords = (steps + spw - 1) / spw;
+  /* reads with m % K = rem != 0: K-steps over bases 0 .. m-rem-1, the last rem
+   * bases from the remainder table; code-word row nwords holds their codes
+   * (written by the host packer or by the pack kernel, read by the fused ones
+   * from the ASCII) -- the layout kfmi_search uses */
+  const uint32_t rem = size % K;
+  const uint32_t steps = (size - rem) / K, spw = 32 / (2 * K), nwords = (steps + spw - 1) / spw;
+  const uint32_t rows = nwords + (rem ? 1u : 0u);   /* code-word rows per read */
   const bool pin_in = host_pinned(ascii), pin_out = host_pinned(results);
 
-  std::lock_guard<std::mutex> lk(g_pool_mu[di->device]);
-  StreamPool& pool = g_pool[di->device];
+  std::lock_guard<std::mutex> lk(g_pool_mu[di->device][member]);
+  StreamPool& pool = g_pool[di->device][member];
   pool.init = true;
   const int nslot = stream_slots();
   for (int k = 0; k < nslot; ++k) {
     StreamSlot& s = pool.slot[k];
-    err = slot_reserve(s, chunk, size, nwords, !pin_in && any_ascii, !pin_out, any_pack);
+    err = slot_reserve(s, chunk, size, rows, !pin_in && any_ascii, !pin_out, any_pack);
     if (err) return err;
     s.busy = false;
   }
   /* cost model: pool.r_* per byte (see StreamPool) -> ms per read */
-  const double abytes = (double) size, pbytes = 4.0 * nwords;
+  const double abytes = (double) size, pbytes = 4.0 * rows;
   uint64_t npacked = 0;
   double t_host = 0, t_link = 0;                      /* model clocks of this call */
   auto ema = [](double& v, double x) { v = v > 0 ? 0.6 * v + 0.4 * x : x; };
@@ -367,6 +377,7 @@ static int32_t stream_on(kfmi_dev_index* di, const char* ascii, uint64_t num, ui
   const Op op = is_coop(di->backend) ? Op::Coop : Op::Task;
   IdxArgs ix = idx_args(di);
   err = use_ftab(di, ctx->st, ix, ftab);   /* the caller's setting (member threads have their own) */
+  if (!err) err = use_rtab(di, ctx->st, ix, rem);   /* rem != 0: the table, no ftab (as kfmi_search) */
   if (err) return err;
   int32_t status = KFMI_SUCCESS;
   using clk = std::chrono::steady_clock;
@@ -415,7 +426,7 @@ static int32_t stream_on(kfmi_dev_index* di, const char* ascii, uint64_t num, ui
     s.packed_mode = host_pack;
     npacked += host_pack ? s.n : 0;
     const auto th = clk::now();
-    if (host_pack) par_pack(src, s.n, size, s.h_pk);
+    if (host_pack) par_pack(src, s.n, size, rem, s.h_pk);
     else if (!pin_in) {
       par_copy(s.h_in, src, bytes);
       hsrc = s.h_in;
@@ -429,6 +440,8 @@ static int32_t stream_on(kfmi_dev_index* di, const char* ascii, uint64_t num, ui
     s.dq.K = K;
     s.dq.steps = steps;
     s.dq.nwords = nwords;
+    s.dq.rem = rem;
+    s.dq.packed_rows = rows;
     SearchLaunch a;
     a.st = s.st;
     a.ix = ix;
@@ -442,7 +455,7 @@ static int32_t stream_on(kfmi_dev_index* di, const char* ascii, uint64_t num, ui
     a.res = s.d_res;
     void* hdst = pin_out ? (void*) (results + 2 * s.q0) : (void*) s.h_out;
     const bool up_ok = hipEventRecord(s.x0, s.st) == hipSuccess &&
-                       (host_pack ? hipMemcpyAsync(s.dq.packed, s.h_pk, 4ull * nwords * s.n, hipMemcpyHostToDevice,
+                       (host_pack ? hipMemcpyAsync(s.dq.packed, s.h_pk, 4ull * rows * s.n, hipMemcpyHostToDevice,
                                                    s.st) == hipSuccess
                                   : hipMemcpyAsync(s.dq.ascii, hsrc, bytes, hipMemcpyHostToDevice, s.st) == hipSuccess) &&
                        hipEventRecord(s.x1, s.st) == hipSuccess &&
@@ -474,16 +487,22 @@ extern "C" int32_t kfmi_search_stream(void* index, const char* ascii, uint64_t n
 {
   kfmi_fmi_t* f = (kfmi_fmi_t*) index;
   if (!f || (!ascii && num) || (!results && num)) return KFMI_E_BAD_ARGUMENT;
+  DeviceGuard dg;
+  std::shared_lock<std::shared_mutex> lk(index_lock(f));
   GroupIndex* g = (GroupIndex*) f->grp;
   if (!g && !f->dev) return KFMI_E_NOT_ON_DEVICE;
-  const uint32_t K = g ? g->di[0]->K : f->dev->K;
-  if (size == 0 || size % K || 64ull * size + 16 > 160ull * 1024) return KFMI_E_BAD_ARGUMENT;
+  const kfmi_dev_index* d0 = g ? g->di[0] : f->dev;
+  const uint32_t K = d0->K;
+  /* m % K != 0 takes the remainder table, like kfmi_search: not on the
+   * AltCounters layouts (their semantics differ there) */
+  if (size == 0 || 64ull * size + 16 > 160ull * 1024) return KFMI_E_BAD_ARGUMENT;
+  if (size % K && !rem_supported(d0->layout)) return KFMI_E_BAD_ARGUMENT;
   double ms[KFMI_MAX_GROUP][3] = {};
   uint64_t np[KFMI_MAX_GROUP] = {};
   int32_t err = KFMI_SUCCESS;
   const uint32_t ftab = ftab_bases();
   if (!g) {
-    err = stream_on(f->dev, ascii, num, size, results, chunk, ftab, ms[0], &np[0]);
+    err = stream_on(f->dev, 0, ascii, num, size, results, chunk, ftab, ms[0], &np[0]);
   } else {
     const int n = g->n;
     uint64_t per = (num + n - 1) / n;
@@ -494,7 +513,7 @@ extern "C" int32_t kfmi_search_stream(void* index, const char* ascii, uint64_t n
     for (int i = 0; i < n; ++i) {
       const uint64_t a = per * i < num ? per * i : num, b = per * (i + 1) < num ? per * (i + 1) : num;
       th.emplace_back([&, i, a, b] {
-        errs[i] = stream_on(g->di[i], ascii + a * size, b - a, size, results + 2 * a, chunk, ftab, ms[i], &np[i]);
+        errs[i] = stream_on(g->di[i], i, ascii + a * size, b - a, size, results + 2 * a, chunk, ftab, ms[i], &np[i]);
       });
     }
     for (auto& t : th) t.join();

@@ -9,6 +9,7 @@
  */
 #define _GNU_SOURCE
 #include <pthread.h>
+#include <sched.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -124,7 +125,7 @@ int32_t freeReference(void **reference, void **index)
  *
  * The reference reads line by line with fgets on one thread into 32-bit
  * offsets (common.c:132-199, :163, :167).  Here a regular file is mapped and
- * parsed by KFMI_HOST_THREADS threads (default min(16, cores)) in two passes
+ * parsed by kfmi_host_threads() threads (KFMI_HOST_THREADS) in two passes
  * over contiguous byte ranges: count the read lines of each range (and note the
  * first malformed one), then -- after a prefix sum gives every range its first
  * read number -- copy each read to q * size.  Same semantics as the
@@ -198,13 +199,40 @@ static void *lq_worker(void *arg)
   return NULL;
 }
 
-static int host_threads(void)
+/* Host threads of the parallel paths (this loader, the streamed search's
+ * packers and staging copies, the device loader's reads): KFMI_HOST_THREADS,
+ * else the CPUs this process may use -- its affinity mask capped by the cgroup
+ * CPU quota (the GPU boxes show 256 cores but grant 16) -- divided among the
+ * ranks torchrun started on this host (LOCAL_WORLD_SIZE), 2 to 16.  Eight
+ * ranks of 16 threads each on a 16-CPU quota would oversubscribe it 8x. */
+int32_t kfmi_host_threads(void)
 {
   const char *e = getenv("KFMI_HOST_THREADS");
-  long n = sysconf(_SC_NPROCESSORS_ONLN);
-  int v = e ? atoi(e) : (int) (n > 16 ? 16 : (n < 1 ? 1 : n));
-  return v < 1 ? 1 : (v > 64 ? 64 : v);
+  long cpus = sysconf(_SC_NPROCESSORS_ONLN), ranks = 1;
+  cpu_set_t set;
+  FILE *fp;
+  if (e) {
+    int v = atoi(e);
+    return v < 1 ? 1 : (v > 64 ? 64 : v);
+  }
+  CPU_ZERO(&set);
+  if (sched_getaffinity(0, sizeof(set), &set) == 0 && CPU_COUNT(&set) > 0 && CPU_COUNT(&set) < cpus)
+    cpus = CPU_COUNT(&set);
+  if ((fp = fopen("/sys/fs/cgroup/cpu.max", "r")) != NULL) {
+    char q[32] = {0};
+    long long per = 0;
+    if (fscanf(fp, "%31s %lld", q, &per) == 2 && strcmp(q, "max") != 0 && per > 0) {
+      long long quota = (atoll(q) + per - 1) / per;
+      if (quota > 0 && quota < cpus) cpus = (long) quota;
+    }
+    fclose(fp);
+  }
+  if ((e = getenv("LOCAL_WORLD_SIZE")) != NULL && atoi(e) > 0) ranks = atoi(e);
+  cpus /= ranks;
+  return (int32_t) (cpus < 2 ? 2 : (cpus > 16 ? 16 : cpus));
 }
+
+static int host_threads(void) { return kfmi_host_threads(); }
 
 static int32_t load_queries_mapped(const char *base, uint64_t size, kfmi_qrys_t *q, uint64_t numqueries,
                                    uint32_t sizequery)

@@ -221,6 +221,7 @@ int32_t freeIndex(void **index)
   if (f->d_entries) kfmi_free_dev_entries(f);
   free(f->h_sa);
   free(f->image);
+  free(f->image_retired);
   free(f);
   *index = NULL;
   return KFMI_SUCCESS;

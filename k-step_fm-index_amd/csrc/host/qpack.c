@@ -38,14 +38,17 @@ static void pack_tail(const uint8_t* row, uint32_t m, uint32_t r0, uint32_t* out
   }
 }
 
-static void pack_rows_scalar(const uint8_t* a, uint64_t n, uint32_t m, uint32_t* out, uint64_t ostride)
+/* Every packer: rows at a, row q at a + q * stride, its first m bases packed
+ * (stride >= m: a read whose last stride - m bases go to the remainder table). */
+static void pack_rows_scalar(const uint8_t* a, uint64_t n, uint32_t stride, uint32_t m, uint32_t* out,
+                             uint64_t ostride)
 {
-  for (uint64_t q = 0; q < n; ++q) pack_tail(a + q * m, m, 0, out + q, ostride);
+  for (uint64_t q = 0; q < n; ++q) pack_tail(a + q * stride, m, 0, out + q, ostride);
 }
 
 /* 32 bases per iteration: load, reverse, codes, 4 codes per byte. */
-__attribute__((target("avx2"))) static void pack_rows_avx2(const uint8_t* a, uint64_t n, uint32_t m, uint32_t* out,
-                                                           uint64_t ostride)
+__attribute__((target("avx2"))) static void pack_rows_avx2(const uint8_t* a, uint64_t n, uint32_t stride, uint32_t m,
+                                                           uint32_t* out, uint64_t ostride)
 {
   const __m256i rev = _mm256_setr_epi8(15, 14, 13, 12, 11, 10, 9, 8, 7, 6, 5, 4, 3, 2, 1, 0,
                                        15, 14, 13, 12, 11, 10, 9, 8, 7, 6, 5, 4, 3, 2, 1, 0);
@@ -56,7 +59,7 @@ __attribute__((target("avx2"))) static void pack_rows_avx2(const uint8_t* a, uin
                                           0, 4, 8, 12, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1);
   const uint32_t full = m / 32;   /* 32-base groups from the end */
   for (uint64_t q = 0; q < n; ++q) {
-    const uint8_t* row = a + q * m;
+    const uint8_t* row = a + q * stride;
     uint32_t* o = out + q;
     for (uint32_t k = 0; k < full; ++k) {
       __m256i v = _mm256_loadu_si256((const __m256i*) (row + m - 32 * (k + 1)));
@@ -81,8 +84,8 @@ __attribute__((target("avx2"))) static void pack_rows_avx2(const uint8_t* a, uin
  * vpermb.  Codes, 4 per byte (maddubs, madd), vpmovdb -> 16 bytes = 4 words;
  * zero bytes code as 0, the padding the words need past 2m bits. */
 __attribute__((target("avx512f,avx512bw,avx512vbmi,avx512vl"))) static void pack_rows_avx512(const uint8_t* a,
-                                                                                            uint64_t n, uint32_t m,
-                                                                                            uint32_t* out,
+                                                                                            uint64_t n, uint32_t stride,
+                                                                                            uint32_t m, uint32_t* out,
                                                                                             uint64_t ostride)
 {
   uint8_t ridx[64], tidx[64];
@@ -97,7 +100,7 @@ __attribute__((target("avx512f,avx512bw,avx512vbmi,avx512vl"))) static void pack
   const __m512i w14 = _mm512_set1_epi16(0x0401), w116 = _mm512_set1_epi32(0x00100001);
   const uint32_t tw = (cnt + 15) / 16;   /* words of the partial block */
   for (uint64_t q = 0; q < n; ++q) {
-    const uint8_t* row = a + q * m;
+    const uint8_t* row = a + q * stride;
     uint32_t* o = out + q;
     for (uint32_t k = 0; k <= full; ++k) {
       __m512i v;
@@ -118,8 +121,12 @@ __attribute__((target("avx512f,avx512bw,avx512vbmi,avx512vl"))) static void pack
   }
 }
 
-/* KFMI_QPACK_ISA=scalar|avx2|avx512 pins the path (tests); default: the widest the host has */
-void kfmi_pack_rows(const uint8_t* ascii, uint64_t n, uint32_t m, uint32_t* out, uint64_t ostride)
+/* KFMI_QPACK_ISA=scalar|avx2|avx512 pins the path (tests); default: the widest the host has.
+ * rem = m % K bases at the end of every read go to the remainder table (DESIGN.md
+ * 5e): the K-step stream covers bases 0 .. m-rem-1 (ceil((m-rem)/16) words) and
+ * word row ceil((m-rem)/16) holds each read's remainder code (base m-1 at bits
+ * 0-1, base m-2 at 2-3, ...) -- the rows pack_queries_kernel writes. */
+void kfmi_pack_rows_rem(const uint8_t* ascii, uint64_t n, uint32_t m, uint32_t rem, uint32_t* out, uint64_t ostride)
 {
   static int isa = -1;   /* 0 scalar, 1 avx2, 2 avx512 */
   const char* e = getenv("KFMI_QPACK_ISA");
@@ -136,9 +143,24 @@ void kfmi_pack_rows(const uint8_t* ascii, uint64_t n, uint32_t m, uint32_t* out,
     const int want = !strcmp(e, "scalar") ? 0 : !strcmp(e, "avx2") ? 1 : 2;
     use = want < isa ? want : isa;
   }
-  if (use == 2) pack_rows_avx512(ascii, n, m, out, ostride);
-  else if (use == 1) pack_rows_avx2(ascii, n, m, out, ostride);
-  else pack_rows_scalar(ascii, n, m, out, ostride);
+  const uint32_t mk = m - rem;
+  if (use == 2) pack_rows_avx512(ascii, n, m, mk, out, ostride);
+  else if (use == 1) pack_rows_avx2(ascii, n, m, mk, out, ostride);
+  else pack_rows_scalar(ascii, n, m, mk, out, ostride);
+  if (rem) {
+    uint32_t* o = out + (uint64_t) ((mk + 15) / 16) * ostride;
+    for (uint64_t q = 0; q < n; ++q) {
+      const uint8_t* row = ascii + q * m;
+      uint32_t c = 0;
+      for (uint32_t u = 0; u < rem; ++u) c |= code2(row[m - 1 - u]) << (2 * u);
+      o[q] = c;
+    }
+  }
+}
+
+void kfmi_pack_rows(const uint8_t* ascii, uint64_t n, uint32_t m, uint32_t* out, uint64_t ostride)
+{
+  kfmi_pack_rows_rem(ascii, n, m, 0, out, ostride);
 }
 
 int32_t kfmi_pack_queries(const char* ascii, uint64_t num, uint32_t size, uint32_t* words)

@@ -33,6 +33,8 @@ typedef struct {
   /* file image: header followed by nentries entries, one allocation */
   uint8_t  *image;
   uint64_t  image_bytes;
+  uint8_t  *image_retired; /* the header-only image an on-demand fetch replaced (kfmi_host_entries):
+                              kept until freeIndex, so a reader holding it never sees it freed */
   uint32_t  header_bytes;
   uint32_t *h_index;       /* = (uint32_t *)(image + header_bytes), may be unaligned to 16;
                               NULL while the entries live only on the device (d_entries) */
@@ -113,6 +115,10 @@ int32_t kfmi_sa_alloc(kfmi_fmi_t *f, uint32_t rate);
 /* qpack.c: ASCII rows -> word-major 2-bit code words (word w of row q at
  * out[w * ostride + q]; ceil(m/16) words per row) */
 void kfmi_pack_rows(const uint8_t *ascii, uint64_t n, uint32_t m, uint32_t *out, uint64_t ostride);
+/* the same for reads whose last rem = m % K bases come from the remainder table:
+ * the stream of bases 0 .. m-rem-1, then one word row of remainder codes */
+void kfmi_pack_rows_rem(const uint8_t *ascii, uint64_t n, uint32_t m, uint32_t rem, uint32_t *out,
+                        uint64_t ostride);
 int     kfmi_sa_rate_ok(uint32_t rate);
 
 /* builders with SA sampling (fmi_build.c, kfmi_build.hip) */

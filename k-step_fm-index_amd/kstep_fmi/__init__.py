@@ -79,6 +79,7 @@ def load() -> ctypes.CDLL:
         "kfmi_get_backend": (ctypes.c_char_p, []),
         "kfmi_set_device": (i32, [i32]),
         "kfmi_device_count": (i32, []),
+        "kfmi_device_pci_bus_id": (i32, [i32, ctypes.c_char_p, i32]),
         "kfmi_last_error": (i32, []),
         "kfmi_search": (i32, [vp, vp, vp]),
         "kfmi_last_timing": (i32, [ctypes.POINTER(ctypes.c_double)] * 3),
@@ -100,6 +101,7 @@ def load() -> ctypes.CDLL:
         "kfmi_device_index_bytes": (u64, [vp]),
         "kfmi_search_stream": (i32, [vp, vp, u64, u32, vp, u64]),
         "kfmi_host_alloc": (i32, [u64, pvp]),
+        "kfmi_host_threads": (i32, []),
         "kfmi_host_free": (i32, [vp]),
         "kfmi_stream_release": (i32, []),
         "kfmi_stream_hostpacked_fraction": (ctypes.c_double, []),
@@ -176,6 +178,18 @@ def build_stats() -> dict:
 
 def device_count() -> int:
     return int(load().kfmi_device_count())
+
+
+def host_threads() -> int:
+    """Threads of the library's parallel host paths (kfmi_host_threads)."""
+    return int(load().kfmi_host_threads())
+
+
+def device_pci_bus_id(dev: int) -> str:
+    """PCI bus id of HIP device `dev` (the physical GPU, stable across processes)."""
+    buf = ctypes.create_string_buffer(64)
+    _check(load().kfmi_device_pci_bus_id(int(dev), buf, 64), f"device_pci_bus_id({dev})")
+    return buf.value.decode()
 
 
 def last_timing():

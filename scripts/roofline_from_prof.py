@@ -11,9 +11,10 @@ warmup launches, then exactly `steps` timed launches (later legs -- variants,
 config #1, locate -- launch kernels of the same name with other grids or
 after them).  So the timed launches are dispatches [warmup, warmup + steps) of
 the kernel whose grid covers the rank's queries.  Traffic: TCC_EA0_RDREQ per
-launch x 128 B (every MID128 LF request is one 128-B line; on gfx950 one
-random line read of up to 128 B is one RDREQ, scripts/traffic_from_pmc.py),
-taken over the same dispatch indices of the PMC pass.
+launch (every MID128 LF request is one 128-B line; on gfx950 one random line
+read of up to 128 B is one RDREQ, scripts/traffic_from_pmc.py), taken over the
+same dispatch indices of the PMC pass; x 128 B it bounds the HBM bytes from
+above (Infinity-Cache hits are counted too).
 """
 import argparse
 import csv
@@ -63,8 +64,8 @@ if a.pmc:
     disp = sorted(by_disp)[a.warmup:a.warmup + a.steps]
     req = statistics.median(by_disp[d]["TCC_EA0_RDREQ_sum"] for d in disp)
     out.update({"pmc": a.pmc, "pmc_launches": len(disp), "rdreq_per_launch": int(req),
-                "traffic_bytes_per_launch": int(req * a.line_bytes),
-                "traffic_GBs": round(req * a.line_bytes / (avg_ms / 1e3) / 1e9, 1),
+                # requests x line bytes counts Infinity-Cache hits too: an upper bound on HBM bytes
+                "request_bytes_upper_bound_per_launch": int(req * a.line_bytes),
                 "rdreq_per_query": round(req / nq, 2),
                 "line_requests_G_per_s": round(req / (avg_ms / 1e3) / 1e9, 2)})
     for c in ("TCC_HIT_sum", "TCC_MISS_sum", "TCC_EA0_RDREQ_DRAM_sum", "TCC_EA0_WRREQ_sum"):

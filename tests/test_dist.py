@@ -33,8 +33,29 @@ WORKER = textwrap.dedent(r"""
                      "lf_ms": 9.0 + D.rank, "step_ms": 9.5 + D.rank, "elapsed_s": el,
                      "parity_ok": D.rank == 0, "parity_sample": 100})
     agg = bench.aggregate_ranks(rows)
+    # an auxiliary leg whose local step fails on rank 1 only: both ranks still make
+    # the same collective calls (all_ok, then gather), skip the timed part together
+    # and report rank 1's error (bench.Steps; ADVICE r2: no hang on a one-rank error)
+    S = bench.Steps()
+    def boom():
+        raise RuntimeError("rank 1 fails")
+    S.run(lambda: 1)
+    if D.rank == 1:
+        S.run(boom)
+    S.run(lambda: 2)                      # skipped after the failure
+    timed_ran = False
+    if D.all_ok(S.ok):
+        D.barrier()
+        timed_ran = True
+    errs = D.gather(S.err)
+    # both ranks on one physical GPU (a one-card rehearsal): one distinct device
+    dev_same = bench.aggregate_devices(D.gather({"rank": D.rank, "local_rank": D.local, "device": 0,
+                                                 "pci_bus_id": "0000:75:00.0", "host": "h"}))
+    dev_two = bench.aggregate_devices(D.gather({"rank": D.rank, "local_rank": D.local, "device": D.local,
+                                                "pci_bus_id": "0000:%%02x:00.0" %% (0x75 + D.local), "host": "h"}))
     out = json.dumps({"rank": D.rank, "world": D.world, "local": D.local, "el": el, "el_max": el_max,
-                      "total": total, "first": reads[0].tobytes().decode(), "start0": int(st[0]), "agg": agg})
+                      "total": total, "first": reads[0].tobytes().decode(), "start0": int(st[0]), "agg": agg,
+                      "timed_ran": timed_ran, "errs": errs, "dev_same": dev_same, "dev_two": dev_two})
     with open("rank%%d.json" %% D.rank, "w") as f:
         f.write(out)
     D.close()
@@ -74,6 +95,12 @@ def test_two_rank_gloo_bench_plumbing(tmp_path):
         assert agg["step_ms_min"] == 9.5 and agg["step_ms_max"] == 10.5
         assert [x["rank"] for x in agg["ranks"]] == [0, 1]
         assert agg["parity_ok_all"] is False                  # one failed rank fails the job
+        # a leg's local failure on one rank: no hang, timed part skipped by both, error reported
+        assert r["timed_ran"] is False
+        assert r["errs"] == [None, "RuntimeError: rank 1 fails"]
+        # device identity: two ranks on one card = one GPU, a rehearsal (no scaling claim)
+        assert r["dev_same"] == {"distinct_devices": 1, "shared_devices": True, "ranks_per_device": [2]}
+        assert r["dev_two"] == {"distinct_devices": 2, "shared_devices": False, "ranks_per_device": [1, 1]}
 
 
 def test_aggregate_ranks_single_and_cpu_threads():
@@ -95,3 +122,30 @@ def test_cpu_thread_counts(monkeypatch):
     if aff > 1:
         assert bench.baseline_thread_counts() == [aff, 1]
     assert bench.cpu_effective() == 1
+
+
+def test_aggregate_devices_fallbacks():
+    import bench
+    # no bus id: the device number per host stands in for it
+    rows = [{"rank": 0, "device": 0, "pci_bus_id": None, "host": "a"},
+            {"rank": 1, "device": 0, "pci_bus_id": None, "host": "a"},
+            {"rank": 2, "device": 0, "pci_bus_id": None, "host": "b"}]
+    agg = bench.aggregate_devices(rows)
+    assert agg["distinct_devices"] == 2 and agg["shared_devices"] is True
+    rows = [{"rank": i, "device": i, "pci_bus_id": f"0000:{i:02x}:00.0", "host": "a"} for i in range(8)]
+    assert bench.aggregate_devices(rows) == {"distinct_devices": 8, "shared_devices": False,
+                                             "ranks_per_device": [1] * 8}
+
+
+def test_steps_and_phases():
+    import bench
+    S = bench.Steps()
+    assert S.run(lambda x: x + 1, 1) == 2 and S.ok
+    assert S.run(lambda: 1 / 0) is None and not S.ok and S.err.startswith("ZeroDivisionError")
+    assert S.run(lambda: 5) is None                    # later steps skipped
+    ph = bench.Phases()
+    ph.mark("a")
+    ph.mark("b")
+    ph.mark("a")                                       # accumulates
+    assert set(ph.rows) == {"a", "b"} and all(v >= 0 for v in ph.rows.values())
+    assert bench.Phases.peak_rss_gb() > 0

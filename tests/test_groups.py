@@ -153,35 +153,32 @@ def test_group_search_driver(tmp_path):
 
 
 @pytest.mark.gpu
-def test_group_replication_setup_time(kfmi_mod):
+def test_group_replication_breakdown(kfmi_mod):
     """A group's index replicas are built once (host upload + relayout on the
-    first member) and fanned out device-to-device, so three replicas on one
-    card cost well under twice the single-device setup (1 Gbase, MID128: a
-    1.5 GB host image, large enough that the fixed per-member cost of streams
-    and events does not dominate)."""
-    import time
+    first member) and fanned out device-to-device.  No wall-clock pass/fail
+    here (bench.py reports the setup times, variants.group_replication): the
+    test checks the replicas and that kfmi_last_timing splits the setup into
+    its parts -- members' streams/events, the fan-out copies, the rest being
+    the first member's upload -- as disjoint parts of the total."""
     K = kfmi_mod
     rng = np.random.default_rng(7)
-    text = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, size=1_000_000_000, dtype=np.uint8)].tobytes()
+    text = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, size=20_000_000, dtype=np.uint8)].tobytes()
     idx = K.Index.build(text, k=2, d=64, gpu=True)
     K.set_backend("task-mid")
-
-    def setup_s(group):
-        best = 1e9
-        for _ in range(3):
+    try:
+        K.set_devices([])
+        K.transfer_to_gpu(idx, None, None)
+        single = idx.device_bytes()
+        for group in ([0, 0], [0, 0, 0]):
             K.set_devices(group)
             idx.free_gpu()
-            t = time.perf_counter()
             K.transfer_to_gpu(idx, None, None)
-            best = min(best, time.perf_counter() - t)
-        return best
-
-    try:
-        one = setup_s([])
-        three = setup_s([0, 0, 0])
-        assert idx.device_bytes() > 0
-        print(f"setup single {one * 1e3:.1f} ms, group of 3 on one card {three * 1e3:.1f} ms")
-        assert three < 2 * one, (one, three)
+            t = K.last_timing()
+            print(f"group {group}: setup {t['total_ms']:.2f} ms = members' streams/events {t['pack_ms']:.2f} + "
+                  f"fan-out {t['lf_ms']:.2f} + first member's upload")
+            assert idx.device_bytes() == len(group) * single > 0
+            assert t["pack_ms"] >= 0 and t["lf_ms"] >= 0
+            assert t["total_ms"] >= t["pack_ms"] + t["lf_ms"]
     finally:
         K.set_devices([])
         idx.free_gpu()
@@ -215,3 +212,50 @@ def test_group_takes_device_parsed_queries(setup, tmp_path, group):
         idx.free_gpu()
         q.close()
         r.close()
+
+
+@pytest.mark.gpu
+def test_two_physical_devices(setup, tmp_path):
+    """A group over two different GPUs: peer access, hipMemcpyPeerAsync replica
+    fan-out, device-to-device read slices, streamed search and block counts
+    across devices -- and the caller's current device left as it was (every
+    entry point restores it).  Needs two GPUs (the driver's one-GPU boxes skip
+    it; the same-device branches are covered by the tests above)."""
+    K, idx, reads = setup
+    if K.device_count() < 2:
+        pytest.skip("one GPU visible: the cross-device branch needs two")
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+
+    def current():
+        d = ctypes.c_int(-1)
+        assert hip.hipGetDevice(ctypes.byref(d)) == 0
+        return d.value
+
+    assert hip.hipSetDevice(1) == 0
+    K.set_backend("task-mid")
+    K.set_devices([])
+    want = K.search_array(idx, reads)
+    assert current() == 1
+    path = tmp_path / "q.fa"
+    path.write_bytes(b"".join(b">r\n" + r.tobytes() + b"\n" for r in reads))
+    try:
+        K.set_devices([0, 1])
+        q, r, got = run_trio(K, idx, reads)
+        assert np.array_equal(got, want)
+        assert current() == 1
+        assert K.count_blocks(idx, q) > 0
+        assert np.array_equal(K.search_stream(idx, reads), want)
+        q.close(); r.close()
+        qd = K.Queries.load_gpu(path, 100)            # parsed on device 0, sliced to device 1 over xGMI
+        rd = K.Results.alloc(reads.shape[0])
+        K.transfer_to_gpu(idx, qd, rd)
+        K.search(idx, qd, rd)
+        K.transfer_to_cpu(rd)
+        assert np.array_equal(rd.array(), want)
+        qd.close(); rd.close()
+        assert current() == 1
+    finally:
+        K.set_devices([])
+        idx.free_gpu()
+        hip.hipSetDevice(0)

@@ -101,10 +101,14 @@ def test_stream_errors(setup):
     K.set_backend("task-mid")
     K.transfer_to_gpu(idx, None, None)
     assert K.search_stream(idx, reads[:0]).size == 0
-    odd = np.ascontiguousarray(reads[:10, :99])          # 99 % K != 0 (B6)
+    odd = np.ascontiguousarray(reads[:10, :99])          # 99 % K != 0 (B6): the remainder table
+    assert np.array_equal(K.search_stream(idx, odd), K.search_array(idx, odd, "task-mid"))
+    K.set_backend("coop-ac")                             # AltCounters semantics: no result defined there
+    K.transfer_to_gpu(idx, None, None)
     with pytest.raises(K.KfmiError) as e:
         K.search_stream(idx, odd)
     assert e.value.code == 33
+    K.set_backend("task-mid")
     fresh = K.Index.build(b"ACGTACGTTGCA" * 50, k=2, d=64, gpu=False)
     with pytest.raises(K.KfmiError) as e:
         K.search_stream(fresh, reads[:10])
@@ -198,3 +202,53 @@ def test_threads_with_different_ftab(setup, oracle_mod):
     for t in ths:
         t.join()
     assert not errs, errs
+
+
+@pytest.fixture(scope="module")
+def rem_setup(kfmi_mod):
+    """One text, its K = 1 image (the oracle's intervals are K-independent) and
+    K = 2 / K = 4 indexes; reads of m % K != 0 with N and lowercase mixed in."""
+    K = kfmi_mod
+    if K.device_count() < 1:
+        pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
+    K.set_device(0)
+    rng = np.random.default_rng(151)
+    text = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=200_003).tobytes()
+    i1 = K.Index.build(text, k=1, d=64, gpu=False)
+    idx = {2: K.Index.build(text, k=2, d=64, gpu=True), 4: K.Index.build(text, k=4, d=64, gpu=True, host_image=False)}
+    return K, text, i1.image(), idx
+
+
+@pytest.mark.parametrize("group", [[], [0, 0]])
+@pytest.mark.parametrize("hostpack", ["1", "0", "2", "3"])
+@pytest.mark.parametrize("k", [2, 4])
+@pytest.mark.parametrize("m", [101, 150, 151])
+def test_stream_remainder_reads(rem_setup, oracle_mod, k, m, hostpack, group, monkeypatch):
+    """m % K != 0 streamed: the last m % K bases of every read come
+    from the remainder table -- host packing writes their codes as one more
+    word row, ASCII chunks are packed in the kernel -- on one device and on a
+    device group; results equal the K = 1 oracle (true suffix-array
+    intervals) and the resident-batch search."""
+    K, text, img1, idx = rem_setup
+    monkeypatch.setenv("KFMI_STREAM_HOSTPACK", hostpack)
+    rng = np.random.default_rng(m * 7 + k)
+    t = np.frombuffer(text, np.uint8)
+    reads = np.concatenate([t[rng.integers(0, len(text) - m, size=3_000)[:, None] + np.arange(m)],
+                            rng.choice(np.frombuffer(b"ACGTNacgt", np.uint8), size=(131, m))])
+    # reads ending inside the text's first / last bases, and ones sharing the text's last bases
+    reads[0] = t[len(text) - m:]
+    reads[1, :] = t[:m]
+    want, _ = oracle_mod.search(img1, reads, 8)
+    backend = "task-mid" if k == 2 else "coop-grp"
+    try:
+        K.set_devices(group)
+        K.set_backend(backend)
+        K.transfer_to_gpu(idx[k], None, None)
+        got = K.search_stream(idx[k], reads, chunk=1_000)
+        assert np.array_equal(got, want)
+        assert np.array_equal(K.search_stream(idx[k], reads), want)
+        if not group:
+            assert np.array_equal(K.search_array(idx[k], reads, backend), want)
+    finally:
+        K.set_devices([])
+        idx[k].free_gpu()
