@@ -66,9 +66,11 @@ for be in ("task", "task-mid", "coop-mid"):
     out["ftab_" + be] = h(got)
     out["ftab_ok_" + be] = bool(np.array_equal(got, want[:40_000]))
 
-# 3. reads with m %% K != 0 (remainder table) on the same index
+# 3. reads with m %% K != 0 (remainder table) on the same index; the oracle
+#    restates the reference, which needs m %% K == 0: its K = 1 image pins them
 r101 = text[st[:5_000, None] + np.arange(101)[None, :]]
-w101, _ = oracle.search(img, r101)
+i1 = K.Index.build(text.tobytes(), k=1, d=64, gpu=False)
+w101, _ = oracle.search(i1.image(), r101)
 got = K.search_array(idx, r101, "task-mid")
 out["rem101"] = h(got)
 out["rem101_ok"] = bool(np.array_equal(got, w101))
