@@ -208,6 +208,18 @@ uint64_t  kfmi_results_num(void *results);
 int32_t kfmi_build_index_cpu(const char *text, uint64_t n, uint32_t k, uint32_t d, void **index);
 int32_t kfmi_build_index_gpu(const char *text, uint64_t n, uint32_t k, uint32_t d,
                              int32_t want_host_image, void **index);
+/* Alphabet of the builders (process-wide; NULL = KFMI_ALPHABET, else "acgt"):
+ *   "acgt" only A/C/G/T (anything else: KFMI_E_BUILDING_BWT);
+ *   "map"  every byte through base2index (N -> G, lowercase -> uppercase), a
+ *          consistent index of that text (true suffix-array intervals);
+ *   "ref"  byte-compatible with the reference builder (genFMindex.c) on any
+ *          text: raw-byte suffix order (divbwt64), base2index codes, and for
+ *          K >= 2 its LF walk, whose unwritten rows hold KFMI_REF_FILL (the
+ *          reference: uninitialised malloc memory).  loadRef also copies the
+ *          file the reference's way (readRef, common.c:42-76: later header
+ *          lines kept, 255-byte fgets pieces each losing their last byte).
+ * All three agree on ACGT-only text. */
+int32_t kfmi_set_alphabet(const char *mode);
 /* Diagnostics of the last GPU build in this process: sorted positions whose
  * 32-base key tied with their predecessor, and the prefix-doubling rounds the
  * device spent resolving them (0 when there were none). */

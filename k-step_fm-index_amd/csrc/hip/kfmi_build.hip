@@ -45,9 +45,11 @@ namespace {
     }                                                                                      \
   } while (0)
 
+/* map = 0: A/C/G/T only (anything else flagged in *bad); map = 1: every byte
+ * through base2index (genFMindex.c:71-84), the "map" and "ref" alphabets */
 __global__ __launch_bounds__(256) void k_encode(const uint8_t* __restrict__ ascii, uint64_t n,
                                                 uint32_t* __restrict__ packed, uint64_t nwords,
-                                                uint32_t* __restrict__ bad)
+                                                uint32_t* __restrict__ bad, uint32_t map)
 {
   const uint64_t w = (uint64_t) blockIdx.x * 256 + threadIdx.x;
   if (w >= nwords) return;
@@ -60,7 +62,10 @@ __global__ __launch_bounds__(256) void k_encode(const uint8_t* __restrict__ asci
     if (i < n) {
       const uint8_t x = ascii[i];
       c = x == 'A' ? 0u : x == 'C' ? 1u : x == 'G' ? 2u : x == 'T' ? 3u : 4u;
-      if (c == 4u) { inval = 1; c = 0; }
+      if (c == 4u) {
+        if (map) c = (((uint32_t) x >> 1) & 3u) ^ (((uint32_t) x >> 2) & 1u);   /* base2index */
+        else { inval = 1; c = 0; }
+      }
     }
     word |= c << (30 - 2 * j);
   }
@@ -83,6 +88,25 @@ __global__ __launch_bounds__(256) void k_keys(const uint32_t* __restrict__ packe
   const uint64_t a = packed[w], b = packed[w + 1], c = packed[w + 2];
   uint64_t k = ((a << 32) | b) << sh;
   if (sh) k |= c >> (32 - sh);
+  keys[i] = k;
+  vals[i] = (uint32_t) i;
+}
+
+/* "ref" alphabet: the key of suffix i is its first L raw bytes as dense ranks
+ * of `bits` bits each (rank 0 past the end, below every byte: '$' sorts
+ * lowest), so the radix sort orders suffixes by raw bytes as divbwt64 does
+ * (genFMindex.c:482); ties go to the prefix doubling with h0 = L. */
+__global__ __launch_bounds__(256) void k_keys_ref(const uint8_t* __restrict__ text, uint64_t n,
+                                                  const uint8_t* __restrict__ lut, uint32_t bits, uint32_t L,
+                                                  uint64_t* __restrict__ keys, uint32_t* __restrict__ vals)
+{
+  __shared__ uint8_t rk[256];
+  rk[threadIdx.x] = lut[threadIdx.x];
+  __syncthreads();
+  const uint64_t i = (uint64_t) blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  uint64_t k = 0;
+  for (uint32_t j = 0; j < L; ++j) k = (k << bits) | (i + j < n ? (uint64_t) rk[text[i + j]] : 0ull);
   keys[i] = k;
   vals[i] = (uint32_t) i;
 }
@@ -299,7 +323,7 @@ uint32_t g_last_tie_rounds = 0;
 
 /* Sorts every group of equal 32-base keys in `sa` (length n, sorted by the
  * keys in `keys`) into true suffix order; see k_dbl_key. */
-int32_t resolve_ties(const uint64_t* keys, uint32_t* sa, uint64_t n, hipStream_t st, uint32_t* rounds)
+int32_t resolve_ties(const uint64_t* keys, uint32_t* sa, uint64_t n, uint64_t h0, hipStream_t st, uint32_t* rounds)
 {
   const dim3 gn((uint32_t) ((n + 255) / 256)), blk(256);
   DevBuf rank, gs, hv0, act, flags, cnt;
@@ -349,7 +373,7 @@ int32_t resolve_ties(const uint64_t* keys, uint32_t* sa, uint64_t n, hipStream_t
   gs.release();
   hv0.release();
   uint32_t r = 0;
-  for (uint64_t h = 32; m > 0; h *= 2, ++r) {
+  for (uint64_t h = h0; m > 0; h *= 2, ++r) {
     if (h > 2 * n + 64) return KFMI_E_BUILDING_BWT;   /* cannot happen: all suffixes differ by then */
     const dim3 gm((uint32_t) ((m + 255) / 256));
     DevBuf k2a, k2b, sfa, sfb, ga, gb, hv, ngs, head, nact, tmp;
@@ -419,22 +443,45 @@ int32_t build_gpu(const char* text, uint64_t n, uint32_t k, uint32_t d, uint32_t
   const uint32_t nc = 1u << (2 * k), nb = d / 32;
   const uint64_t nwords = (n + 15) / 16 + 4;
 
+  /* 0. alphabet (fmi_build.c): "ref" on a text with bytes other than A/C/G/T
+   * sorts raw bytes -- keys of dense byte ranks, `bits` each -- and for K >= 2
+   * leaves BWT_1.. to the reference's LF walk on the host */
+  const int mode = kfmi_alphabet_mode();
+  bool raw_sort = false;
+  uint8_t lut[256] = {0};
+  uint32_t kbits = 2, klen = 32;
+  if (mode == KFMI_ALPHA_REF) {
+    std::vector<uint64_t> hist(256, 0);
+    for (uint64_t i = 0; i < n; ++i) hist[(uint8_t) text[i]]++;
+    if (hist[0]) return KFMI_E_BUILDING_BWT;   /* NUL would tie with '$' */
+    uint32_t sigma = 0;
+    for (int b = 1; b < 256; ++b) {
+      if (hist[b]) lut[b] = (uint8_t) ++sigma;
+      if (hist[b] && b != 'A' && b != 'C' && b != 'G' && b != 'T') raw_sort = true;
+    }
+    if (raw_sort) {
+      kbits = 1;
+      while ((1u << kbits) <= sigma) ++kbits;   /* ranks 1..sigma, 0 past the end */
+      klen = 64 / kbits;
+    }
+  }
+
   /* 1. encode */
-  DevBuf packed, bad;
+  DevBuf packed, bad, ascii;
   BHIP(packed.alloc(nwords * 4));
   BHIP(bad.alloc(4));
   BHIP(hipMemsetAsync(bad.p, 0, 4, st));
   {
-    DevBuf ascii;
     BHIP(ascii.alloc(n));
     BHIP(hipMemcpyAsync(ascii.p, text, n, hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(k_encode, dim3((uint32_t) ((nwords + 255) / 256)), dim3(256), 0, st, ascii.as<uint8_t>(), n,
-                       packed.as<uint32_t>(), nwords, bad.as<uint32_t>());
+                       packed.as<uint32_t>(), nwords, bad.as<uint32_t>(), mode == KFMI_ALPHA_ACGT ? 0u : 1u);
     BHIP(hipGetLastError());
     uint32_t hbad = 0;
     BHIP(hipMemcpyAsync(&hbad, bad.p, 4, hipMemcpyDeviceToHost, st));
     BHIP(hipStreamSynchronize(st));
-    if (hbad) return KFMI_E_BUILDING_BWT;   /* non-ACGT text (see fmi_build.c) */
+    if (hbad) return KFMI_E_BUILDING_BWT;   /* non-ACGT text in the "acgt" alphabet (see fmi_build.c) */
+    if (!raw_sort) ascii.release();
   }
 
   /* 2-3. keys and radix sort */
@@ -445,9 +492,20 @@ int32_t build_gpu(const char* text, uint64_t n, uint32_t k, uint32_t d, uint32_t
     BHIP(k0.alloc(n * 8));
     BHIP(k1.alloc(n * 8));
     BHIP(v0.alloc(n * 4));
-    hipLaunchKernelGGL(k_keys, dim3((uint32_t) ((n + 255) / 256)), dim3(256), 0, st, packed.as<uint32_t>(), n,
-                       k0.as<uint64_t>(), v0.as<uint32_t>());
-    BHIP(hipGetLastError());
+    if (raw_sort) {
+      DevBuf dl;
+      BHIP(dl.alloc(256));
+      BHIP(hipMemcpyAsync(dl.p, lut, 256, hipMemcpyHostToDevice, st));
+      hipLaunchKernelGGL(k_keys_ref, dim3((uint32_t) ((n + 255) / 256)), dim3(256), 0, st, ascii.as<uint8_t>(), n,
+                         dl.as<uint8_t>(), kbits, klen, k0.as<uint64_t>(), v0.as<uint32_t>());
+      BHIP(hipGetLastError());
+      BHIP(hipStreamSynchronize(st));
+      ascii.release();
+    } else {
+      hipLaunchKernelGGL(k_keys, dim3((uint32_t) ((n + 255) / 256)), dim3(256), 0, st, packed.as<uint32_t>(), n,
+                         k0.as<uint64_t>(), v0.as<uint32_t>());
+      BHIP(hipGetLastError());
+    }
     rocprim::double_buffer<uint64_t> kb(k0.as<uint64_t>(), k1.as<uint64_t>());
     rocprim::double_buffer<uint32_t> vb(v0.as<uint32_t>(), sa.as<uint32_t>());
     size_t tbytes = 0;
@@ -472,7 +530,7 @@ int32_t build_gpu(const char* text, uint64_t n, uint32_t k, uint32_t d, uint32_t
     g_last_ties = nties;
     g_last_tie_rounds = 0;
     if (nties) {
-      int32_t e = resolve_ties(kb.current(), sa.as<uint32_t>(), n, st, &g_last_tie_rounds);
+      int32_t e = resolve_ties(kb.current(), sa.as<uint32_t>(), n, klen, st, &g_last_tie_rounds);
       if (e) return e;
     }
   }
@@ -490,6 +548,30 @@ int32_t build_gpu(const char* text, uint64_t n, uint32_t k, uint32_t d, uint32_t
     BHIP(hipMemcpyAsync(drow, dd.p, 16, hipMemcpyDeviceToHost, st));
     BHIP(hipStreamSynchronize(st));
     /* suffix s < K always exists when n >= K; for n < K the missing ones never match */
+  }
+  if (raw_sort && k > 1) {
+    /* "ref" alphabet, K >= 2, text with bytes other than A/C/G/T: BWT_1.. come
+     * from the reference's LF walk (genFMindex.c:327-400), which is not a
+     * permutation then -- one dependent chain over the n + 1 rows, on the host
+     * (kfmi_index_ref_walk, fmi_build.c) from the device's raw-byte SA */
+    std::vector<uint32_t> sa_full(rows);
+    sa_full[0] = (uint32_t) n;
+    BHIP(hipMemcpyAsync(sa_full.data() + 1, sa.p, 4 * n, hipMemcpyDeviceToHost, st));
+    BHIP(hipStreamSynchronize(st));
+    sa.release();
+    kfmi_fmi_t* f = nullptr;
+    int32_t err = kfmi_index_ref_walk(text, sa_full.data(), n, k, d, kfmi_ref_fill(), &f);
+    if (err) return err;
+    if (sa_rate) {
+      err = kfmi_sa_alloc(f, sa_rate);
+      if (err) {
+        freeIndex((void**) &f);
+        return err;
+      }
+      for (uint64_t i = 0; i < f->sa_count; ++i) f->h_sa[i] = sa_full[i * sa_rate];
+    }
+    *out = f;
+    return KFMI_SUCCESS;
   }
   kfmi_fmi_t* f = nullptr;
   int32_t err = kfmi_index_alloc_ex(100, k, (uint32_t) rows, nentries, d, nullptr, nullptr, host_image ? 1 : 0, &f);
@@ -562,10 +644,7 @@ int32_t build_gpu(const char* text, uint64_t n, uint32_t k, uint32_t d, uint32_t
       int64_t pos = (int64_t) s - 1 - (int64_t) s2;
       if (pos < 0) pos += (int64_t) rows;
       uint32_t cs = 0;
-      if ((uint64_t) pos != n) {
-        const char ch = text[pos];
-        cs = ch == 'A' ? 0u : ch == 'C' ? 1u : ch == 'G' ? 2u : 3u;
-      }
+      if ((uint64_t) pos != n) cs = base2index((uint8_t) text[pos]);   /* A/C/G/T, or any byte (map, ref) */
       code |= cs << (2 * s2);
     }
     dbase[s] = code;

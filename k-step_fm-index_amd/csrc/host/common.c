@@ -69,13 +69,41 @@ static int32_t read_ref(const char *fn, uint64_t refsize, char **out, uint64_t *
   return KFMI_SUCCESS;
 }
 
+/* The reference's readRef exactly (common.c:42-76), for KFMI_ALPHABET=ref: the
+ * file read in fgets pieces of at most 255 bytes; after the first line every
+ * piece contributes strlen - 1 bytes -- its newline dropped, or, for a line of
+ * 255 bytes or more, its last data byte -- header lines included. */
+static int32_t read_ref_exact(const char *fn, uint64_t refsize, char **out, uint64_t *got)
+{
+  FILE *fp = fopen(fn, "rb");
+  char piece[256], *ref;
+  uint64_t pos = 0;
+  if (!fp) return KFMI_E_OPENING_REFERENCE_FILE;
+  ref = (char *) malloc(refsize ? refsize : 1);
+  if (!ref) { fclose(fp); return KFMI_E_ALLOCATING_REFERENCE; }
+  if (!fgets(piece, sizeof(piece), fp)) { free(ref); fclose(fp); return KFMI_E_READING_REFERENCE_FILE; }
+  if (piece[0] != '>') { free(ref); fclose(fp); return KFMI_E_READING_MFASTA_FILE; }
+  while (pos < refsize && fgets(piece, sizeof(piece), fp)) {
+    uint64_t l = strlen(piece);
+    if (l) l--;
+    if (l > refsize - pos) l = refsize - pos;
+    memcpy(ref + pos, piece, l);
+    pos += l;
+  }
+  fclose(fp);
+  *out = ref;
+  *got = pos;
+  return KFMI_SUCCESS;
+}
+
 int32_t loadRef(const char *fn, uint32_t refsize, void **reference)
 {
   kfmi_ref_t *ref = (kfmi_ref_t *) calloc(1, sizeof(*ref));
   uint64_t got = 0;
   int32_t err;
   if (!ref) return KFMI_E_ALLOCATING_REFERENCE;
-  err = read_ref(fn, refsize, &ref->h_reference, &got);
+  err = kfmi_alphabet_mode() == KFMI_ALPHA_REF ? read_ref_exact(fn, refsize, &ref->h_reference, &got)
+                                               : read_ref(fn, refsize, &ref->h_reference, &got);
   if (err) { free(ref); return err; }
   if (got != refsize) { free(ref->h_reference); free(ref); return KFMI_E_READING_REFERENCE_FILE; }
   ref->size = got;

@@ -13,9 +13,23 @@
  *   planes   : bit 31-p of plane (s,t,w) of entry b = bit t of code(BWT_s[b*d+32w+p]),
  *              rows >= n+1 are 0 (bwt2bin :402-455)
  *   dollarBaseBWT[s] = c(D_s)
- * The text must be A/C/G/T only: the reference builder's LF walk only counts
- * those four letters (precalculateBasesPreviousBWT :283-309) and produces a
- * broken index for anything else, so other letters are rejected here.
+ * Alphabet modes (KFMI_ALPHABET or kfmi_set_alphabet; the reference has one):
+ *   "acgt" (default): the text must be A/C/G/T only -- the reference builder's
+ *          LF walk only counts those four letters (precalculateBasesPreviousBWT
+ *          :283-309) and produces a broken index for anything else.
+ *   "map": every byte goes through base2index first (N -> G, lowercase ->
+ *          uppercase, genFMindex.c:71-84) and the index is the consistent
+ *          index of that 4-letter text; searches return true suffix-array
+ *          intervals of the mapped text (reads are mapped the same way).
+ *   "ref": byte-compatible with the reference tool on any text: suffixes
+ *          sorted by raw bytes as divbwt64 sorts them (genFMindex.c:482), codes
+ *          and counters through base2index (:86-99, :184-260, :402-424), and for
+ *          K >= 2 the reference's own LF walk (generateOthersBWTs :327-400),
+ *          which for non-ACGT text is not a permutation: rows it never visits
+ *          keep whatever malloc returned there (:342).  That byte is
+ *          KFMI_REF_FILL here (default 0); the reference run under glibc's
+ *          MALLOC_PERTURB_=p fills it with p ^ 0xff, which pins the output
+ *          (tests/golden/alpha).  For ACGT-only text the three modes agree.
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -241,19 +255,215 @@ int32_t kfmi_index_from_sa(const uint8_t *codes, const uint32_t *sa, uint64_t n,
   return KFMI_SUCCESS;
 }
 
-static int text_to_codes(const char *text, uint64_t n, uint8_t *codes)
+/* ----------------------------------------------------------------------- */
+/* alphabet modes (see the header comment)                                   */
+/* ----------------------------------------------------------------------- */
+
+static int g_alpha = -1;   /* -1: KFMI_ALPHABET */
+
+int kfmi_alphabet_mode(void)
+{
+  const char *e;
+  if (g_alpha >= 0) return g_alpha;
+  e = getenv("KFMI_ALPHABET");
+  if (e && !strcmp(e, "map")) return KFMI_ALPHA_MAP;
+  if (e && !strcmp(e, "ref")) return KFMI_ALPHA_REF;
+  return KFMI_ALPHA_ACGT;
+}
+
+int32_t kfmi_set_alphabet(const char *name)
+{
+  if (!name) { g_alpha = -1; return KFMI_SUCCESS; }
+  if (!strcmp(name, "acgt")) g_alpha = KFMI_ALPHA_ACGT;
+  else if (!strcmp(name, "map")) g_alpha = KFMI_ALPHA_MAP;
+  else if (!strcmp(name, "ref")) g_alpha = KFMI_ALPHA_REF;
+  else return KFMI_E_BAD_ARGUMENT;
+  return KFMI_SUCCESS;
+}
+
+uint8_t kfmi_ref_fill(void)
+{
+  const char *e = getenv("KFMI_REF_FILL");
+  return (uint8_t) (e ? strtol(e, NULL, 0) : 0);
+}
+
+/* 2-bit codes of the text: exact A/C/G/T only (acgt; -1 on any other byte), or
+ * base2index of every byte (map, ref; ref rejects NUL, which would tie with
+ * the '$' sentinel of the raw-byte sort).  *acgt_only: no byte outside A/C/G/T. */
+static int text_to_codes(const char *text, uint64_t n, uint8_t *codes, int mode, int *acgt_only)
 {
   uint64_t i;
+  int pure = 1;
   for (i = 0; i < n; i++) {
-    switch (text[i]) {
+    const uint8_t x = (uint8_t) text[i];
+    switch (x) {
       case 'A': codes[i] = 0; break;
       case 'C': codes[i] = 1; break;
       case 'G': codes[i] = 2; break;
       case 'T': codes[i] = 3; break;
-      default: return -1;
+      default:
+        if (mode == KFMI_ALPHA_ACGT || (mode == KFMI_ALPHA_REF && x == 0)) return -1;
+        codes[i] = (uint8_t) base2index(x);
+        pure = 0;
     }
   }
+  if (acgt_only) *acgt_only = pure;
   return 0;
+}
+
+/* ----------------------------------------------------------------------- */
+/* "ref" mode, K >= 2: the reference builder's own LF walk                  */
+/* ----------------------------------------------------------------------- */
+
+static inline int64_t ref_mod(int64_t x, int64_t m) { return (x % m + m) % m; }   /* genFMindex.c:60-62 */
+
+/* Tag-100 index of `text` (n raw bytes) from its raw-byte suffix array sa
+ * (n + 1 rows of T$, sa[0] == n) the way genFMindex.c:457-543 builds it:
+ * BWT_0 from the sort, BWT_1..BWT_{k-1} by the walk of generateOthersBWTs
+ * (:327-400) on the chunk-32 counters of precalculateBasesPreviousBWT
+ * (:262-325, exact 'A'/'C'/'G'/'T' only; any other byte sends the walk to row
+ * 0 + its in-chunk count), rows the walk never writes holding `fill`; '$' -> A
+ * at every D_s (:505-509); then counters, planes and dollarBaseBWT through
+ * base2index (precalculateBasesKSteps :184-260, bwt2bin :427-455, :518-520). */
+int32_t kfmi_index_ref_walk(const char *text, const uint32_t *sa, uint64_t n, uint32_t k, uint32_t d, uint8_t fill,
+                            kfmi_fmi_t **out)
+{
+  const uint64_t rows = n + 1;
+  const uint32_t nc = 1u << (2 * k), nb = d / 32, nchunk = (uint32_t) ((rows + 31) / 32);
+  uint8_t *bwt[KFMI_MAX_STEPS] = {NULL, NULL, NULL, NULL};
+  uint32_t (*cnt32)[4] = NULL;
+  uint32_t nentries, s, c, dpos[KFMI_MAX_STEPS], dbase[KFMI_MAX_STEPS];
+  uint64_t r, tot[4] = {0, 0, 0, 0}, *total = NULL;
+  uint32_t *cprime = NULL, *run = NULL;
+  int64_t position, refpos;
+  kfmi_fmi_t *f = NULL;
+  int32_t err = KFMI_E_ALLOCATING_BWT;
+  if (k < 1 || k > KFMI_MAX_STEPS || d == 0 || d % 32 || rows > 0x7FFFFFFFull || rows < k) return KFMI_E_BAD_ARGUMENT;
+  for (s = 0; s < k; s++) {
+    bwt[s] = (uint8_t *) malloc(rows);
+    if (!bwt[s]) goto done;
+    if (s) memset(bwt[s], fill, rows);
+  }
+  for (s = 0; s < k; s++) { dpos[s] = 0; dbase[s] = 0; }
+  /* BWT_0 with '$' at its primary index (:482-494) */
+  for (r = 0; r < rows; r++) {
+    bwt[0][r] = sa[r] == 0 ? (uint8_t) '$' : (uint8_t) text[sa[r] - 1];
+    if (sa[r] == 0) dpos[0] = (uint32_t) r;
+  }
+  if (k > 1) {
+    /* precalculateBasesPreviousBWT, chunk 32 (:262-325) */
+    cnt32 = (uint32_t (*)[4]) malloc(sizeof(*cnt32) * nchunk);
+    if (!cnt32) goto done;
+    for (r = 0; r < rows; r++) {
+      if (r % 32 == 0)
+        for (c = 0; c < 4; c++) cnt32[r / 32][c] = (uint32_t) tot[c];
+      switch (bwt[0][r]) {
+        case 'A': tot[0]++; break;
+        case 'C': tot[1]++; break;
+        case 'G': tot[2]++; break;
+        case 'T': tot[3]++; break;
+        default: break;
+      }
+    }
+    {
+      const uint32_t acc[4] = {1u, (uint32_t) (1 + tot[0]), (uint32_t) (1 + tot[0] + tot[1]),
+                               (uint32_t) (1 + tot[0] + tot[1] + tot[2])};
+      uint32_t j;
+      for (j = 0; j < nchunk; j++)
+        for (c = 0; c < 4; c++) cnt32[j][c] += acc[c];
+    }
+    /* generateOthersBWTs (:347-391) */
+    position = dpos[0];
+    for (refpos = (int64_t) rows - 1; refpos >= 0; refpos--) {
+      const int64_t desp = position % 32, posb = position - desp;
+      uint8_t base;
+      int64_t j;
+      if (refpos >= (int64_t) k - 1) {
+        for (s = 1; s < k; s++) bwt[s][position] = (uint8_t) text[refpos - s];
+      } else {
+        for (s = 1; s < k; s++) {
+          const int64_t m = ref_mod(refpos - (int64_t) s, (int64_t) rows);
+          bwt[s][position] = m == (int64_t) rows - 1 ? (uint8_t) '$' : (uint8_t) text[m];
+        }
+        dpos[refpos + 1] = (uint32_t) position;
+      }
+      base = bwt[0][position];
+      switch (base) {
+        case 'A': position = cnt32[position / 32][0]; break;
+        case 'C': position = cnt32[position / 32][1]; break;
+        case 'G': position = cnt32[position / 32][2]; break;
+        case 'T': position = cnt32[position / 32][3]; break;
+        default: position = 0; break;
+      }
+      for (j = 0; j < desp; j++)
+        if (bwt[0][posb + j] == base) position++;
+    }
+  }
+  for (s = 0; s < k; s++) bwt[s][dpos[s]] = 'A';   /* :505-509 */
+
+  /* precalculateBasesKSteps (:184-260) and bwt2bin (:427-455) */
+  nentries = (uint32_t) ((rows + d - 1) / d);
+  err = kfmi_index_alloc(100, k, (uint32_t) rows, nentries, d, NULL, NULL, &f);
+  if (err) goto done;
+  err = KFMI_E_ALLOCATING_FMI;
+  total = (uint64_t *) calloc(nc, sizeof(uint64_t));
+  cprime = (uint32_t *) calloc(nc, sizeof(uint32_t));
+  run = (uint32_t *) calloc(nc, sizeof(uint32_t));
+  if (!total || !cprime || !run) goto done;
+  {
+    const uint32_t ew = f->entry_words, nbw = 2 * nb * k;
+    for (r = 0; r < rows; r++) {
+      const uint64_t b = r / d;
+      const uint32_t off = (uint32_t) (r % d), w = off / 32, p = off % 32;
+      uint32_t *ent = f->h_index + b * ew, code = 0, isd = 0;
+      if (off == 0) memcpy(ent + nbw, run, sizeof(uint32_t) * nc);
+      for (s = 0; s < k; s++) {
+        const uint32_t cs = base2index(bwt[s][r]);
+        code |= cs << (2 * s);
+        if (cs & 1u) ent[kfmi_plane_index(100, k, nb, s, 0, w)] |= 1u << (31 - p);
+        if (cs & 2u) ent[kfmi_plane_index(100, k, nb, s, 1, w)] |= 1u << (31 - p);
+      }
+      for (s = 0; s < k; s++) if (dpos[s] == r) isd = 1;   /* checkPositionBWT (:114-121) */
+      if (!isd) { run[code]++; total[code]++; }
+    }
+    for (s = 0; s < k; s++) {   /* index2BaseBWT at D_s (:518-520) */
+      uint32_t code = 0, t;
+      for (t = 0; t < k; t++) code |= base2index(bwt[t][dpos[s]]) << (2 * t);
+      dbase[s] = code;
+    }
+    {
+      uint64_t acc = 0;
+      for (c = 0; c < nc; c++) { cprime[c] = (uint32_t) acc; acc += total[c]; }
+      for (s = 0; s < k; s++) {   /* dollar2BaseBWT adjustments (:246-250) */
+        const uint32_t masked = dbase[s] & (0xFFFFFFFFu << (2 * s));
+        for (c = masked; c < nc; c++) cprime[c]++;
+      }
+    }
+    for (r = 0; r < nentries; r++) {
+      uint32_t *cn = f->h_index + r * ew + nbw;
+      for (c = 0; c < nc; c++) cn[c] += cprime[c];
+    }
+  }
+  for (s = 0; s < k; s++) {
+    f->dollarPositionBWT[s] = dpos[s];
+    f->dollarBaseBWT[s] = dbase[s];
+    f->modposdollarBWT[s] = dpos[s] / d;
+  }
+  {
+    const void *img; uint64_t bytes;
+    kfmi_index_image(f, &img, &bytes);   /* refresh header words */
+  }
+  *out = f;
+  f = NULL;
+  err = KFMI_SUCCESS;
+done:
+  if (f) freeIndex((void **) &f);
+  for (s = 0; s < k; s++) free(bwt[s]);
+  free(cnt32);
+  free(total);
+  free(cprime);
+  free(run);
+  return err;
 }
 
 int32_t kfmi_build_index_cpu(const char *text, uint64_t n, uint32_t k, uint32_t d, void **index)
@@ -270,6 +480,8 @@ int32_t kfmi_build_index_cpu_sa(const char *text, uint64_t n, uint32_t k, uint32
   uint32_t *sa;
   uint64_t i;
   int32_t err;
+  const int mode = kfmi_alphabet_mode();
+  int acgt_only = 1;
   if (n == 0 || n + 1 < k || n + 1 > 0xFFFFFFFEull) return KFMI_E_BAD_ARGUMENT;
   if (k < 1 || k > KFMI_MAX_STEPS || d == 0 || d % 32) return KFMI_E_BAD_ARGUMENT;
   if (sa_rate && !kfmi_sa_rate_ok(sa_rate)) return KFMI_E_BAD_ARGUMENT;
@@ -277,12 +489,23 @@ int32_t kfmi_build_index_cpu_sa(const char *text, uint64_t n, uint32_t k, uint32
   sym = (uint8_t *) malloc(n + 1);
   sa = (uint32_t *) malloc(sizeof(uint32_t) * (n + 1));
   if (!codes || !sym || !sa) { free(codes); free(sym); free(sa); return KFMI_E_ALLOCATING_BWT; }
-  if (text_to_codes(text, n, codes)) { free(codes); free(sym); free(sa); return KFMI_E_BUILDING_BWT; }
-  for (i = 0; i < n; i++) sym[i] = (uint8_t) (codes[i] + 1);   /* '$' = 0 < A..T = 1..4 */
-  sym[n] = 0;
-  err = kfmi_sais(sym, sa, (uint32_t) (n + 1), 5);
+  if (text_to_codes(text, n, codes, mode, &acgt_only)) { free(codes); free(sym); free(sa); return KFMI_E_BUILDING_BWT; }
+  if (mode == KFMI_ALPHA_REF && !acgt_only) {
+    for (i = 0; i < n; i++) sym[i] = (uint8_t) text[i];        /* raw bytes, as divbwt64 sorts them */
+    sym[n] = 0;
+    err = kfmi_sais(sym, sa, (uint32_t) (n + 1), 256);
+  } else {
+    for (i = 0; i < n; i++) sym[i] = (uint8_t) (codes[i] + 1);   /* '$' = 0 < A..T = 1..4 */
+    sym[n] = 0;
+    err = kfmi_sais(sym, sa, (uint32_t) (n + 1), 5);
+  }
   free(sym);
-  if (!err) err = kfmi_index_from_sa(codes, sa, n, k, d, (kfmi_fmi_t **) index);
+  if (!err) {
+    if (mode == KFMI_ALPHA_REF && !acgt_only && k > 1)
+      err = kfmi_index_ref_walk(text, sa, n, k, d, kfmi_ref_fill(), (kfmi_fmi_t **) index);
+    else
+      err = kfmi_index_from_sa(codes, sa, n, k, d, (kfmi_fmi_t **) index);
+  }
   if (!err && sa_rate) {
     kfmi_fmi_t *f = (kfmi_fmi_t *) *index;
     err = kfmi_sa_alloc(f, sa_rate);

@@ -110,6 +110,7 @@ def load() -> ctypes.CDLL:
         "kfmi_get_devices": (i32, [ctypes.POINTER(ctypes.c_int32), i32]),
         "kfmi_build_index_ex": (i32, [vp, u64, u32, u32, u32, i32, pvp]),
         "kfmi_set_ftab": (i32, [u32]),
+        "kfmi_set_alphabet": (i32, [ctypes.c_char_p]),
         "kfmi_index_sa": (i32, [vp, pvp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32)]),
         "kfmi_save_sa": (i32, [ctypes.c_char_p, vp]),
         "kfmi_load_sa": (i32, [ctypes.c_char_p, vp]),
@@ -149,6 +150,12 @@ def get_backend() -> str:
 def set_ftab(bases: int) -> None:
     """Bowtie-style jump-start table of `bases` bases for the task backends (0 = off)."""
     _check(load().kfmi_set_ftab(int(bases)), f"set_ftab({bases})")
+
+
+def set_alphabet(mode: str | None) -> None:
+    """Builders' alphabet: "acgt" (default), "map" (base2index every byte) or
+    "ref" (byte-compatible with the reference builder); None = KFMI_ALPHABET."""
+    _check(load().kfmi_set_alphabet(mode.encode() if mode else None), f"set_alphabet({mode})")
 
 
 def set_device(dev: int) -> None:
