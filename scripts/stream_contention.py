@@ -12,6 +12,9 @@ library then splits the host's CPU share among the ranks, kfmi_host_threads).
 On a one-GPU box the P processes also share the card and its PCIe link, so
 the ASCII mode is charged more than on an 8-GPU node (one link per rank);
 the host-side numbers (packing time, staging) are what this measures.
+Summary per (P, input, mode): every rank's median wall over rounds 1.. (round
+0 -- first-touch of the output arrays and staging buffers -- excluded), then
+the slowest rank.
 """
 from __future__ import annotations
 
@@ -79,7 +82,7 @@ print(json.dumps(rows))
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--procs", type=int, nargs="+", default=[1, 2])
-    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--rounds", type=int, default=7, help="rounds per mode; round 0 is a warm-up, not summarised")
     ap.add_argument("--ref-size", type=int, default=1_000_000_000)
     ap.add_argument("--queries", type=int, default=10_000_000)
     ap.add_argument("--qlen", type=int, default=150)
@@ -108,7 +111,7 @@ def main() -> int:
             for kind in ("pageable", "pinned"):
                 per = {}
                 for mode in ("adaptive", "host-packed", "ascii"):
-                    sel = [r for r in rows if r["input"] == kind and r["mode"] == mode]
+                    sel = [r for r in rows if r["input"] == kind and r["mode"] == mode and r["round"] > 0]
                     # per-rank median over rounds, then the slowest rank (the job's wall)
                     med = []
                     for rank in range(P):
