@@ -253,7 +253,10 @@ int32_t kfmi_search_stream(void *index, const char *ascii, uint64_t num, uint32_
  * `numqueries` reads out as loadQueries would (0 = every read in the file);
  * same format and errors as loadQueries.  The returned queries live on the
  * device only (no host copy): transferCPUtoGPU uses them as they are (on the
- * device they were loaded on; not for device groups). */
+ * device they were loaded on); on a device group every member copies its slice
+ * device to device, and the parsing device's full copy stays allocated beside
+ * the slices (its bytes count twice there) so that the same handle still works
+ * in single-device mode afterwards -- freeQueriesGPU releases both. */
 int32_t kfmi_load_queries_gpu(const char *fn, uint32_t sizequery, uint64_t numqueries, void **queries);
 /* Packs num reads of `size` bases (plain layout q*size, as loadQueries keeps
  * them, common.c:163-173) into the 2-bit code words the search consumes, on the
