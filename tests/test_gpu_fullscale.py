@@ -132,3 +132,39 @@ def test_3g_kstep4_full_scale(gpu, g3, reads, split, tmp_path, monkeypatch):
     finally:
         i4.free_gpu()
         i4.close()
+
+
+def test_3g_config5_whole_batch(gpu, g3, oracle_mod):
+    """Config #5's whole batch in one process: 80M x 150 bp reads (12 GB of
+    ASCII, more than 2^32 bytes and 2^32 intervals' worth of offsets) on the
+    3 Gbase index, through the reference's own handles laid out as config #5
+    lays them out -- the index replicated on 8 members (KFMI_DEVICES; here the
+    one card listed 8 times, so the replicas and slices are real but the card
+    is shared) and the reads cut into 8 slices -- and through the streamed
+    path on the same group.  Both equal, and an evenly spread 200 K-read sample
+    equals the CPU oracle.  (The 8-GPU timing is the driver's SCALE run.)"""
+    from kstep_fmi import synth
+    text, idx = g3
+    n = 80_000_000
+    rng = np.random.default_rng(805)
+    reads = synth.gather_reads(text, rng.integers(0, N3G - 150, size=n), 150)
+    assert reads.nbytes > 2 ** 32
+    sel = np.linspace(0, n - 1, 200_000).astype(np.int64)
+    want, _ = oracle_mod.search(idx.image(), reads[sel])
+    gpu.set_backend("task-mid")
+    try:
+        gpu.set_devices([0] * 8)
+        q = gpu.Queries.from_array(reads)
+        r = gpu.Results.alloc(n)
+        gpu.transfer_to_gpu(idx, q, r)
+        gpu.search(idx, q, r)
+        gpu.transfer_to_cpu(r)
+        res = r.array().copy()
+        q.close()
+        r.close()
+        assert np.array_equal(res.reshape(-1, 2)[sel], want.reshape(-1, 2))
+        streamed = gpu.search_stream(idx, reads)
+        assert np.array_equal(streamed, res)
+    finally:
+        gpu.set_devices([])
+        idx.free_gpu()
