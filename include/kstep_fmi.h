@@ -265,6 +265,12 @@ int32_t kfmi_load_queries_gpu(const char *fn, uint32_t sizequery, uint64_t numqu
  * the read's bit string (fmIndexCPUBaseline.c:200-226 order; K-independent).
  * kfmi_search_stream uses it to send 4 bytes per 16 bases over PCIe. */
 int32_t kfmi_pack_queries(const char *ascii, uint64_t num, uint32_t size, uint32_t *words);
+/* The same for a K-step index (K = 1, 2 or 4) and reads of any length: with
+ * r = size % K, the stream covers bases 0 .. size-r-1 (ceil((size-r)/16) word
+ * rows) and, when r > 0, one more row holds each read's remainder-table index
+ * (base size-1 at bits 0-1, size-2 at 2-3, ...) -- what kfmi_search_stream
+ * sends for such reads.  r = 0 gives kfmi_pack_queries' words. */
+int32_t kfmi_pack_queries_k(const char *ascii, uint64_t num, uint32_t size, uint32_t k, uint32_t *words);
 /* Host threads of the parallel host paths (loadQueries, the streamed search's
  * packers, the device loader's reads): KFMI_HOST_THREADS, else this process's
  * CPUs (affinity mask capped by the cgroup quota) divided among the ranks on

@@ -170,3 +170,11 @@ int32_t kfmi_pack_queries(const char* ascii, uint64_t num, uint32_t size, uint32
   kfmi_pack_rows((const uint8_t*) ascii, num, size, words, num);
   return KFMI_SUCCESS;
 }
+
+int32_t kfmi_pack_queries_k(const char* ascii, uint64_t num, uint32_t size, uint32_t k, uint32_t* words)
+{
+  if ((!ascii || !words) && num) return KFMI_E_BAD_ARGUMENT;
+  if (size == 0 || (k != 1 && k != 2 && k != 4)) return KFMI_E_BAD_ARGUMENT;
+  kfmi_pack_rows_rem((const uint8_t*) ascii, num, size, size % k, words, num);
+  return KFMI_SUCCESS;
+}

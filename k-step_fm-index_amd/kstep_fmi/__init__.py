@@ -106,6 +106,7 @@ def load() -> ctypes.CDLL:
         "kfmi_stream_release": (i32, []),
         "kfmi_stream_hostpacked_fraction": (ctypes.c_double, []),
         "kfmi_pack_queries": (i32, [vp, u64, u32, vp]),
+        "kfmi_pack_queries_k": (i32, [vp, u64, u32, u32, vp]),
         "kfmi_set_devices": (i32, [ctypes.POINTER(ctypes.c_int32), i32]),
         "kfmi_get_devices": (i32, [ctypes.POINTER(ctypes.c_int32), i32]),
         "kfmi_build_index_ex": (i32, [vp, u64, u32, u32, u32, i32, pvp]),
@@ -478,6 +479,18 @@ def pack_queries(reads: np.ndarray) -> np.ndarray:
     n, m = reads.shape
     out = np.empty(((m + 15) // 16, n), dtype=np.uint32)
     _check(load().kfmi_pack_queries(reads.ctypes.data, n, m, out.ctypes.data), "kfmi_pack_queries")
+    return out
+
+
+def pack_queries_k(reads: np.ndarray, k: int) -> np.ndarray:
+    """Host packing for a K-step index and any read length (kfmi_pack_queries_k):
+    uint32 [rows, N], the K-step stream of bases 0 .. m-r-1 plus, for r = m % K
+    > 0, a row of remainder codes."""
+    reads = np.ascontiguousarray(reads, dtype=np.uint8)
+    n, m = reads.shape
+    r = m % k
+    out = np.empty(((m - r + 15) // 16 + (1 if r else 0), n), dtype=np.uint32)
+    _check(load().kfmi_pack_queries_k(reads.ctypes.data, n, m, int(k), out.ctypes.data), "kfmi_pack_queries_k")
     return out
 
 

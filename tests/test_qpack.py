@@ -58,3 +58,36 @@ def test_pack_large_batch_and_errors(kfmi_mod):
     assert np.array_equal(got, w.T)
     assert K.pack_queries(reads[:0]).shape == (7, 0)
     assert K.load().kfmi_pack_queries(None, 5, 100, None) == 33
+
+
+def words_rem_ref(reads: np.ndarray, k: int) -> np.ndarray:
+    """Remainder layout: the K-step stream of bases 0 .. m-r-1
+    (as if the read were m - r long), then one row: code of base m-1 at bits
+    0-1, m-2 at 2-3, ... (the remainder-table index)."""
+    n, m = reads.shape
+    r = m % k
+    head = words_ref(np.ascontiguousarray(reads[:, :m - r]), 1) if m - r else np.zeros((0, n), np.uint32)
+    if not r:
+        return head
+    rc = np.zeros(n, dtype=np.uint32)
+    for u in range(r):
+        rc |= np.array([util.code_of(int(x)) for x in reads[:, m - 1 - u]], dtype=np.uint32) << np.uint32(2 * u)
+    return np.vstack([head, rc[None, :]])
+
+
+@pytest.mark.parametrize("isa", ["scalar", "avx2", "avx512"])
+@pytest.mark.parametrize("k", [1, 2, 4])
+@pytest.mark.parametrize("m", [1, 3, 5, 17, 33, 63, 65, 99, 101, 150, 151, 257])
+def test_pack_remainder_rows(kfmi_mod, isa, k, m, monkeypatch):
+    """Host packing of reads with m % K != 0 for the streamed search: the
+    stream stops r = m % K bases early and a row of remainder codes follows,
+    the rows the device pack kernel writes (every ISA path, every length class)."""
+    K = kfmi_mod
+    monkeypatch.setenv("KFMI_QPACK_ISA", isa)
+    rng = np.random.default_rng(m * 10 + k)
+    reads = rng.choice(np.frombuffer(b"ACGTNacgtn", np.uint8), size=(29, m))
+    got = K.pack_queries_k(reads, k)
+    assert np.array_equal(got, words_rem_ref(reads, k))
+    if m % k == 0:
+        assert np.array_equal(got, K.pack_queries(reads))
+    assert K.load().kfmi_pack_queries_k(reads.ctypes.data, 29, m, 3, got.ctypes.data) == 33   # K = 3 streams ASCII
