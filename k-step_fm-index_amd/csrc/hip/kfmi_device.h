@@ -82,6 +82,11 @@ struct Geo {
   static constexpr bool SMALL = BMW <= 16;                // whole bitmap fits in registers
   static constexpr bool TWO_SIDED = LAY == LAY_AC || LAY == LAY_MID || LAY == LAY_AC128 || LAY == LAY_MIDAC;
   static constexpr bool MIDLINES = LAY == LAY_MID || LAY == LAY_MIDAC;   // pairs of blocks per line
+  // the reference's own layouts (tag 101 / 201), register-resident blocks: a
+  // block whose counter lies past the 128-B line of its planes is counted
+  // forward from the previous block's counter when that entry lies in the
+  // line (line_local_prev): one HBM line per LF where the layout allows it
+  static constexpr bool NEIGHBOR = (LAY == LAY_INTER || LAY == LAY_AC) && SMALL;
 };
 
 // Superblock shift of the packed layout: the largest S with (2^S - 1) * d <= 65535.
@@ -308,7 +313,48 @@ struct Where {
   const uint32_t* planes;
   const uint32_t* cnt;      // counter word (unused for packed: see delta/sb)
   bool e;                   // backward (two-sided layouts)
+  bool prev = false;        // NEIGHBOR: counted forward from block b-1 (cnt is cnt_{b-1}[c])
+  const uint32_t* pplanes = nullptr;   // NEIGHBOR, prev: the planes of block b-1
 };
+
+// Reference layouts (tag 101 INTER: [planes | cnt[NC]]; tag 201 AC:
+// [cnt_half | planes]) in HBM as stored, 128-B lines.  When the counter the
+// reference reads for (b, c) sits in another line than block b's planes --
+// INTER, K=2, d=64: blocks b % 4 == 1 (entry [96, 192) of a line pair) and
+// b % 4 == 2 with c >= 8; AC: odd blocks with c < NC/2, whose counter is entry
+// b+1's -- but the whole previous entry b-1 lies in the planes' line (INTER
+// b % 4 == 1; AC every odd b), the step is taken forward from cnt_{b-1}[c]:
+//   X' = cnt_{b-1}[c] + popc(rows [start(b-1), X) of code c) - #{s : D_s in
+//        blocks b-1, b, dollarBase_s == c, X > D_s}
+// -- the same integer, since the reference builder derives every counter from
+// the planes it stores (cnt_b = cnt_{b-1} + rows of block b-1 with code c,
+// '$' rows excluded), so counts are consistent block to block.  The AC
+// semantics differ from this only where the tfmiAC sentinel's counters are
+// read (blocks >= E-1, ix.ac_tail_b0), which keep the reference's step.
+// Which path a step takes changes no result, only the lines it touches:
+// INTER 1.375 -> 1.125 lines per LF, AC 1.25 -> 1.
+template <class G>
+__device__ __forceinline__ void line_local_prev(const IdxArgs& ix, uint32_t b, uint32_t c, Where<G>& w)
+{
+  if constexpr (G::NEIGHBOR) {
+    if (b == 0) return;
+    const uint64_t pb = 4ull * ((uint64_t) b * G::EW + G::BOFF);   /* bytes: planes of block b */
+    const uint64_t line = pb >> 7;
+    if (((uint64_t) (w.cnt - ix.ent) * 4ull) >> 7 == line) return;  /* the reference's counter is in the line */
+    if constexpr (G::LAY == LAY_AC) {
+      if (!w.e || b >= ix.ac_tail_b0) return;   /* forward already, or the sentinel's counters */
+    }
+    const uint32_t cw = G::LAY == LAY_AC ? (c & (G::HALF - 1)) : (uint32_t) G::BMW + c;
+    const uint64_t e0 = (uint64_t) (b - 1) * G::EW;
+    if ((4ull * (e0 + G::BOFF)) >> 7 != line || (4ull * (e0 + G::BOFF + G::BMW) - 1) >> 7 != line ||
+        (4ull * (e0 + cw)) >> 7 != line)
+      return;
+    w.prev = true;
+    w.e = false;
+    w.pplanes = ix.ent + e0 + G::BOFF;
+    w.cnt = ix.ent + e0 + cw;
+  }
+}
 
 template <class G>
 __device__ __forceinline__ Where<G> locate(const IdxArgs& ix, uint32_t b, uint32_t c)
@@ -416,9 +462,11 @@ __device__ __forceinline__ uint32_t ac_tail_step(const IdxArgs& ix, uint32_t b, 
 template <class G>
 struct Blk {
   uint32_t bm[G::BMW];
+  uint32_t bp[G::NEIGHBOR ? G::BMW : 1];   // NEIGHBOR, prev: planes of block b-1
   uint32_t cnt;
   uint32_t b;
   bool e;
+  bool prev;
 };
 
 template <class G, bool NT = false>
@@ -445,10 +493,15 @@ __device__ __forceinline__ void load_planes(const uint32_t* __restrict__ p, uint
 template <class G, bool NT = false>
 __device__ __forceinline__ void fetch_block(const IdxArgs& ix, uint32_t b, uint32_t c, Blk<G>& k)
 {
-  const Where<G> w = locate<G>(ix, b, c);
+  Where<G> w = locate<G>(ix, b, c);
+  line_local_prev<G>(ix, b, c, w);
   k.b = b;
   k.e = w.e;
+  k.prev = w.prev;
   load_planes<G, NT>(w.planes, k.bm);
+  if constexpr (G::NEIGHBOR) {
+    if (w.prev) load_planes<G, NT>(w.pplanes, k.bp);
+  }
   k.cnt = load_counter<G, NT>(ix, w, b, c);
 }
 
@@ -470,6 +523,20 @@ __device__ __forceinline__ uint32_t lf_from_block(const IdxArgs& ix, const Blk<G
 #pragma unroll
       for (int w = 0; w < G::NB; ++w) all += __popc(select_rows<G::K>(&k.bm[w * G::PW], sx));
       return ac_tail_step<G>(ix, k.b, c, X, pop, all);
+    }
+  }
+  if constexpr (G::NEIGHBOR) {
+    if (k.prev) {   /* forward from cnt_{b-1}: all of block b-1, then rows [start(b), X) of block b */
+#pragma unroll
+      for (int w = 0; w < G::NB; ++w) pop += __popc(select_rows<G::K>(&k.bp[w * G::PW], sx));
+      int corr = 0;
+#pragma unroll
+      for (int s = 0; s < G::K; ++s)
+        corr += ((ix.dl.dblk[s] == k.b || ix.dl.dblk[s] + 1u == k.b) && ix.dl.dbase[s] == c && X > ix.dl.dpos[s]) ? 1
+                                                                                                                 : 0;
+      const uint32_t v = k.cnt + pop - (uint32_t) corr;
+      if constexpr (G::ACRULE) return ac_clamp<G>(ix, v);
+      return v;
     }
   }
   return finish<G>(ix, k.cnt, pop, k.b, c, X, k.e);

@@ -832,6 +832,9 @@ int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx, kfmi_dev_
   di->device = dev;
   di->backend = backend;
   di->layout = lay;
+  /* LAY_AC: the last real block E-1 (tag-201 entries end with the sentinel E):
+   * steps from there on keep the reference's counter (line_local_prev) */
+  if (lay == LAY_AC) di->ac_tail_b0 = src->nentries >= 2 ? src->nentries - 2 : 0;
   di->K = f->steps;
   di->d = f->chunk;
   di->nb = f->nbitmaps;
