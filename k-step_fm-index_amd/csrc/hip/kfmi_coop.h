@@ -25,10 +25,16 @@
 
 namespace kfmi {
 
+// NEIGHBOR geometries (reference tag-101/201 layouts, kfmi_device.h
+// line_local_prev): the DMA carries bit planes only -- block b's and, when the
+// step is counted forward from entry b-1, block b-1's -- and the lane owning
+// the interval end loads its one counter word itself (same 128-B line, merged
+// in L2 with the DMA's request), so no request needs a second line's chunk.
 template <class G>
 struct CoopCfg {
   static constexpr int BC = G::BMW / 4;                 // 16-byte bitmap chunks per block
-  static constexpr int TPR = pow2ceil(BC + 1);          // lanes per request (+1 counter chunk)
+  static constexpr bool NBR = G::NEIGHBOR;              // planes of b [and b-1]; counter per lane
+  static constexpr int TPR = NBR ? pow2ceil(2 * BC) : pow2ceil(BC + 1);   // lanes per request
   static constexpr int RPR = 64 / TPR;                  // requests per round
   static constexpr int SLOT = TPR * 16;                 // LDS bytes per request slot
   static constexpr int MAXREQ = 128;                    // 64 L + up to 64 R
@@ -121,6 +127,41 @@ __device__ __forceinline__ uint32_t coop_lf(const IdxArgs& ix, const uint8_t* sl
     cnt = reinterpret_cast<const uint32_t*>(slot + 16 * C::BC)[c & 3u];
   if constexpr (G::LAY == LAY_MIDAC)
     if (b >= ix.ac_tail_b0) return ac_tail_step<G>(ix, b, c, X, pop, all);
+  return finish<G>(ix, cnt, pop, b, c, X, e);
+}
+
+// NEIGHBOR geometries: the slot holds block b's planes (chunks 0 .. BC-1) and,
+// when w.prev, block b-1's (chunks BC .. 2BC-1); cnt is the word w.cnt names.
+template <class G>
+__device__ __forceinline__ uint32_t coop_lf_nbr(const IdxArgs& ix, const uint8_t* slot, uint32_t b, uint32_t X,
+                                                uint32_t c, const uint32_t (&sx)[2 * G::K], uint32_t cnt, bool e,
+                                                bool prev)
+{
+  using C = CoopCfg<G>;
+  const int o = (int) (X - b * (uint32_t) G::D);
+  uint32_t pl[G::BMW];
+#pragma unroll
+  for (int k = 0; k < C::BC; ++k) {
+    const uint4 v = *reinterpret_cast<const uint4*>(slot + 16 * k);
+    pl[4 * k] = v.x; pl[4 * k + 1] = v.y; pl[4 * k + 2] = v.z; pl[4 * k + 3] = v.w;
+  }
+  uint32_t pop = 0;
+#pragma unroll
+  for (int w = 0; w < G::NB; ++w) {
+    uint32_t m = row_mask(o - 32 * w);
+    if constexpr (G::TWO_SIDED) m = e ? ~m : m;
+    pop += __popc(m & select_rows<G::K>(&pl[w * G::PW], sx));
+  }
+  if (prev) {
+#pragma unroll
+    for (int k = 0; k < C::BC; ++k) {
+      const uint4 v = *reinterpret_cast<const uint4*>(slot + 16 * (C::BC + k));
+      pl[4 * k] = v.x; pl[4 * k + 1] = v.y; pl[4 * k + 2] = v.z; pl[4 * k + 3] = v.w;
+    }
+#pragma unroll
+    for (int w = 0; w < G::NB; ++w) pop += __popc(select_rows<G::K>(&pl[w * G::PW], sx));
+    return finish_prev<G>(ix, cnt, pop, b, c, X);
+  }
   return finish<G>(ix, cnt, pop, b, c, X, e);
 }
 
@@ -239,10 +280,37 @@ __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, 
         sbL = ix.sb[(uint64_t) (bl >> S) * G::NC + c];
         sbR = ix.sb[(uint64_t) (br >> S) * G::NC + c];
       }
+      bool eL = false, eR = false, pL = false, pR = false;
+      if constexpr (C::NBR) {   // each end's counter word, loaded by its own lane
+        Where<G> wL = locate<G>(ix, bl, c);
+        line_local_prev<G>(ix, bl, c, wL);
+        eL = wL.e;
+        pL = wL.prev;
+        sbL = ld1<false>(wL.cnt);
+        if (needR) {
+          Where<G> wR = locate<G>(ix, br, c);
+          line_local_prev<G>(ix, br, c, wR);
+          eR = wR.e;
+          pR = wR.prev;
+          sbR = ld1<false>(wR.cnt);
+        }
+      }
       const uint32_t rounds = (nreq + C::RPR - 1) / C::RPR;
       for (uint32_t r = 0; r < rounds; ++r) {
         const uint32_t s = r * C::RPR + g;
-        if (s < nreq && k <= C::BC) {
+        if constexpr (C::NBR) {
+          if (s < nreq && k < 2 * C::BC) {
+            const Desc desc = tab[s];
+            const uint32_t b = (uint32_t) (desc / (Desc) G::NC), cc = (uint32_t) (desc % (Desc) G::NC);
+            Where<G> w = locate<G>(ix, b, cc);
+            line_local_prev<G>(ix, b, cc, w);
+            if (k < C::BC || w.prev) {
+              const uint32_t* p = k < C::BC ? w.planes + 4 * k : w.pplanes + 4 * (k - C::BC);
+              __builtin_amdgcn_global_load_lds((const void*) p,
+                                               (__attribute__((address_space(3))) void*) (wl + r * 1024), 16, 0, 0);
+            }
+          }
+        } else if (s < nreq && k <= C::BC) {
           const Desc desc = tab[s];
           const uint32_t b = (uint32_t) (desc / (Desc) G::NC), cc = (uint32_t) (desc % (Desc) G::NC);
           const uint8_t* src = coop_chunk_addr<G>(ix, b, cc, k);
@@ -253,9 +321,15 @@ __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, 
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       uint32_t sx[2 * G::K];
       plane_xor<G::K>(c, sx);
-      const uint32_t nL = coop_lf<G>(ix, wl + lane * C::SLOT, bl, L, c, sx, sbL);
-      const uint32_t nR = coop_lf<G>(ix, wl + (needR ? slotR : (uint32_t) lane) * C::SLOT, br, R, c, sx,
-                                     needR ? sbR : sbL);
+      uint32_t nL, nR;
+      if constexpr (C::NBR) {
+        nL = coop_lf_nbr<G>(ix, wl + lane * C::SLOT, bl, L, c, sx, sbL, eL, pL);
+        nR = coop_lf_nbr<G>(ix, wl + (needR ? slotR : (uint32_t) lane) * C::SLOT, br, R, c, sx,
+                            needR ? sbR : sbL, needR ? eR : eL, needR ? pR : pL);
+      } else {
+        nL = coop_lf<G>(ix, wl + lane * C::SLOT, bl, L, c, sx, sbL);
+        nR = coop_lf<G>(ix, wl + (needR ? slotR : (uint32_t) lane) * C::SLOT, br, R, c, sx, needR ? sbR : sbL);
+      }
       L = nL;
       R = nR;
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

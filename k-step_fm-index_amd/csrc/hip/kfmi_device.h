@@ -85,8 +85,10 @@ struct Geo {
   // the reference's own layouts (tag 101 / 201), register-resident blocks: a
   // block whose counter lies past the 128-B line of its planes is counted
   // forward from the previous block's counter when that entry lies in the
-  // line (line_local_prev): one HBM line per LF where the layout allows it
-  static constexpr bool NEIGHBOR = (LAY == LAY_INTER || LAY == LAY_AC) && SMALL;
+  // line (line_local_prev): one HBM line per LF where the layout allows it --
+  // only where entry b-1 and block b's planes fit one 128-B line at all
+  // (BOFF + EW + BMW words: K=2 d=64 and K=1 d<=128)
+  static constexpr bool NEIGHBOR = (LAY == LAY_INTER || LAY == LAY_AC) && SMALL && BOFF + EW + BMW <= 32;
 };
 
 // Superblock shift of the packed layout: the largest S with (2^S - 1) * d <= 65535.
@@ -121,13 +123,16 @@ struct IdxArgs {
   // bases m-1 .. m-rem at bits 0-1 ..), the start of their K-steps; null = rem 0
   const uint2* __restrict__ rtab;
   uint32_t rem;
-  // task kernels: per-lane index gathers issued as 4 exec-masked groups of 16
-  // lanes (4: every task kernel; 2: the fused m <= 128 kernel only; 1: none).
-  // A wave instruction whose 64 lanes hit 64 pages of a table beyond the
-  // translation reach (~3.5 GB) stalls on translation; 16 pages per
-  // instruction do not (profiles/r02/gather_mask_r2ag.jsonl)
+  // task kernels: per-lane index gathers issued as exec-masked lane groups
+  // (split_for, kfmi_search.hip: 4, 2 or 1 requested; launch_task picks the
+  // fetch form).  A wave instruction whose 64 lanes hit 64 pages of a table
+  // beyond the translation reach (~3.5 GB) stalls on translation; 16-32 pages
+  // per instruction do not (profiles/r02/gather_mask_r2ag.jsonl)
   uint32_t split;
 };
+
+// IdxArgs::split: KFMI_SPLIT forced this form (no per-geometry choice)
+#define KFMI_SPLIT_FORCED 0x100u
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 typedef unsigned int v2u __attribute__((ext_vector_type(2)));
@@ -192,8 +197,11 @@ __device__ __forceinline__ void row_codes(const uint8_t* __restrict__ base, uint
 {
   const uint32_t* a = reinterpret_cast<const uint32_t*>(base + (off & ~3ull));
   const uint32_t sh = (uint32_t) (off & 3u);
+  /* zeros written in place: as plain `cw[k] = 0` the compiler hoists MAXW
+   * zero registers out of the staging loop and keeps them live beside the
+   * working copy (MAXW = 16: 100 VGPRs, 5 waves/SIMD; this way 62, 8) */
 #pragma unroll
-  for (int k = 0; k < MAXW; ++k) cw[k] = 0;
+  for (int k = 0; k < MAXW; ++k) asm volatile("v_mov_b32 %0, 0" : "=v"(cw[k]));
   const uint32_t ng = m >> 2, rem = m & 3u;
   uint32_t lo = a[0];
 #pragma unroll 8
@@ -433,6 +441,21 @@ __device__ __forceinline__ uint32_t finish(const IdxArgs& ix, uint32_t cnt, uint
   return cnt + bc;
 }
 
+// line_local_prev's step: cnt = cnt_{b-1}[c], pop = rows of code c in block b-1
+// and in rows [start(b), X) of block b; '$' rows of both blocks below X excluded
+template <class G>
+__device__ __forceinline__ uint32_t finish_prev(const IdxArgs& ix, uint32_t cnt, uint32_t pop, uint32_t b,
+                                               uint32_t c, uint32_t X)
+{
+  int corr = 0;
+#pragma unroll
+  for (int s = 0; s < G::K; ++s)
+    corr += ((ix.dl.dblk[s] == b || ix.dl.dblk[s] + 1u == b) && ix.dl.dbase[s] == c && X > ix.dl.dpos[s]) ? 1 : 0;
+  const uint32_t v = cnt + pop - (uint32_t) corr;
+  if constexpr (G::ACRULE) return ac_clamp<G>(ix, v);
+  return v;
+}
+
 // LAY_MIDAC, block b >= E-1: the AltCounters searcher's step
 // (fmIndexCPUBaseline-AltCounters.c:218-303) from what the MID step already
 // has -- its popcount over the MID direction (pop_mid; forward for odd b,
@@ -529,14 +552,7 @@ __device__ __forceinline__ uint32_t lf_from_block(const IdxArgs& ix, const Blk<G
     if (k.prev) {   /* forward from cnt_{b-1}: all of block b-1, then rows [start(b), X) of block b */
 #pragma unroll
       for (int w = 0; w < G::NB; ++w) pop += __popc(select_rows<G::K>(&k.bp[w * G::PW], sx));
-      int corr = 0;
-#pragma unroll
-      for (int s = 0; s < G::K; ++s)
-        corr += ((ix.dl.dblk[s] == k.b || ix.dl.dblk[s] + 1u == k.b) && ix.dl.dbase[s] == c && X > ix.dl.dpos[s]) ? 1
-                                                                                                                 : 0;
-      const uint32_t v = k.cnt + pop - (uint32_t) corr;
-      if constexpr (G::ACRULE) return ac_clamp<G>(ix, v);
-      return v;
+      return finish_prev<G>(ix, k.cnt, pop, k.b, c, X);
     }
   }
   return finish<G>(ix, k.cnt, pop, k.b, c, X, k.e);

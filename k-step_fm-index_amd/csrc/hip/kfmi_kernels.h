@@ -41,6 +41,145 @@ __device__ __forceinline__ void fetch_ends(const IdxArgs& ix, const uint32_t (&L
   }
 }
 
+/* Issue-all-then-wait fetch for 32-byte, 16-byte-aligned plane blocks (K=2
+ * d=64, K=1 d=128) with one u32 counter word: every load of both ends from ONE
+ * asm block that sets exec per lane group and per condition (R only where its
+ * block differs from L's, block b-1's planes only where line_local_prev chose
+ * them), then a single vmcnt(0).  Written in C++ (fetch_ends) the compiler
+ * copies block(L) into block(R) before R's loads issue -- a wait for L's
+ * data -- so the two ends' lines are never in flight together.
+ * A part no lane of a group needs (R where every R shares L's block, the
+ * b-1 planes where no lane counts forward) is branched over.  Forms (the
+ * SPLIT template value): 8 = one group, 7 = two 32-lane groups (32 pages per
+ * instruction at most), 6 = four 16-lane groups.  3 Gbase, 10M x 100 bp,
+ * against the C++ four-group split (profiles/r03/sweep_r3n.jsonl): task (tag
+ * 101, 4.5 GB) 12.52 -> 10.93 ms with 7 (6: 11.28, 8: 16.11 -- past the
+ * translation reach one group stalls); task-ac (tag 201, 3 GB) 11.47 ->
+ * 9.51 (8: 9.79); task-mid 9.46 -> 9.40; 150 bp task-ac 17.01 -> 14.43,
+ * task-mid 14.41 -> 14.34.  Issuing every part unconditionally, empty exec
+ * or not, cost 15-19 % on task / task-ac (sweep_r3m.jsonl): an instruction
+ * with no active lane still takes its issue slot.
+ */
+template <class G>
+struct X4 {
+  static constexpr bool OK = G::SMALL && G::BMW == 8 && G::LAY != LAY_PACKED && G::BOFF % 4 == 0 && G::EW % 4 == 0;
+};
+
+#define KFMI_X4_BODY(T)                                      \
+  "s_and_b64 exec, %[sv], %[gm]\n"                           \
+  "global_load_dwordx4 %[l0], %[al], off\n"                  \
+  "global_load_dwordx4 %[l1], %[al], off offset:16\n"        \
+  "global_load_dword %[cl], %[acl], off\n"                   \
+  KFMI_X4_PREV_L(T)                                          \
+  "s_and_b64 exec, %[sv], %[gm]\n"                           \
+  "s_and_b64 exec, exec, %[nr]\n"                            \
+  KFMI_X4_SJ("r" T)                                          \
+  "global_load_dwordx4 %[r0], %[ar], off\n"                  \
+  "global_load_dwordx4 %[r1], %[ar], off offset:16\n"        \
+  "global_load_dword %[cr], %[acr], off\n"                   \
+  KFMI_X4_PREV_R(T)                                          \
+  KFMI_X4_SL("r" T)
+#define KFMI_X4_G1 "s_mov_b64 %[gm], -1\n" KFMI_X4_BODY("a")
+#define KFMI_X4_G2 "s_bfm_b64 %[gm], 32, 0\n" KFMI_X4_BODY("a") "s_bfm_b64 %[gm], 32, 32\n" KFMI_X4_BODY("b")
+#define KFMI_X4_G4                                                                          \
+  "s_bfm_b64 %[gm], 16, 0\n" KFMI_X4_BODY("a") "s_bfm_b64 %[gm], 16, 16\n" KFMI_X4_BODY("b") \
+  "s_bfm_b64 %[gm], 16, 32\n" KFMI_X4_BODY("c") "s_bfm_b64 %[gm], 16, 48\n" KFMI_X4_BODY("d")
+#define KFMI_X4_ASM(GROUPS) "s_mov_b64 %[sv], exec\n" GROUPS "s_mov_b64 exec, %[sv]\ns_waitcnt vmcnt(0)\n"
+#define KFMI_X4_OUT                                                                                          \
+  [l0] "=&v"(l0), [l1] "=&v"(l1), [r0] "=&v"(r0), [r1] "=&v"(r1), [cl] "=&v"(cl), [cr] "=&v"(cr), [sv] "=&s"(sv), \
+      [gm] "=&s"(gm)
+#define KFMI_X4_IN [al] "v"(wl.planes), [acl] "v"(wl.cnt), [ar] "v"(wr.planes), [acr] "v"(wr.cnt), [nr] "s"(nr)
+#define KFMI_X4_OUTP KFMI_X4_OUT, [p0] "=&v"(p0), [p1] "=&v"(p1), [q0] "=&v"(q0), [q1] "=&v"(q1)
+#define KFMI_X4_INP KFMI_X4_IN, [pl] "s"(pl), [pr] "s"(pr), [po0] "i"(PO), [po1] "i"(PO + 16)
+/* empty-exec skips: a branch over a part no lane of the group needs */
+#define KFMI_X4_SJ(L) "s_cbranch_execz .Lx4" L "_%=\n"
+#define KFMI_X4_SL(L) ".Lx4" L "_%=:\n"
+#define KFMI_X4_PREV_L_ON(T)                                 \
+  "s_and_b64 exec, exec, %[pl]\n"                            \
+  KFMI_X4_SJ("p" T)                                          \
+  "global_load_dwordx4 %[p0], %[al], off offset:%[po0]\n"    \
+  "global_load_dwordx4 %[p1], %[al], off offset:%[po1]\n"    \
+  KFMI_X4_SL("p" T)
+#define KFMI_X4_PREV_R_ON(T)                                 \
+  "s_and_b64 exec, exec, %[pr]\n"                            \
+  KFMI_X4_SJ("r" T)                                          \
+  "global_load_dwordx4 %[q0], %[ar], off offset:%[po0]\n"    \
+  "global_load_dwordx4 %[q1], %[ar], off offset:%[po1]\n"
+
+template <class G, int SPLIT>
+__device__ __forceinline__ void fetch_ends_x4(const IdxArgs& ix, uint32_t L, uint32_t R, uint32_t c, Blk<G>& kl,
+                                              Blk<G>& kr)
+{
+  static_assert(SPLIT >= 6 && SPLIT <= 8, "fetch form: 6, 7, 8 = four, two, one lane group(s)");
+  const uint32_t bl = L / (uint32_t) G::D, br = R / (uint32_t) G::D;
+  Where<G> wl = locate<G>(ix, bl, c);
+  Where<G> wr = locate<G>(ix, br, c);
+  line_local_prev<G>(ix, bl, c, wl);
+  line_local_prev<G>(ix, br, c, wr);
+  const bool needR = br != bl;
+  const uint64_t nr = __ballot(needR);
+  v4u l0, l1, r0, r1;
+  uint32_t cl, cr;
+  uint64_t sv, gm;
+  if constexpr (G::NEIGHBOR) {
+    const uint64_t pl = __ballot(wl.prev), pr = __ballot(wr.prev);
+    constexpr int PO = -4 * G::EW;   /* block b-1's planes, relative to block b's */
+    v4u p0, p1, q0, q1;
+#define KFMI_X4_PREV_L(T) KFMI_X4_PREV_L_ON(T)
+#define KFMI_X4_PREV_R(T) KFMI_X4_PREV_R_ON(T)
+    if constexpr (SPLIT == 8)
+      asm volatile(KFMI_X4_ASM(KFMI_X4_G1) : KFMI_X4_OUTP : KFMI_X4_INP : "memory", "scc");
+    else if constexpr (SPLIT == 7)
+      asm volatile(KFMI_X4_ASM(KFMI_X4_G2) : KFMI_X4_OUTP : KFMI_X4_INP : "memory", "scc");
+    else
+      asm volatile(KFMI_X4_ASM(KFMI_X4_G4) : KFMI_X4_OUTP : KFMI_X4_INP : "memory", "scc");
+#undef KFMI_X4_PREV_L
+#undef KFMI_X4_PREV_R
+    const v4u pa = needR ? q0 : p0, pb = needR ? q1 : p1;
+    kl.bp[0] = p0.x; kl.bp[1] = p0.y; kl.bp[2] = p0.z; kl.bp[3] = p0.w;
+    kl.bp[4] = p1.x; kl.bp[5] = p1.y; kl.bp[6] = p1.z; kl.bp[7] = p1.w;
+    kr.bp[0] = pa.x; kr.bp[1] = pa.y; kr.bp[2] = pa.z; kr.bp[3] = pa.w;
+    kr.bp[4] = pb.x; kr.bp[5] = pb.y; kr.bp[6] = pb.z; kr.bp[7] = pb.w;
+  } else {
+#define KFMI_X4_PREV_L(T)
+#define KFMI_X4_PREV_R(T)
+    if constexpr (SPLIT == 8)
+      asm volatile(KFMI_X4_ASM(KFMI_X4_G1) : KFMI_X4_OUT : KFMI_X4_IN : "memory", "scc");
+    else if constexpr (SPLIT == 7)
+      asm volatile(KFMI_X4_ASM(KFMI_X4_G2) : KFMI_X4_OUT : KFMI_X4_IN : "memory", "scc");
+    else
+      asm volatile(KFMI_X4_ASM(KFMI_X4_G4) : KFMI_X4_OUT : KFMI_X4_IN : "memory", "scc");
+#undef KFMI_X4_PREV_L
+#undef KFMI_X4_PREV_R
+  }
+  const v4u ra = needR ? r0 : l0, rb = needR ? r1 : l1;
+  kl.bm[0] = l0.x; kl.bm[1] = l0.y; kl.bm[2] = l0.z; kl.bm[3] = l0.w;
+  kl.bm[4] = l1.x; kl.bm[5] = l1.y; kl.bm[6] = l1.z; kl.bm[7] = l1.w;
+  kr.bm[0] = ra.x; kr.bm[1] = ra.y; kr.bm[2] = ra.z; kr.bm[3] = ra.w;
+  kr.bm[4] = rb.x; kr.bm[5] = rb.y; kr.bm[6] = rb.z; kr.bm[7] = rb.w;
+  kl.cnt = cl;
+  kr.cnt = needR ? cr : cl;
+  kl.b = bl;
+  kr.b = br;
+  kl.e = wl.e;
+  kr.e = wr.e;
+  kl.prev = wl.prev;
+  kr.prev = wr.prev;
+}
+#undef KFMI_X4_BODY
+#undef KFMI_X4_G1
+#undef KFMI_X4_G2
+#undef KFMI_X4_G4
+#undef KFMI_X4_ASM
+#undef KFMI_X4_OUT
+#undef KFMI_X4_IN
+#undef KFMI_X4_OUTP
+#undef KFMI_X4_INP
+#undef KFMI_X4_SJ
+#undef KFMI_X4_SL
+#undef KFMI_X4_PREV_L_ON
+#undef KFMI_X4_PREV_R_ON
+
 /* SPLIT > 1: the same loads as SPLIT exec-masked groups of 64/SPLIT lanes, so
  * one wave instruction touches at most 64/SPLIT pages (IdxArgs::split). */
 template <class G, bool NT, int QPT, int SPLIT>
@@ -48,12 +187,14 @@ __device__ __forceinline__ void fetch_ends_split(const IdxArgs& ix, const uint32
                                                  const uint32_t (&R)[QPT], const uint32_t (&c)[QPT],
                                                  Blk<G> (&kl)[QPT], Blk<G> (&kr)[QPT])
 {
-  if constexpr (SPLIT == 1) {
+  if constexpr (SPLIT >= 6 && !NT && QPT == 1 && X4<G>::OK) {
+    fetch_ends_x4<G, SPLIT>(ix, L[0], R[0], c[0], kl[0], kr[0]);
+  } else if constexpr (SPLIT == 1) {
     fetch_ends<G, NT, QPT>(ix, L, R, c, kl, kr);
-  } else {
-    const int grp = (int) (threadIdx.x & 63) / (64 / SPLIT);
+  } else {   /* 4 (and 6-8 where the asm form does not apply): four 16-lane groups */
+    const int grp = (int) (threadIdx.x & 63) / 16;
 #pragma unroll
-    for (int g = 0; g < SPLIT; ++g)
+    for (int g = 0; g < 4; ++g)
       if (grp == g) fetch_ends<G, NT, QPT>(ix, L, R, c, kl, kr);
   }
 }
@@ -226,10 +367,14 @@ __global__ __launch_bounds__(256) void task_sorted_kernel(IdxArgs ix, const uint
       plane_xor<G::K>(c, sx);
       if constexpr (G::SMALL) {
         Blk<G> kl, kr;
-        fetch_block<G>(ix, L / (uint32_t) G::D, c, kl);
-        const uint32_t br = R / (uint32_t) G::D;
-        if (br != kl.b) fetch_block<G>(ix, br, c, kr);
-        else kr = kl;
+        if constexpr (X4<G>::OK) {
+          fetch_ends_x4<G, 8>(ix, L, R, c, kl, kr);
+        } else {
+          fetch_block<G>(ix, L / (uint32_t) G::D, c, kl);
+          const uint32_t br = R / (uint32_t) G::D;
+          if (br != kl.b) fetch_block<G>(ix, br, c, kr);
+          else kr = kl;
+        }
         L = lf_from_block<G>(ix, kl, L, c, sx);
         R = lf_from_block<G>(ix, kr, R, c, sx);
       } else {
@@ -391,7 +536,22 @@ static hipError_t launch_task(const SearchLaunch& a)
 {
   /* the split only exists for the one-line-per-block path (d <= 128 at K=2) */
   if constexpr (G::SMALL) {
-    if (a.ix.split == 4 || (a.ix.split == 2 && a.maxw == 8)) {
+    const uint32_t want = a.ix.split & ~KFMI_SPLIT_FORCED;
+    if (a.ix.split & KFMI_SPLIT_FORCED) {   /* KFMI_SPLIT: the form as given */
+      switch (want) {
+        case 4: launch_task_split<G, 4>(a); return hipGetLastError();
+        case 6: launch_task_split<G, 6>(a); return hipGetLastError();
+        case 7: launch_task_split<G, 7>(a); return hipGetLastError();
+        case 8: launch_task_split<G, 8>(a); return hipGetLastError();
+        default: launch_task_split<G, 1>(a); return hipGetLastError();
+      }
+    }
+    if constexpr (X4<G>::OK) {   /* asm fetch: two groups on split tables, else one */
+      if (want == 1) launch_task_split<G, 8>(a);
+      else launch_task_split<G, 7>(a);
+      return hipGetLastError();
+    }
+    if (want == 4 || (want == 2 && a.maxw == 8)) {
       launch_task_split<G, 4>(a);
       return hipGetLastError();
     }

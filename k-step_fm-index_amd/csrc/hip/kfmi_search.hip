@@ -1009,9 +1009,12 @@ int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx, kfmi_dev_
   return KFMI_SUCCESS;
 }
 
-/* Gather split for the per-lane (task) kernels (IdxArgs::split): 4 = every
- * task kernel issues its index gathers as 4 exec-masked groups of 16 lanes;
- * 2 = only the fused kernel for reads of <= 128 bases; 1 = none.
+/* Gather split for the per-lane (task) kernels (IdxArgs::split): how many
+ * exec-masked lane groups issue each step's index gathers (launch_task,
+ * kfmi_kernels.h, turns it into a fetch form per geometry).  Auto values:
+ * 4 = every task kernel splits; 2 = only the fused kernel for reads of <= 128
+ * bases, except where the asm fetch (fetch_ends_x4) applies, which splits
+ * in two groups whenever this is 2 or 4; 1 = none.
  *  - tables over 3.5 GB: 4.  Past the translation reach the per-instruction
  *    page cliff costs up to 2.7x (task-grp 96 GB: 17.6 -> 6.8 ms at 100 bp,
  *    25.1 -> 9.1 at 150 bp; task-ac128 6.4 GB: 18.1 -> 10.0, 26.1 -> 15.5);
@@ -1019,13 +1022,19 @@ int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx, kfmi_dev_
  *    100 bp, but 14.41 -> 14.83 ms with the 16-word kernel at 150 bp);
  *  - 2-3.5 GB, other layouts: 4 (task-ac 12.87 -> 11.81 at 100 bp,
  *    18.93 -> 17.94 at 150 bp; task-packed 14.0 -> 13.3).
- * profiles/r02/sweep_split_r2ah.jsonl, sweep_split150_r2aj.jsonl.  The ftab
- * lookup (one gather per read) is never split: that measured slower.
- * KFMI_SPLIT=1|4 forces it. */
+ * profiles/r02/sweep_split_r2ah.jsonl, sweep_split150_r2aj.jsonl; the asm
+ * forms: profiles/r03/sweep_r3n.jsonl, sweep150_r3n.jsonl.  The ftab lookup
+ * (one gather per read) is never split: that measured slower.
+ * KFMI_SPLIT forces a form (KFMI_SPLIT_FORCED set): 1 / 4 = the C++ fetch in
+ * one / four groups, 6 / 7 / 8 = the asm fetch in four / two / one group(s)
+ * where it applies. */
 static uint32_t split_for(uint64_t table_bytes, int layout)
 {
   const char* e = getenv("KFMI_SPLIT");
-  if (e && *e) return atoi(e) == 4 ? 4u : 1u;
+  if (e && *e) {
+    const int v = atoi(e);
+    return KFMI_SPLIT_FORCED | ((v == 4 || (v >= 6 && v <= 8)) ? (uint32_t) v : 1u);
+  }
   if (table_bytes > 3500000000ull) return 4u;
   if (table_bytes > 2000000000ull) return (layout == LAY_MID || layout == LAY_MIDAC) ? 2u : 4u;
   return 1u;

@@ -84,7 +84,7 @@ def random_index(kfmi_mod):
     rng = np.random.default_rng(2026)
     text = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), size=3_000_001).tobytes()
     return text, {(k, d): kfmi_mod.Index.build(text, k=k, d=d) for k, d in
-                  [(2, 64), (1, 64), (2, 192), (2, 448), (2, 960), (1, 32), (2, 128), (2, 256)]}
+                  [(2, 64), (1, 64), (2, 192), (2, 448), (2, 960), (1, 32), (2, 128), (2, 256), (1, 128)]}
 
 
 def _reads(text, n, m, seed):
@@ -97,7 +97,8 @@ def _reads(text, n, m, seed):
 
 
 @pytest.mark.parametrize("backend", PLAIN + ALT)
-@pytest.mark.parametrize("kd", [(2, 64), (1, 64), (2, 192), (2, 448), (2, 960), (1, 32), (2, 128), (2, 256)],
+@pytest.mark.parametrize("kd", [(2, 64), (1, 64), (2, 192), (2, 448), (2, 960), (1, 32), (2, 128), (2, 256),
+                                (1, 128)],
                          ids=lambda kd: f"k{kd[0]}d{kd[1]}")
 def test_backend_matches_oracle_random(gpu, oracle_mod, random_index, backend, kd):
     text, idxs = random_index
@@ -316,17 +317,20 @@ def test_ac_tail_blocks(gpu, oracle_mod, n, tail):
                     assert np.array_equal(gpu.search_array(idx, q, b), want), (n, tail, k, d, m, b, defined)
 
 
+@pytest.mark.parametrize("split", ["4", "6", "7", "8"])
 @pytest.mark.parametrize("backend", ["task-mid", "task", "task-packed", "task-ac", "task-ac128", "task-ac-mid"])
-def test_split_gathers_equal_oracle(gpu, oracle_mod, random_index, backend, monkeypatch):
-    """KFMI_SPLIT=4 (per-lane gathers as 4 exec-masked groups of 16 lanes, the
-    default for index tables over 2 GB) forced on small indexes:
+def test_split_gathers_equal_oracle(gpu, oracle_mod, random_index, backend, split, monkeypatch):
+    """Every gather form forced on small indexes (split tables take
+    the asm fetch in two groups, 7, where it applies, else the C++ fetch in
+    four 16-lane groups, 4; 6 / 8 are the asm fetch in four groups / one):
     the same results as the oracle, incl. partial last waves (n % 64 != 0),
     reads with m % K != 0 (remainder table), fused and pack-kernel reads, and
-    the ftab jump start.  d = 192 has no split path (lf_stream) and must be
-    unaffected."""
+    the ftab jump start.  Geometries without the asm form (K=1 d=64, the
+    packed layout, d = 128 at K=2) take the C++ four-group fetch under 6-8;
+    d = 192 has no split path (lf_stream) and must be unaffected."""
     text, idxs = random_index
-    monkeypatch.setenv("KFMI_SPLIT", "4")
-    for k, d in ((2, 64), (1, 64), (1, 32), (2, 128), (2, 192)):
+    monkeypatch.setenv("KFMI_SPLIT", split)
+    for k, d in ((2, 64), (1, 64), (1, 32), (1, 128), (2, 128), (2, 192)):
         idx = idxs[(k, d)]
         if not coop_supported(backend, k, d):
             continue
