@@ -281,19 +281,19 @@ __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, 
         sbR = ix.sb[(uint64_t) (br >> S) * G::NC + c];
       }
       bool eL = false, eR = false, pL = false, pR = false;
-      if constexpr (C::NBR) {   // each end's counter word, loaded by its own lane
+      const uint32_t* acL = nullptr;
+      const uint32_t* acR = nullptr;
+      if constexpr (C::NBR) {   // each end's counter word, loaded by its own lane after the DMA
         Where<G> wL = locate<G>(ix, bl, c);
+        Where<G> wR = locate<G>(ix, br, c);
         line_local_prev<G>(ix, bl, c, wL);
+        line_local_prev<G>(ix, br, c, wR);
         eL = wL.e;
         pL = wL.prev;
-        sbL = ld1<false>(wL.cnt);
-        if (needR) {
-          Where<G> wR = locate<G>(ix, br, c);
-          line_local_prev<G>(ix, br, c, wR);
-          eR = wR.e;
-          pR = wR.prev;
-          sbR = ld1<false>(wR.cnt);
-        }
+        acL = wL.cnt;
+        eR = wR.e;
+        pR = wR.prev;
+        acR = wR.cnt;
       }
       const uint32_t rounds = (nreq + C::RPR - 1) / C::RPR;
       for (uint32_t r = 0; r < rounds; ++r) {
@@ -318,7 +318,35 @@ __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, 
                                            (__attribute__((address_space(3))) void*) (wl + r * 1024), 16, 0, 0);
         }
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if constexpr (C::NBR) {
+        /* the two counter words, after the DMA (their lines are then already
+         * requested), as two exec-masked 32-lane groups (32 pages per
+         * instruction at most, as the task kernels' fetch_ends_x4), R only
+         * where it has its own block; one vmcnt(0) for all */
+        uint64_t sv, gm;
+        asm volatile("s_mov_b64 %[sv], exec\n"
+                     "s_bfm_b64 %[gm], 32, 0\n"
+                     "s_and_b64 exec, %[sv], %[gm]\n"
+                     "global_load_dword %[cl], %[al], off\n"
+                     "s_and_b64 exec, exec, %[nr]\n"
+                     "s_cbranch_execz .Lcc0_%=\n"
+                     "global_load_dword %[cr], %[ar], off\n"
+                     ".Lcc0_%=:\n"
+                     "s_bfm_b64 %[gm], 32, 32\n"
+                     "s_and_b64 exec, %[sv], %[gm]\n"
+                     "global_load_dword %[cl], %[al], off\n"
+                     "s_and_b64 exec, exec, %[nr]\n"
+                     "s_cbranch_execz .Lcc1_%=\n"
+                     "global_load_dword %[cr], %[ar], off\n"
+                     ".Lcc1_%=:\n"
+                     "s_mov_b64 exec, %[sv]\n"
+                     "s_waitcnt vmcnt(0)\n"
+                     : [cl] "=&v"(sbL), [cr] "=&v"(sbR), [sv] "=&s"(sv), [gm] "=&s"(gm)
+                     : [al] "v"(acL), [ar] "v"(acR), [nr] "s"(mask)
+                     : "memory", "scc");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
       uint32_t sx[2 * G::K];
       plane_xor<G::K>(c, sx);
       uint32_t nL, nR;
