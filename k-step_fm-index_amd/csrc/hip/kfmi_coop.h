@@ -30,6 +30,8 @@ namespace kfmi {
 // step is counted forward from entry b-1, block b-1's -- and the lane owning
 // the interval end loads its one counter word itself (same 128-B line, merged
 // in L2 with the DMA's request), so no request needs a second line's chunk.
+__host__ __device__ constexpr int ilog2(int x) { int l = 0; while ((1 << (l + 1)) <= x) ++l; return l; }
+
 template <class G>
 struct CoopCfg {
   static constexpr int BC = G::BMW / 4;                 // 16-byte bitmap chunks per block
@@ -38,8 +40,22 @@ struct CoopCfg {
   static constexpr int RPR = 64 / TPR;                  // requests per round
   static constexpr int SLOT = TPR * 16;                 // LDS bytes per request slot
   static constexpr int MAXREQ = 128;                    // 64 L + up to 64 R
+  static constexpr int MAXR = MAXREQ / RPR;             // staging rounds per K-step, at most
   using Desc = typename std::conditional<(G::NC > 16), uint64_t, uint32_t>::type;   // b * NC + c
-  static constexpr int WAVE_LDS = MAXREQ * SLOT + MAXREQ * (int) sizeof(Desc);
+  // Line geometries (one power-of-two line holds a request's planes and its
+  // counter chunk): a request is posted as its line's address with the planes'
+  // and the counter's 16-byte chunk numbers in the low bits (LCB bits each)
+  static constexpr int LINEB = G::EW * 4;
+  static constexpr int LCB = ilog2(LINEB > 16 ? LINEB / 16 : 1);
+  static constexpr bool LINE = !NBR && (G::MIDLINES || G::LAY == LAY_GRP || G::LAY == LAY_AC128) &&
+                               (LINEB & (LINEB - 1)) == 0 && LINEB >= 64 && 2 * LCB <= ilog2(LINEB);
+  // Pre-addressed issue (IdxArgs::coop_issue): each lane posts its own ends'
+  // addresses (64-bit) and the staging rounds only read them back -- all of a
+  // step's table reads in flight together instead of a read, a decode and a
+  // wait per round
+  static constexpr bool PRE = NBR || LINE;
+  static constexpr int TABB = PRE ? 8 : (int) sizeof(Desc);
+  static constexpr int WAVE_LDS = MAXREQ * SLOT + MAXREQ * TABB;
   static constexpr int WPB0 = 65536 / WAVE_LDS;
   static constexpr int WPB = WPB0 < 1 ? 1 : (WPB0 > 4 ? 4 : WPB0);   // waves per block
   static constexpr bool OK = (G::BMW % 4 == 0) && (G::EW % 4 == 0) && (G::BOFF % 4 == 0) &&
@@ -78,6 +94,32 @@ __device__ __forceinline__ const uint8_t* coop_chunk_addr(const IdxArgs& ix, uin
   } else {
     return base + eb + 4 * G::BMW + 2 * (c & ~7u);
   }
+}
+
+// LINE geometries: request (b, c) as its line's address | planes chunk |
+// counter chunk << LCB (chunk numbers within the line, as coop_chunk_addr)
+template <class G>
+__device__ __forceinline__ uint64_t coop_line_post(const IdxArgs& ix, uint32_t b, uint32_t c)
+{
+  using C = CoopCfg<G>;
+  const uint8_t* base = reinterpret_cast<const uint8_t*>(ix.ent);
+  uint64_t lb;
+  uint32_t p0, cc;
+  if constexpr (G::MIDLINES) {
+    lb = (uint64_t) (b >> 1) * C::LINEB;
+    p0 = (b & 1u) * (G::BMW / 4);
+    cc = (G::MIDCNT + (c & ~3u)) / 4;
+  } else if constexpr (G::LAY == LAY_GRP) {
+    lb = ((uint64_t) b * G::NGRP + c / G::NCG) * C::LINEB;
+    p0 = 0;
+    cc = (G::BMW + ((c % G::NCG) & ~3u)) / 4;
+  } else {   // LAY_AC128
+    lb = (uint64_t) b * C::LINEB;
+    p0 = 0;
+    const bool e = ((b & 1u) != 0) == (c < (uint32_t) G::HALF);
+    cc = (G::BMW + (e ? G::HALF : 0) + ((c & (G::HALF - 1)) & ~3u)) / 4;
+  }
+  return reinterpret_cast<uint64_t>(base + lb) | p0 | ((uint64_t) cc << C::LCB);
 }
 
 template <class G>
@@ -196,6 +238,8 @@ __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, 
   uint8_t* wl = lds + wave * C::WAVE_LDS;
   using Desc = typename C::Desc;
   Desc* tab = reinterpret_cast<Desc*>(wl + C::MAXREQ * C::SLOT);
+  uint64_t* post = reinterpret_cast<uint64_t*>(wl + C::MAXREQ * C::SLOT);   // PRE: request addresses
+  const bool pre = C::PRE && ix.coop_issue != 0;                            // wave-uniform
   const uint64_t q0 = ((uint64_t) blockIdx.x * C::WPB + wave) * 64;
   if (q0 >= num) return;                       // whole wave idle (wave-uniform)
   const uint64_t q = q0 + lane;
@@ -272,17 +316,10 @@ __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, 
       const uint32_t nreq = 64u + (uint32_t) __popcll(mask);
       const uint32_t slotR = 64u + __builtin_amdgcn_mbcnt_hi((uint32_t) (mask >> 32),
                                                              __builtin_amdgcn_mbcnt_lo((uint32_t) mask, 0u));
-      tab[lane] = (Desc) bl * (Desc) G::NC + c;
-      if (needR) tab[slotR] = (Desc) br * (Desc) G::NC + c;
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      uint32_t sbL = 0, sbR = 0;
-      if constexpr (G::LAY == LAY_PACKED) {
-        sbL = ix.sb[(uint64_t) (bl >> S) * G::NC + c];
-        sbR = ix.sb[(uint64_t) (br >> S) * G::NC + c];
-      }
       bool eL = false, eR = false, pL = false, pR = false;
       const uint32_t* acL = nullptr;
       const uint32_t* acR = nullptr;
+      uint64_t postL = 0, postR = 0;
       if constexpr (C::NBR) {   // each end's counter word, loaded by its own lane after the DMA
         Where<G> wL = locate<G>(ix, bl, c);
         Where<G> wR = locate<G>(ix, br, c);
@@ -294,9 +331,56 @@ __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, 
         eR = wR.e;
         pR = wR.prev;
         acR = wR.cnt;
+        postL = reinterpret_cast<uint64_t>(wL.planes) | (pL ? 1u : 0u);   // planes 16-B aligned
+        postR = reinterpret_cast<uint64_t>(wR.planes) | (pR ? 1u : 0u);
+      } else if constexpr (C::LINE) {
+        postL = coop_line_post<G>(ix, bl, c);
+        postR = coop_line_post<G>(ix, br, c);
+      }
+      if (pre) {
+        post[lane] = postL;
+        if (needR) post[slotR] = postR;
+      } else {
+        tab[lane] = (Desc) bl * (Desc) G::NC + c;
+        if (needR) tab[slotR] = (Desc) br * (Desc) G::NC + c;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      uint32_t sbL = 0, sbR = 0;
+      if constexpr (G::LAY == LAY_PACKED) {
+        sbL = ix.sb[(uint64_t) (bl >> S) * G::NC + c];
+        sbR = ix.sb[(uint64_t) (br >> S) * G::NC + c];
       }
       const uint32_t rounds = (nreq + C::RPR - 1) / C::RPR;
-      for (uint32_t r = 0; r < rounds; ++r) {
+      if constexpr (C::PRE) {
+        if (pre) {
+          /* every round's post read back at once, then the rounds' DMA issued
+           * back to back (requests s >= nreq of the last round masked off) */
+          uint64_t pe[C::MAXR];
+#pragma unroll
+          for (int r = 0; r < C::MAXR; ++r) pe[r] = post[r * C::RPR + g];
+#pragma unroll
+          for (int r = 0; r < C::MAXR; ++r) {
+            if ((uint32_t) r >= rounds) break;
+            const uint32_t s = (uint32_t) r * C::RPR + g;
+            const uint64_t e = pe[r];
+            const uint8_t* p = nullptr;
+            if constexpr (C::NBR) {
+              const uint8_t* pl = reinterpret_cast<const uint8_t*>(e & ~1ull);
+              if (k < C::BC) p = pl + 16 * k;
+              else if (k < 2 * C::BC && (e & 1u)) p = pl - G::EW * 4 + 16 * (k - C::BC);   // block b-1
+            } else {
+              const uint8_t* ln = reinterpret_cast<const uint8_t*>(e & ~(uint64_t) (C::LINEB - 1));
+              const uint32_t cm = (1u << C::LCB) - 1u;
+              if (k < C::BC) p = ln + 16 * (((uint32_t) e & cm) + k);
+              else if (k == C::BC) p = ln + 16 * (((uint32_t) (e >> C::LCB)) & cm);
+            }
+            if (s < nreq && p)
+              __builtin_amdgcn_global_load_lds((const void*) p,
+                                               (__attribute__((address_space(3))) void*) (wl + r * 1024), 16, 0, 0);
+          }
+        }
+      }
+      for (uint32_t r = 0; !pre && r < rounds; ++r) {
         const uint32_t s = r * C::RPR + g;
         if constexpr (C::NBR) {
           if (s < nreq && k < 2 * C::BC) {

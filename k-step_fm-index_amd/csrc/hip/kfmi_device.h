@@ -129,6 +129,9 @@ struct IdxArgs {
   // beyond the translation reach (~3.5 GB) stalls on translation; 16-32 pages
   // per instruction do not (profiles/r02/gather_mask_r2ag.jsonl)
   uint32_t split;
+  // coop kernels: 1 = pre-addressed staging rounds where the geometry allows
+  // (CoopCfg::PRE), 0 = each round decodes its request (KFMI_COOP_ISSUE)
+  uint32_t coop_issue;
 };
 
 // IdxArgs::split: KFMI_SPLIT forced this form (no per-geometry choice)

@@ -1057,6 +1057,8 @@ IdxArgs idx_args(const kfmi_dev_index* di)
   ix.rtab = nullptr;
   ix.rem = 0;
   ix.split = split_for(di->ent_bytes + di->sb_bytes, di->layout);
+  e = getenv("KFMI_COOP_ISSUE");   /* 0: coop staging rounds decode their requests */
+  ix.coop_issue = (e && *e) ? (uint32_t) (atoi(e) != 0) : 1u;
   return ix;
 }
 

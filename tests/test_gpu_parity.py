@@ -317,6 +317,40 @@ def test_ac_tail_blocks(gpu, oracle_mod, n, tail):
                     assert np.array_equal(gpu.search_array(idx, q, b), want), (n, tail, k, d, m, b, defined)
 
 
+@pytest.mark.parametrize("issue", ["1", "0"])
+@pytest.mark.parametrize("backend", ["coop", "coop-packed", "coop-mid", "coop-ac", "coop-ac128", "coop-ac-mid"])
+def test_coop_issue_forms_equal_oracle(gpu, oracle_mod, random_index, backend, issue, monkeypatch):
+    """Both staging-round forms of the coop kernel (KFMI_COOP_ISSUE, DESIGN 5
+    "Coop issue"): 1 = each lane posts its ends' line addresses and the rounds
+    read them back all at once (reference layouts at K=2 d=64 and the line
+    layouts MID/MIDAC/AC128; others keep the decoding rounds), 0 = every
+    round decodes its request.  Same results as the oracle, incl. partial
+    last waves, reads with m % K != 0, the pack kernel (m > 256) and the ftab
+    jump start."""
+    text, idxs = random_index
+    monkeypatch.setenv("KFMI_COOP_ISSUE", issue)
+    for k, d in ((2, 64), (1, 64), (1, 32), (1, 128), (2, 128), (2, 256)):
+        idx = idxs[(k, d)]
+        if not coop_supported(backend, k, d):
+            continue
+        ref_img = idx.alt_counters()[0].image() if backend in ALT else idx.image()
+        lens = [(100, 20011), (150, 3001), (2 * k, 999), (300, 517)]
+        if backend not in ALT:
+            lens.append((101, 1203))
+        for m, n in lens:
+            q = _reads(text, n, m, seed=m * 13 + k)
+            want, _ = oracle_mod.search(ref_img if m % k == 0 else idxs[(1, 64)].image(), q)
+            got = gpu.search_array(idx, q, backend)
+            assert np.array_equal(got, want), (backend, k, d, m)
+        if d == 64:
+            monkeypatch.setenv("KFMI_FTAB", str(4 * k))
+            q = _reads(text, 5003, 100, seed=19 + k)
+            want, _ = oracle_mod.search(ref_img, q)
+            got = gpu.search_array(idx, q, backend)
+            monkeypatch.delenv("KFMI_FTAB")
+            assert np.array_equal(got, want), (backend, k, d, "ftab")
+
+
 @pytest.mark.parametrize("split", ["4", "6", "7", "8"])
 @pytest.mark.parametrize("backend", ["task-mid", "task", "task-packed", "task-ac", "task-ac128", "task-ac-mid"])
 def test_split_gathers_equal_oracle(gpu, oracle_mod, random_index, backend, split, monkeypatch):
