@@ -26,10 +26,11 @@
 namespace kfmi {
 
 // NEIGHBOR geometries (reference tag-101/201 layouts, kfmi_device.h
-// line_local_prev): the DMA carries bit planes only -- block b's and, when the
-// step is counted forward from entry b-1, block b-1's -- and the lane owning
-// the interval end loads its one counter word itself (same 128-B line, merged
-// in L2 with the DMA's request), so no request needs a second line's chunk.
+// line_local_prev): a request's DMA carries block b's bit planes and either
+// the 16-byte chunk holding its counter word or, when the step is counted
+// forward from entry b-1, block b-1's planes -- whose counter word (same
+// 128-B line, merged in L2 with the DMA's request) the lane owning that
+// interval end then loads itself.  No request needs a second line's chunk.
 __host__ __device__ constexpr int ilog2(int x) { int l = 0; while ((1 << (l + 1)) <= x) ++l; return l; }
 
 template <class G>
@@ -94,6 +95,21 @@ __device__ __forceinline__ const uint8_t* coop_chunk_addr(const IdxArgs& ix, uin
   } else {
     return base + eb + 4 * G::BMW + 2 * (c & ~7u);
   }
+}
+
+// NEIGHBOR geometries: request (b, c) as block b's planes address (below
+// 2^48, checked on the host: IdxArgs::coop_issue), bit 48 = counted forward
+// from block b-1, bits 56-63 = the counter chunk's signed offset from the
+// planes in 16-byte chunks (INTER: 2 .. 5, AC: -2 .. 3)
+static constexpr uint64_t NBR_ADDR = (1ull << 48) - 1;
+
+template <class G>
+__device__ __forceinline__ uint64_t nbr_post(const Where<G>& w)
+{
+  const int64_t off = ((int64_t) (reinterpret_cast<uintptr_t>(w.cnt) & ~(uintptr_t) 15) -
+                       (int64_t) reinterpret_cast<uintptr_t>(w.planes)) >> 4;
+  return reinterpret_cast<uint64_t>(w.planes) | ((uint64_t) (w.prev ? 1u : 0u) << 48) |
+         ((uint64_t) (uint8_t) (int8_t) off << 56);
 }
 
 // LINE geometries: request (b, c) as its line's address | planes chunk |
@@ -173,7 +189,8 @@ __device__ __forceinline__ uint32_t coop_lf(const IdxArgs& ix, const uint8_t* sl
 }
 
 // NEIGHBOR geometries: the slot holds block b's planes (chunks 0 .. BC-1) and,
-// when w.prev, block b-1's (chunks BC .. 2BC-1); cnt is the word w.cnt names.
+// when w.prev, block b-1's (chunks BC .. 2BC-1), else the counter's chunk
+// (chunk BC); cnt is the word w.cnt names.
 template <class G>
 __device__ __forceinline__ uint32_t coop_lf_nbr(const IdxArgs& ix, const uint8_t* slot, uint32_t b, uint32_t X,
                                                 uint32_t c, const uint32_t (&sx)[2 * G::K], uint32_t cnt, bool e,
@@ -331,8 +348,8 @@ __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, 
         eR = wR.e;
         pR = wR.prev;
         acR = wR.cnt;
-        postL = reinterpret_cast<uint64_t>(wL.planes) | (pL ? 1u : 0u);   // planes 16-B aligned
-        postR = reinterpret_cast<uint64_t>(wR.planes) | (pR ? 1u : 0u);
+        postL = nbr_post<G>(wL);
+        postR = nbr_post<G>(wR);
       } else if constexpr (C::LINE) {
         postL = coop_line_post<G>(ix, bl, c);
         postR = coop_line_post<G>(ix, br, c);
@@ -365,9 +382,13 @@ __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, 
             const uint64_t e = pe[r];
             const uint8_t* p = nullptr;
             if constexpr (C::NBR) {
-              const uint8_t* pl = reinterpret_cast<const uint8_t*>(e & ~1ull);
+              const uint8_t* pl = reinterpret_cast<const uint8_t*>(e & NBR_ADDR);
               if (k < C::BC) p = pl + 16 * k;
-              else if (k < 2 * C::BC && (e & 1u)) p = pl - G::EW * 4 + 16 * (k - C::BC);   // block b-1
+              else if ((e >> 48) & 1u) {
+                if (k < 2 * C::BC) p = pl - G::EW * 4 + 16 * (k - C::BC);                  // block b-1
+              } else if (k == C::BC) {
+                p = pl + 16 * (int) (int8_t) (e >> 56);                                     // counter chunk
+              }
             } else {
               const uint8_t* ln = reinterpret_cast<const uint8_t*>(e & ~(uint64_t) (C::LINEB - 1));
               const uint32_t cm = (1u << C::LCB) - 1u;
@@ -388,11 +409,13 @@ __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, 
             const uint32_t b = (uint32_t) (desc / (Desc) G::NC), cc = (uint32_t) (desc % (Desc) G::NC);
             Where<G> w = locate<G>(ix, b, cc);
             line_local_prev<G>(ix, b, cc, w);
-            if (k < C::BC || w.prev) {
-              const uint32_t* p = k < C::BC ? w.planes + 4 * k : w.pplanes + 4 * (k - C::BC);
+            const uint32_t* p = k < C::BC ? w.planes + 4 * k
+                                : w.prev ? w.pplanes + 4 * (k - C::BC)
+                                : k == C::BC ? reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(w.cnt) & ~(uintptr_t) 15)
+                                : nullptr;
+            if (p)
               __builtin_amdgcn_global_load_lds((const void*) p,
                                                (__attribute__((address_space(3))) void*) (wl + r * 1024), 16, 0, 0);
-            }
           }
         } else if (s < nreq && k <= C::BC) {
           const Desc desc = tab[s];
@@ -403,30 +426,41 @@ __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, 
         }
       }
       if constexpr (C::NBR) {
-        /* the two counter words, after the DMA (their lines are then already
-         * requested), as two exec-masked 32-lane groups (32 pages per
+        /* the counter words of the ends counted forward from block b-1 (the
+         * others came with the DMA), after the DMA (their lines are then
+         * already requested), as two exec-masked 32-lane groups (32 pages per
          * instruction at most, as the task kernels' fetch_ends_x4), R only
-         * where it has its own block; one vmcnt(0) for all */
+         * where it has its own block, parts no lane of a group needs branched
+         * over; one vmcnt(0) for all */
+        const uint64_t mpl = __ballot(pL), mpr = __ballot(needR && pR);
         uint64_t sv, gm;
         asm volatile("s_mov_b64 %[sv], exec\n"
                      "s_bfm_b64 %[gm], 32, 0\n"
                      "s_and_b64 exec, %[sv], %[gm]\n"
+                     "s_and_b64 exec, exec, %[ml]\n"
+                     "s_cbranch_execz .Lcl0_%=\n"
                      "global_load_dword %[cl], %[al], off\n"
-                     "s_and_b64 exec, exec, %[nr]\n"
+                     ".Lcl0_%=:\n"
+                     "s_and_b64 exec, %[sv], %[gm]\n"
+                     "s_and_b64 exec, exec, %[mr]\n"
                      "s_cbranch_execz .Lcc0_%=\n"
                      "global_load_dword %[cr], %[ar], off\n"
                      ".Lcc0_%=:\n"
                      "s_bfm_b64 %[gm], 32, 32\n"
                      "s_and_b64 exec, %[sv], %[gm]\n"
+                     "s_and_b64 exec, exec, %[ml]\n"
+                     "s_cbranch_execz .Lcl1_%=\n"
                      "global_load_dword %[cl], %[al], off\n"
-                     "s_and_b64 exec, exec, %[nr]\n"
+                     ".Lcl1_%=:\n"
+                     "s_and_b64 exec, %[sv], %[gm]\n"
+                     "s_and_b64 exec, exec, %[mr]\n"
                      "s_cbranch_execz .Lcc1_%=\n"
                      "global_load_dword %[cr], %[ar], off\n"
                      ".Lcc1_%=:\n"
                      "s_mov_b64 exec, %[sv]\n"
                      "s_waitcnt vmcnt(0)\n"
                      : [cl] "=&v"(sbL), [cr] "=&v"(sbR), [sv] "=&s"(sv), [gm] "=&s"(gm)
-                     : [al] "v"(acL), [ar] "v"(acR), [nr] "s"(mask)
+                     : [al] "v"(acL), [ar] "v"(acR), [ml] "s"(mpl), [mr] "s"(mpr)
                      : "memory", "scc");
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -435,9 +469,16 @@ __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, 
       plane_xor<G::K>(c, sx);
       uint32_t nL, nR;
       if constexpr (C::NBR) {
-        nL = coop_lf_nbr<G>(ix, wl + lane * C::SLOT, bl, L, c, sx, sbL, eL, pL);
-        nR = coop_lf_nbr<G>(ix, wl + (needR ? slotR : (uint32_t) lane) * C::SLOT, br, R, c, sx,
-                            needR ? sbR : sbL, needR ? eR : eL, needR ? pR : pL);
+        /* the counter word: loaded above where that end steps from block b-1,
+         * else word c % 4 of the slot's counter chunk (entries are 16-B
+         * aligned and the counter index is c, or c mod NC/2, past a multiple
+         * of 4 words) */
+        const uint8_t* sL = wl + lane * C::SLOT;
+        const uint8_t* sR = wl + (needR ? slotR : (uint32_t) lane) * C::SLOT;
+        const uint32_t cL = pL ? sbL : reinterpret_cast<const uint32_t*>(sL + 16 * C::BC)[c & 3u];
+        const uint32_t cR = needR ? (pR ? sbR : reinterpret_cast<const uint32_t*>(sR + 16 * C::BC)[c & 3u]) : cL;
+        nL = coop_lf_nbr<G>(ix, sL, bl, L, c, sx, cL, eL, pL);
+        nR = coop_lf_nbr<G>(ix, sR, br, R, c, sx, cR, needR ? eR : eL, needR ? pR : pL);
       } else {
         nL = coop_lf<G>(ix, wl + lane * C::SLOT, bl, L, c, sx, sbL);
         nR = coop_lf<G>(ix, wl + (needR ? slotR : (uint32_t) lane) * C::SLOT, br, R, c, sx, needR ? sbR : sbL);

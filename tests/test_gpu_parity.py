@@ -84,7 +84,8 @@ def random_index(kfmi_mod):
     rng = np.random.default_rng(2026)
     text = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), size=3_000_001).tobytes()
     return text, {(k, d): kfmi_mod.Index.build(text, k=k, d=d) for k, d in
-                  [(2, 64), (1, 64), (2, 192), (2, 448), (2, 960), (1, 32), (2, 128), (2, 256), (1, 128)]}
+                  [(2, 64), (1, 64), (2, 192), (2, 448), (2, 960), (1, 32), (2, 128), (2, 256), (1, 128),
+                   (2, 32)]}
 
 
 def _reads(text, n, m, seed):
@@ -98,7 +99,7 @@ def _reads(text, n, m, seed):
 
 @pytest.mark.parametrize("backend", PLAIN + ALT)
 @pytest.mark.parametrize("kd", [(2, 64), (1, 64), (2, 192), (2, 448), (2, 960), (1, 32), (2, 128), (2, 256),
-                                (1, 128)],
+                                (1, 128), (2, 32)],
                          ids=lambda kd: f"k{kd[0]}d{kd[1]}")
 def test_backend_matches_oracle_random(gpu, oracle_mod, random_index, backend, kd):
     text, idxs = random_index
@@ -329,7 +330,7 @@ def test_coop_issue_forms_equal_oracle(gpu, oracle_mod, random_index, backend, i
     jump start."""
     text, idxs = random_index
     monkeypatch.setenv("KFMI_COOP_ISSUE", issue)
-    for k, d in ((2, 64), (1, 64), (1, 32), (1, 128), (2, 128), (2, 256)):
+    for k, d in ((2, 64), (1, 64), (1, 32), (1, 128), (2, 128), (2, 256), (2, 32)):
         idx = idxs[(k, d)]
         if not coop_supported(backend, k, d):
             continue
