@@ -37,15 +37,11 @@ template <class G>
 struct CoopCfg {
   static constexpr int BC = G::BMW / 4;                 // 16-byte bitmap chunks per block
   static constexpr bool NBR = G::NEIGHBOR;              // planes of b [and b-1]; counter per lane
-  // lanes per request: a power of two, except on the grouped-counter lines
-  // (K = 3, 4: BC + 1 = 4 or 5 chunks), where 5 lanes per request (12 per
-  // round, 4 lanes idle) take 11 KiB of staging per wave instead of 16
-  static constexpr int TPR = NBR ? pow2ceil(2 * BC) : (G::LAY == LAY_GRP ? BC + 1 : pow2ceil(BC + 1));
+  static constexpr int TPR = NBR ? pow2ceil(2 * BC) : pow2ceil(BC + 1);   // lanes per request
   static constexpr int RPR = 64 / TPR;                  // requests per round
   static constexpr int SLOT = TPR * 16;                 // LDS bytes per request slot
   static constexpr int MAXREQ = 128;                    // 64 L + up to 64 R
-  static constexpr int MAXR = (MAXREQ + RPR - 1) / RPR; // staging rounds per K-step, at most
-  static constexpr int STAGE = MAXR * 1024;             // staging bytes per wave (round r at r * 1 KiB)
+  static constexpr int MAXR = MAXREQ / RPR;             // staging rounds per K-step, at most
   using Desc = typename std::conditional<(G::NC > 16), uint64_t, uint32_t>::type;   // b * NC + c
   // Line geometries (one power-of-two line holds a request's planes and its
   // counter chunk): a request is posted as its line's address with the planes'
@@ -60,22 +56,13 @@ struct CoopCfg {
   // wait per round
   static constexpr bool PRE = NBR || LINE;
   static constexpr int TABB = PRE ? 8 : (int) sizeof(Desc);
-  static constexpr int WAVE_LDS = STAGE + MAXREQ * TABB;
+  static constexpr int WAVE_LDS = MAXREQ * SLOT + MAXREQ * TABB;
   static constexpr int WPB0 = 65536 / WAVE_LDS;
   static constexpr int WPB = WPB0 < 1 ? 1 : (WPB0 > 4 ? 4 : WPB0);   // waves per block
   static constexpr bool OK = (G::BMW % 4 == 0) && (G::EW % 4 == 0) && (G::BOFF % 4 == 0) &&
                              (!G::ACRULE || G::HALF >= 4) && (!G::MIDLINES || G::NC >= 4) &&
                              TPR <= 64;
 };
-
-// LDS offset of request s's slot: round s / RPR at 1 KiB steps, TPR lanes of
-// 16 bytes per request within it (= s * SLOT when TPR is a power of two)
-template <class G>
-__device__ __forceinline__ uint32_t coop_slot(uint32_t s)
-{
-  using C = CoopCfg<G>;
-  return (s / C::RPR) * 1024u + (s % C::RPR) * C::SLOT;
-}
 
 // byte address of chunk k of request (b, c)
 template <class G>
@@ -267,8 +254,8 @@ __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, 
   const int lane = threadIdx.x & 63;
   uint8_t* wl = lds + wave * C::WAVE_LDS;
   using Desc = typename C::Desc;
-  Desc* tab = reinterpret_cast<Desc*>(wl + C::STAGE);
-  uint64_t* post = reinterpret_cast<uint64_t*>(wl + C::STAGE);   // PRE: request addresses
+  Desc* tab = reinterpret_cast<Desc*>(wl + C::MAXREQ * C::SLOT);
+  uint64_t* post = reinterpret_cast<uint64_t*>(wl + C::MAXREQ * C::SLOT);   // PRE: request addresses
   const bool pre = C::PRE && ix.coop_issue != 0;                            // wave-uniform
   const uint64_t q0 = ((uint64_t) blockIdx.x * C::WPB + wave) * 64;
   if (q0 >= num) return;                       // whole wave idle (wave-uniform)
@@ -276,7 +263,6 @@ __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, 
   const uint64_t qs = q < num ? q : num - 1;   // tail lanes replay a valid query, never stored
   const int k = lane % C::TPR;
   const int g = lane / C::TPR;
-  const bool gok = g < C::RPR;   // lanes past RPR * TPR (TPR not a power of two) stage nothing
   uint32_t cw[CW];
   uint32_t rc = 0;
   if constexpr (MAXW > 0) {
@@ -388,7 +374,7 @@ __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, 
            * back to back (requests s >= nreq of the last round masked off) */
           uint64_t pe[C::MAXR];
 #pragma unroll
-          for (int r = 0; r < C::MAXR; ++r) pe[r] = post[gok ? r * C::RPR + g : 0];
+          for (int r = 0; r < C::MAXR; ++r) pe[r] = post[r * C::RPR + g];
 #pragma unroll
           for (int r = 0; r < C::MAXR; ++r) {
             if ((uint32_t) r >= rounds) break;
@@ -409,14 +395,14 @@ __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, 
               if (k < C::BC) p = ln + 16 * (((uint32_t) e & cm) + k);
               else if (k == C::BC) p = ln + 16 * (((uint32_t) (e >> C::LCB)) & cm);
             }
-            if (gok && s < nreq && p)
+            if (s < nreq && p)
               __builtin_amdgcn_global_load_lds((const void*) p,
                                                (__attribute__((address_space(3))) void*) (wl + r * 1024), 16, 0, 0);
           }
         }
       }
       for (uint32_t r = 0; !pre && r < rounds; ++r) {
-        const uint32_t s = gok ? r * C::RPR + g : 0xFFFFFFFFu;
+        const uint32_t s = r * C::RPR + g;
         if constexpr (C::NBR) {
           if (s < nreq && k < 2 * C::BC) {
             const Desc desc = tab[s];
@@ -487,15 +473,15 @@ __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, 
          * else word c % 4 of the slot's counter chunk (entries are 16-B
          * aligned and the counter index is c, or c mod NC/2, past a multiple
          * of 4 words) */
-        const uint8_t* sL = wl + coop_slot<G>((uint32_t) lane);
-        const uint8_t* sR = wl + coop_slot<G>(needR ? slotR : (uint32_t) lane);
+        const uint8_t* sL = wl + lane * C::SLOT;
+        const uint8_t* sR = wl + (needR ? slotR : (uint32_t) lane) * C::SLOT;
         const uint32_t cL = pL ? sbL : reinterpret_cast<const uint32_t*>(sL + 16 * C::BC)[c & 3u];
         const uint32_t cR = needR ? (pR ? sbR : reinterpret_cast<const uint32_t*>(sR + 16 * C::BC)[c & 3u]) : cL;
         nL = coop_lf_nbr<G>(ix, sL, bl, L, c, sx, cL, eL, pL);
         nR = coop_lf_nbr<G>(ix, sR, br, R, c, sx, cR, needR ? eR : eL, needR ? pR : pL);
       } else {
-        nL = coop_lf<G>(ix, wl + coop_slot<G>((uint32_t) lane), bl, L, c, sx, sbL);
-        nR = coop_lf<G>(ix, wl + coop_slot<G>(needR ? slotR : (uint32_t) lane), br, R, c, sx, needR ? sbR : sbL);
+        nL = coop_lf<G>(ix, wl + lane * C::SLOT, bl, L, c, sx, sbL);
+        nR = coop_lf<G>(ix, wl + (needR ? slotR : (uint32_t) lane) * C::SLOT, br, R, c, sx, needR ? sbR : sbL);
       }
       L = nL;
       R = nR;
