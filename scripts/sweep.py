@@ -38,6 +38,10 @@ def main():
     p.add_argument("--backends", default="task-packed,task,task-ac,coop,coop-ac,coop-packed")
     p.add_argument("--env", default="", help="semicolon list of VAR=v1,v2 knobs swept for every backend")
     p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=1, help="untimed searches per variant before its timed steps")
+    p.add_argument("--repeat", type=int, default=1,
+                   help="time every backend's knob list this many times, in reverse order on odd passes "
+                        "(A B B A ...), so an order effect shows as a disagreement between passes")
     p.add_argument("--sort-suffix", default="0",
                    help="experiment: comma list of N; order reads by their last N bases (backward-search "
                         "order, N <= 32), one pass over the backends per N")
@@ -97,13 +101,15 @@ def main():
         q = K.Queries.from_array(reads)
         r = K.Results.alloc(reads.shape[0])
         for b in a.backends.split(","):
-            for kn in knobs:
+          for rep in range(a.repeat):
+            for kn in (knobs if rep % 2 == 0 else knobs[::-1]):
                 for var, v in kn.items():
                     os.environ[var] = v
                 try:
                     K.set_backend(b)
                     K.transfer_to_gpu(idx, q, r)
-                    K.search(idx, q, r)
+                    for _ in range(max(1, a.warmup)):
+                        K.search(idx, q, r)
                     lf, tot = [], []
                     t0 = time.perf_counter()
                     for _ in range(a.steps):
@@ -118,18 +124,18 @@ def main():
                         res = res.reshape(-1, 2)[inv].reshape(-1)
                     if ref is None:
                         ref = res
-                    out = {"backend": b, "knobs": kn, "order": kind, "sort_suffix": ss, "lf_ms": round(float(np.median(lf)), 3),
+                    out = {"backend": b, "knobs": kn, "pass": rep, "order": kind, "sort_suffix": ss, "lf_ms": round(float(np.median(lf)), 3),
                            "lf_ms_min": round(float(np.min(lf)), 3), "step_ms": round(float(np.median(tot)), 3),
                            "wall_ms": round(wall * 1e3, 3), "mqps": round(reads.shape[0] / wall / 1e6, 1),
                            "equal": bool(np.array_equal(res, ref)), "dev_bytes": idx.device_bytes(),
                            "res_md5": synth.results_md5(res)}
                 except K.KfmiError as e:
-                    out = {"backend": b, "knobs": kn, "order": kind, "sort_suffix": ss, "error": str(e)}
+                    out = {"backend": b, "knobs": kn, "pass": rep, "order": kind, "sort_suffix": ss, "error": str(e)}
                 print(json.dumps(out), flush=True)
                 log(out)
                 for var in kn:
                     os.environ.pop(var, None)
-            idx.free_gpu()
+          idx.free_gpu()
         q.close()
         r.close()
 
