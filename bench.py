@@ -617,10 +617,10 @@ def kstep4_leg(D, text: bytes, reads: np.ndarray, res: np.ndarray, idx2, steps: 
         K.set_backend("coop-grp")
         K.transfer_to_gpu(h["i4"], h["q"], h["r"])
         h["upload_s"] = time.perf_counter() - t
-        # 30 untimed searches: the first ~30 after the 96 GB table's upload run
-        # ~2 % slow (the fresh allocation's page tables warming up,
+        # 60 untimed searches: the first 30-40 after the 96 GB table's upload
+        # run ~2 % slow (the fresh allocation warming up,
         # profiles/r03/sweep_k4_r3y.jsonl), a one-time cost of the upload
-        for _ in range(30):
+        for _ in range(60):
             K.search(h["i4"], h["q"], h["r"])
 
     def timed(lf):
