@@ -1059,9 +1059,12 @@ IdxArgs idx_args(const kfmi_dev_index* di)
   ix.split = split_for(di->ent_bytes + di->sb_bytes, di->layout);
   e = getenv("KFMI_COOP_ISSUE");   /* 0: coop staging rounds decode their requests */
   ix.coop_issue = (e && *e) ? (uint32_t) (atoi(e) != 0) : 1u;
-  /* the reference layouts' posts keep flags above bit 47 of the address
-   * (kfmi_coop.h nbr_post): a table mapped above that decodes its rounds */
-  if ((uint64_t) (uintptr_t) di->ent + di->ent_bytes >= (1ull << 48)) ix.coop_issue = 0;
+  /* the posts keep flags above bit 47 of the address (reference layouts,
+   * kfmi_coop.h nbr_post) or chunk numbers below the line size (line layouts,
+   * coop_line_post, lines of <= 256 B): a table mapped above 2^48 or not
+   * 256-B aligned decodes its rounds */
+  if ((uint64_t) (uintptr_t) di->ent + di->ent_bytes >= (1ull << 48) || ((uintptr_t) di->ent & 255u) != 0)
+    ix.coop_issue = 0;
   return ix;
 }
 
