@@ -488,6 +488,7 @@ struct SearchLaunch {
   uint64_t total;
   uint32_t* pos;
   unsigned long long* slot_ctr;   /* walk slot queue, zeroed before the launch */
+  uint32_t slot_chunk;            /* slots per queue take (64 .. 4096) */
   /* in-call reorder: search order and row-major code words (MAXW = 8) */
   const uint32_t* perm;
   const uint32_t* pk;
@@ -599,7 +600,7 @@ static hipError_t launch_locate(const SearchLaunch& a)
        * profiles/r02/locate_r2ba.jsonl: the walk is not short of lines in flight) */
       hipLaunchKernelGGL((locate_coop_kernel<G>), dim3(grid_blocks(blocks, (uint64_t) cus * 5)), dim3(256), 0, a.st, a.ix,
                          a.sa, a.sa_log2,
-                         a.owner, a.total, a.pos, a.slot_ctr);
+                         a.owner, a.total, a.pos, a.slot_ctr, a.slot_chunk);
       return hipGetLastError();
     }
   }

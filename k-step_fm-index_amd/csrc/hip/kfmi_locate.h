@@ -68,7 +68,7 @@ __device__ __forceinline__ uint32_t lf_row(const IdxArgs& ix, uint32_t X)
 // every lane of the wave (the caller's loop is wave-uniform).  Returns the
 // lane's slot, or ~0 when it wants none or the queue is empty; slots a wave
 // receives only grow, so once a lane is told "empty" it stays so.
-constexpr uint32_t SLOT_CHUNK = 256;
+constexpr uint32_t SLOT_CHUNK = 256;   // default chunk (KFMI_LOCATE_CHUNK: 64 .. 4096)
 
 __device__ __forceinline__ uint64_t uniform64(uint64_t x)
 {
@@ -81,7 +81,8 @@ struct WaveSlots {
   uint64_t fixed = ~0ull;      // ctr == nullptr (KFMI_LOCATE_QUEUE=0): this lane's next slot of i, i + stride, ...
 };
 
-__device__ __forceinline__ uint64_t take_slot(bool want, WaveSlots& ws, unsigned long long* ctr, uint64_t total)
+__device__ __forceinline__ uint64_t take_slot(bool want, WaveSlots& ws, unsigned long long* ctr, uint64_t total,
+                                              uint32_t chunk = SLOT_CHUNK)
 {
   if (!ctr) {   // fixed order (A/B reference)
     if (ws.fixed == ~0ull) ws.fixed = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x;
@@ -104,12 +105,12 @@ __device__ __forceinline__ uint64_t take_slot(bool want, WaveSlots& ws, unsigned
   } else {
     unsigned long long base = ~0ull;   // queue already past its end: no more chunks
     if (ws.end < total) {
-      if ((threadIdx.x & 63) == 0) base = atomicAdd(ctr, (unsigned long long) SLOT_CHUNK);
+      if ((threadIdx.x & 63) == 0) base = atomicAdd(ctr, (unsigned long long) chunk);
       base = __shfl(base, 0);
     }
     slot = rank < have ? ws.cur + rank : (base == ~0ull ? ~0ull : base + (rank - have));
     ws.cur = base == ~0ull ? ws.end : base + (n - have);
-    ws.end = base == ~0ull ? ws.end : base + SLOT_CHUNK;
+    ws.end = base == ~0ull ? ws.end : base + chunk;
   }
   return want && slot < total ? slot : ~0ull;
 }
@@ -199,7 +200,7 @@ template <class G>
 __global__ __launch_bounds__(256) void locate_coop_kernel(IdxArgs ix, const uint32_t* __restrict__ sa,
                                                           uint32_t rate_log2, const uint32_t* __restrict__ rows,
                                                           uint64_t total, uint32_t* __restrict__ pos,
-                                                          unsigned long long* __restrict__ ctr)
+                                                          unsigned long long* __restrict__ ctr, uint32_t chunk)
 {
   constexpr int LB = G::EW * 4;     // line bytes
   constexpr int TPR = LB / 16;      // lanes per line
@@ -211,9 +212,9 @@ __global__ __launch_bounds__(256) void locate_coop_kernel(IdxArgs ix, const uint
   const uint8_t* base = reinterpret_cast<const uint8_t*>(ix.ent);
   const uint32_t mask = (1u << rate_log2) - 1u;
   WaveSlots ws;
-  uint64_t i = take_slot(true, ws, ctr, total);
+  uint64_t i = take_slot(true, ws, ctr, total, chunk);
   uint32_t r = i < total ? rows[i] : 0u;
-  uint64_t i_n = take_slot(true, ws, ctr, total);
+  uint64_t i_n = take_slot(true, ws, ctr, total, chunk);
   uint32_t r_n = i_n < total ? rows[i_n] : 0u;
   bool act = i < total;
   uint32_t steps = 0;
@@ -248,7 +249,7 @@ __global__ __launch_bounds__(256) void locate_coop_kernel(IdxArgs ix, const uint
       r = nr;
       steps += G::K;
     }
-    const uint64_t got = take_slot(fin, ws, ctr, total);
+    const uint64_t got = take_slot(fin, ws, ctr, total, chunk);
     if (fin) {
       i_n = got;
       r_n = got < total ? rows[got] : 0u;

@@ -187,6 +187,9 @@ static int32_t locate_on(kfmi_fmi_t* f, kfmi_dev_index* di, uint32_t* d_res, uin
   const char* qe = getenv("KFMI_LOCATE_QUEUE");
   const bool queue = qe ? atoi(qe) != 0 : (1u << di->sa_log2) >= 8;
   a.slot_ctr = queue ? reinterpret_cast<unsigned long long*>(d_cnt) : nullptr;
+  const char* ce = getenv("KFMI_LOCATE_CHUNK");   /* slots per queue take; >= 64 keeps one take enough per wave */
+  const long cv = ce ? atol(ce) : (long) SLOT_CHUNK;
+  a.slot_chunk = (uint32_t) (cv < 64 ? 64 : (cv > 4096 ? 4096 : cv));
   ok = hipMemsetAsync(d_cnt, 0, 8, st) == hipSuccess && hipEventRecord(ev[1], st) == hipSuccess &&
        (total == 0 || dispatch(Op::Locate, di->K, di->nb, di->layout, a) == hipSuccess) &&
        hipEventRecord(ev[2], st) == hipSuccess &&
