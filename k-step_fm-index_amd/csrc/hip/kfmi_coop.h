@@ -36,7 +36,7 @@ __host__ __device__ constexpr int ilog2(int x) { int l = 0; while ((1 << (l + 1)
 template <class G>
 struct CoopCfg {
   static constexpr int BC = G::BMW / 4;                 // 16-byte bitmap chunks per block
-  static constexpr bool NBR = G::NEIGHBOR;              // planes of b [and b-1]; counter per lane
+  static constexpr bool NBR = G::NEIGHBOR;              // planes of b + counter chunk, or of b and b-1
   static constexpr int TPR = NBR ? pow2ceil(2 * BC) : pow2ceil(BC + 1);   // lanes per request
   static constexpr int RPR = 64 / TPR;                  // requests per round
   static constexpr int SLOT = TPR * 16;                 // LDS bytes per request slot
@@ -53,7 +53,8 @@ struct CoopCfg {
   // Pre-addressed issue (IdxArgs::coop_issue): each lane posts its own ends'
   // addresses (64-bit) and the staging rounds only read them back -- all of a
   // step's table reads in flight together instead of a read, a decode and a
-  // wait per round
+  // wait per round (measured neutral against the decoding rounds, DESIGN.md
+  // 5 "Coop issue"; both forms are parity-tested)
   static constexpr bool PRE = NBR || LINE;
   static constexpr int TABB = PRE ? 8 : (int) sizeof(Desc);
   static constexpr int WAVE_LDS = MAXREQ * SLOT + MAXREQ * TABB;
