@@ -187,12 +187,15 @@ def test_locate_max_occ_repeats_and_empty(gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("queue", ["0", "1"])
-def test_locate_slot_queue_forced(gpu, monkeypatch, queue):
+@pytest.mark.parametrize("queue,chunk", [("0", "256"), ("1", "256"), ("1", "64"), ("1", "4096"), ("1", "100")])
+def test_locate_slot_queue_forced(gpu, monkeypatch, queue, chunk):
     # the cooperative walk's slot queue (default at SA rate >= 8) and the fixed
     # slot order, each forced at every rate: ~3 M positions, so every wave of
-    # the grid takes several chunks of the queue and the last chunk is partial
+    # the grid takes several chunks of the queue and the last chunk is partial;
+    # queue chunks of 64 (the floor: one take covers a wave), 100 (not a power
+    # of two) and 4096 slots (KFMI_LOCATE_CHUNK) give the same positions
     monkeypatch.setenv("KFMI_LOCATE_QUEUE", queue)
+    monkeypatch.setenv("KFMI_LOCATE_CHUNK", chunk)
     text = b"A" * 3000 + b"C" + b"ACGT" * 700 + b"G" + _text(5000, 77)
     sa = util.suffix_array(text + b"$")
     q = np.frombuffer(b"AAAA" * 999 + b"ACGT" + b"TTTT" + b"CGTA", dtype=np.uint8).reshape(-1, 4)
@@ -202,8 +205,8 @@ def test_locate_slot_queue_forced(gpu, monkeypatch, queue):
             res, off, pos = gpu.locate_array(idx, q, backend)
             w_off, w_pos = _expected(sa, res)
             assert int(w_off[-1]) > 2_900_000
-            assert np.array_equal(off, w_off), (queue, rate, backend)
-            assert np.array_equal(pos, w_pos), (queue, rate, backend)
+            assert np.array_equal(off, w_off), (queue, chunk, rate, backend)
+            assert np.array_equal(pos, w_pos), (queue, chunk, rate, backend)
         idx.close()
 
 
