@@ -85,6 +85,76 @@ def parse():
     return p.parse_args()
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n: int, argv: list, script: str | None = None, grace_s: float = 20.0) -> int:
+    """`bench.py --gpus N` without a launcher: start N fresh child processes of
+    `script` (default this file) with argv, one per rank, with the environment
+    torch.distributed.run would give them (RANK, LOCAL_RANK, WORLD_SIZE,
+    LOCAL_WORLD_SIZE, GROUP_RANK, MASTER_ADDR=127.0.0.1, MASTER_PORT), and
+    wait.  Called before this process touches HIP; the children are started,
+    never exec'd into.  Rank 0 shares this process's stdout (its JSON line is
+    the run's line), the others print to stderr.  The first child that exits
+    non-zero ends the run: the rest are terminated (they would wait for it at
+    their next barrier) and its code is returned; 0 when every rank exits 0."""
+    import signal
+    import subprocess
+    port = _free_port()
+    procs = []
+
+    def stop_all():
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        t_end = time.monotonic() + grace_s
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, t_end - time.monotonic()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+
+    def on_signal(signum, frame):
+        stop_all()
+        raise SystemExit(128 + signum)
+
+    old = {s: signal.signal(s, on_signal) for s in (signal.SIGTERM, signal.SIGINT)}
+    failed = None
+    try:
+        sys.stdout.flush()
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                       GROUP_RANK="0", ROLE_RANK=str(r), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                       KFMI_BENCH_LAUNCHER="self-spawned")
+            procs.append(subprocess.Popen([sys.executable, script or str(Path(__file__).resolve()), *argv], env=env,
+                                          stdout=None if r == 0 else sys.stderr))
+        log(f"launcher: {n} ranks started (pids {[p.pid for p in procs]}, master port {port})")
+        while failed is None and any(p.poll() is None for p in procs):
+            for r, p in enumerate(procs):
+                rc = p.poll()
+                if rc is not None and rc != 0:
+                    failed = (r, rc)
+                    break
+            time.sleep(0.2)
+        if failed is None:
+            failed = next(((r, p.returncode) for r, p in enumerate(procs) if p.returncode != 0), None)
+    finally:
+        stop_all()
+        for s, h in old.items():
+            signal.signal(s, h)
+    if failed is not None:
+        log(f"launcher: rank {failed[0]} exited with {failed[1]}; the other ranks were stopped")
+        return failed[1] if failed[1] > 0 else 1
+    return 0
+
+
 class Dist:
     def __init__(self, gpus: int):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -180,11 +250,25 @@ class Phases:
     def __init__(self):
         self.t = time.perf_counter()
         self.rows = {}
+        self.anon_peak = 0.0
 
     def mark(self, name: str) -> None:
         now = time.perf_counter()
         self.rows[name] = round(self.rows.get(name, 0.0) + now - self.t, 2)
         self.t = now
+        self.anon_peak = max(self.anon_peak, self.rss_anon_gb())
+
+    @staticmethod
+    def rss_anon_gb() -> float:
+        """This process's private resident memory now (RssAnon: excludes the
+        page-cache pages of the node-shared text and image mappings)."""
+        try:
+            for ln in open("/proc/self/status"):
+                if ln.startswith("RssAnon:"):
+                    return round(int(ln.split()[1]) / 1e6, 2)
+        except OSError:
+            pass
+        return 0.0
 
     @staticmethod
     def peak_rss_gb() -> float:
@@ -229,13 +313,60 @@ def cuda_sync(dev: int):
         pass
 
 
-def make_text(n: int) -> bytes:
-    if n == 3_000_000_000:
-        return synth.text_3g(n)
-    import random
-    rng = random.Random(n)
-    step = 1 << 27                                  # getrandbits takes < 2^31 bits per call
-    return b"".join(rng.randbytes(min(step, n - i)).translate(synth.TBL) for i in range(0, n, step))
+def bench_text(D, n: int):
+    """The reference text, generated once per node (synth.text_chunks: the
+    md5-pinned 3 Gbase recipe, or random.Random(n) for other sizes).  N = 1:
+    filled into one bytearray chunk by chunk (peak = the text, not text + the
+    joined chunks).  N > 1: local rank 0 streams it to a file in TMPDIR, every
+    rank maps that file read-only -- one copy in the node's page cache instead
+    of one 3 GB object per rank -- and the file is unlinked once every rank
+    holds its mapping."""
+    if D.world == 1:
+        buf = bytearray(n)
+        off = 0
+        for ch in synth.text_chunks(n):
+            buf[off:off + len(ch)] = ch
+            off += len(ch)
+        return buf
+    return _node_shared(D, f"text_{n}", lambda f: [f.write(ch) for ch in synth.text_chunks(n)])
+
+
+def _node_shared(D, name: str, write):
+    """A file written once per node by local rank 0 (`write(f)`), then mapped
+    read-only by every rank of the node; returns the mmap.  Collective: every
+    rank calls it; a failed write fails every rank together."""
+    import mmap
+    d = Path(os.environ.get("TMPDIR") or "/tmp")
+    fn = d / f"kfmi_bench_{name}_{os.environ.get('MASTER_PORT', '0')}.bin"
+    err = None
+    if D.local == 0:
+        try:
+            tmp = fn.with_suffix(".part")
+            with open(tmp, "wb") as f:
+                write(f)
+            os.replace(tmp, fn)
+        except OSError as e:
+            err = f"{type(e).__name__}: {e}"
+    if not D.all_ok(err is None):
+        raise SystemExit(f"bench.py: node-shared file {fn} could not be written ({err})")
+    with open(fn, "rb") as f:
+        mm = mmap.mmap(f.fileno(), 0, access=mmap.ACCESS_READ)
+    D.barrier()                      # every rank holds its mapping: the name can go
+    if D.local == 0:
+        fn.unlink(missing_ok=True)
+    return mm
+
+
+def shared_image(D, idx) -> np.ndarray:
+    """The index's tag-100 image for the CPU oracle.  N = 1: the handle's own
+    host image.  N > 1: every rank built the same index from the same text (on
+    its own GPU, without a host image); local rank 0 fetches its image from
+    the device and the others map rank 0's copy (the parity samples then check
+    each rank's GPU results against that image)."""
+    if D.world == 1:
+        return idx.image()
+    mm = _node_shared(D, "image", lambda f: idx.image().tofile(f))
+    return np.frombuffer(mm, dtype=np.uint8)
 
 
 def cpu_threads() -> int:
@@ -473,13 +604,14 @@ def config1_leg(backend: str, thr: int, steps: int = 5) -> dict:
 
 
 def config5_leg(D, idx, text: bytes, backend: str, qlen: int, nq: int, steps: int, warmup: int, ac: bool,
-                oracle_idx=None, ingest: bool = False) -> dict:
+                oracle_img=None, ingest: bool = False) -> dict:
     """BASELINE config #5's read shape on every rank: this rank's shard of nq
     reads of qlen bases (seed 20 + rank; 10M x 150 bp = one eighth of the
     80M x 150 bp batch at N = 8), searched on the resident index; timed like
     the main leg (barrier + synchronize, max over ranks), then an evenly spread
     100 K-read sample of every rank checked against the CPU oracle (on
-    `oracle_idx`'s image when given: another index of the same text).  Every
+    `oracle_img` when given: the image of another index of the same text, or
+    the node-shared image at N > 1; AltCounters semantics from `idx`).  Every
     rank makes the same collective calls whatever fails locally (Steps)."""
     from oracle import oracle
     S = Steps()
@@ -565,11 +697,13 @@ def config5_leg(D, idx, text: bytes, backend: str, qlen: int, nq: int, steps: in
 
     def parity():
         sel = np.linspace(0, nq - 1, min(100_000, nq)).astype(np.int64)
-        src = oracle_idx if oracle_idx is not None else idx
-        img_idx = src.alt_counters()[0] if ac else src
-        want, _ = oracle.search(img_idx.image(), h["reads"][sel], nthreads=max(1, cpu_effective() // D.world))
         if ac:
+            img_idx = idx.alt_counters()[0]
+            want, _ = oracle.search(img_idx.image(), h["reads"][sel], nthreads=max(1, cpu_effective() // D.world))
             img_idx.close()
+        else:
+            img = oracle_img if oracle_img is not None else idx.image()
+            want, _ = oracle.search(img, h["reads"][sel], nthreads=max(1, cpu_effective() // D.world))
         h["n_sample"] = int(sel.size)
         return bool(np.array_equal(want.reshape(-1, 2), h["res"].reshape(-1, 2)[sel]))
 
@@ -590,7 +724,7 @@ def config5_leg(D, idx, text: bytes, backend: str, qlen: int, nq: int, steps: in
     return out
 
 
-def kstep4_leg(D, text: bytes, reads: np.ndarray, res: np.ndarray, idx2, steps: int, pinned_md5: str | None,
+def kstep4_leg(D, text: bytes, reads: np.ndarray, res: np.ndarray, img2, steps: int, pinned_md5: str | None,
                c5_qlen: int, c5_queries: int) -> dict:
     """Every rank's reads on a K = 4 index (the reference's K_STEPS parameter;
     its GPU files stop at K = 2): built on the device with no host image (the
@@ -677,7 +811,7 @@ def kstep4_leg(D, text: bytes, reads: np.ndarray, res: np.ndarray, idx2, steps: 
     if c5_queries > 0:
         if D.all_ok(S.ok):
             out["config5"] = config5_leg(D, h["i4"], text, "coop-grp", c5_qlen, c5_queries, steps, 5, False,
-                                         oracle_idx=idx2)
+                                         oracle_img=img2)
     if "i4" in h:
         try:
             h["i4"].free_gpu()
@@ -735,6 +869,16 @@ def time_backend(idx, q, r, backend, steps, warmup):
 
 def main():
     a = parse()
+    ws = os.environ.get("WORLD_SIZE")
+    if a.gpus < 1:
+        raise SystemExit(f"bench.py: --gpus {a.gpus}: need at least one rank")
+    if ws is None and a.gpus > 1:
+        # no launcher around us: start the N ranks here, before anything in
+        # this process touches HIP (bench.spawn_ranks; no exec)
+        raise SystemExit(spawn_ranks(a.gpus, sys.argv[1:]))
+    if ws is not None and int(ws) != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but the launcher started WORLD_SIZE={ws} ranks; "
+                         "refusing to report a run of a different size")
     D = Dist(a.gpus)
     ph = Phases()
     K.load()
@@ -762,18 +906,38 @@ def main():
 
     # ---- inputs: reference text, index replica, this rank's reads ----------
     t = time.perf_counter()
-    text = make_text(a.ref_size)
+    text = bench_text(D, a.ref_size)
     log(f"rank {D.rank}: text {len(text)} bases in {time.perf_counter() - t:.1f}s")
     ph.mark("text")
     t = time.perf_counter()
-    idx = K.Index.build(text, k=a.k, d=a.d, gpu=True, sa_rate=a.sa_rate)
+    # N = 1: host image + SA samples (locate runs at N = 1 only).  N > 1: no
+    # host image per rank; the oracle's image is shared on the node (shared_image)
+    if D.world == 1:
+        idx = K.Index.build(text, k=a.k, d=a.d, gpu=True, sa_rate=a.sa_rate)
+    elif not dev_agg["shared_devices"]:
+        idx = K.Index.build(text, k=a.k, d=a.d, gpu=True, host_image=False)
+    else:
+        # a rehearsal with ranks sharing a card: the builders' transient device
+        # memory (the suffix sort) would peak on one card at once, so the ranks
+        # take turns; on a node with a GPU per rank they build concurrently
+        idx, err = None, None
+        for r in range(D.world):
+            if r == D.rank:
+                try:
+                    idx = K.Index.build(text, k=a.k, d=a.d, gpu=True, host_image=False)
+                except K.KfmiError as e:
+                    err = str(e)
+            D.barrier()
+        if not D.all_ok(err is None):
+            raise SystemExit(f"bench.py: rank {D.rank}: index build failed: {err}")
     build_s = time.perf_counter() - t
     log(f"rank {D.rank}: GPU index build {build_s:.1f}s")
+    img = shared_image(D, idx)
     ph.mark("index_build")
     pinned = (a.ref_size == 3_000_000_000 and a.k == 2 and a.d == 64)
     index_md5_ok = None
     if pinned and D.rank == 0 and not a.no_md5:
-        h = hashlib.md5(idx.image().tobytes()).hexdigest()
+        h = hashlib.md5(idx.image()).hexdigest()
         index_md5_ok = h == synth.MD5["ref3g.k2d64.fmi"]
         log(f"index md5 {h} pinned-ok={index_md5_ok}")
     t = time.perf_counter()
@@ -831,8 +995,9 @@ def main():
         t = time.perf_counter()
         sel = np.linspace(0, reads.shape[0] - 1, ns_par).astype(np.int64)
         ac = a.backend in ("task-ac", "coop-ac", "task-ac128", "coop-ac128")
-        img_idx = idx.alt_counters()[0] if ac else idx
-        want, _ = oracle.search(img_idx.image(), reads[sel], nthreads=max(1, cpu_effective() // D.world))
+        img_idx = idx.alt_counters()[0] if ac else None
+        want, _ = oracle.search(img_idx.image() if ac else img, reads[sel],
+                                nthreads=max(1, cpu_effective() // D.world))
         parity_ok = bool(np.array_equal(want.reshape(-1, 2), res.reshape(-1, 2)[sel]))
         if ac:
             img_idx.close()
@@ -877,7 +1042,7 @@ def main():
     if a.config5_queries > 0:
         c5 = config5_leg(D, idx, text, a.backend, a.config5_qlen, a.config5_queries, a.steps, 5,
                          a.backend in ("task-ac", "coop-ac", "task-ac128", "coop-ac128", "task-ac-mid",
-                                       "coop-ac-mid"), ingest=ingest_on)
+                                       "coop-ac-mid"), oracle_img=img, ingest=ingest_on)
         log(f"rank {D.rank}: config #5 leg {c5}")
         ph.mark("config5")
     ingest = None
@@ -890,7 +1055,7 @@ def main():
     k4 = None
     if a.kstep4 and a.k == 2 and a.d == 64:
         # ---- K = 4 on every rank's reads (LAY_GRP, coop kernel) --------------
-        k4 = kstep4_leg(D, text, reads, res, idx, a.steps,
+        k4 = kstep4_leg(D, text, reads, res, img, a.steps,
                         synth.MD5["res3g.q10M"] if (pinned and a.qlen == 100 and a.queries == 10_000_000)
                         else None, a.config5_qlen, a.config5_queries)
         log(f"rank {D.rank}: K=4 leg {k4}")
@@ -1032,7 +1197,6 @@ def main():
         from oracle import oracle
         thrs = [a.cpu_threads] if a.cpu_threads else baseline_thread_counts()
         ns = min(a.cpu_sample, reads.shape[0])
-        img = idx.image()
         ports = []
         for thr in thrs:
             t = time.perf_counter()
@@ -1076,11 +1240,16 @@ def main():
         log(f"cpu baseline {cpu}")
     ph.mark("rank0_n1_legs_and_cpu_baseline")
     # per-rank phase wall times and peak host RSS (the N = 8 budget: DESIGN.md 7)
-    ph_rows = D.gather({"rank": D.rank, "phases_s": ph.rows, "peak_rss_gb": Phases.peak_rss_gb()})
+    ph_rows = D.gather({"rank": D.rank, "phases_s": ph.rows, "peak_rss_gb": Phases.peak_rss_gb(),
+                        "rss_anon_peak_gb": ph.anon_peak})
     phases = {"per_rank": ph_rows,
               "max_over_ranks_s": {k: max(r["phases_s"].get(k, 0.0) for r in ph_rows) for k in ph.rows},
               "wall_s_max": round(max(sum(r["phases_s"].values()) for r in ph_rows), 1),
               "peak_rss_gb_max": max(r["peak_rss_gb"] for r in ph_rows),
+              # private memory (sampled at every phase end): the node-shared text
+              # and image mappings (N > 1) are page cache, counted once per node
+              "rss_anon_peak_gb_max": max(r["rss_anon_peak_gb"] for r in ph_rows),
+              "shared_text_and_image": D.world > 1,
               "host_threads_per_rank": K.host_threads(),
               "ingest_legs": ingest_on}
 
@@ -1108,6 +1277,7 @@ def main():
                                       + (f" (REHEARSAL: {D.world} ranks on {dev_agg['distinct_devices']} GPU(s))"
                                          if dev_agg["shared_devices"] else "")},
             "ranks_launched": D.world,
+            "launcher": os.environ.get("KFMI_BENCH_LAUNCHER", "external" if D.world > 1 else "none"),
             "devices": dict(dev_agg, per_rank=dev_rows),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,

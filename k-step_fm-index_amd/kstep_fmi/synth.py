@@ -48,9 +48,19 @@ def reads_64m(text: bytes, rng: random.Random, num: int = 1 << 20, m: int = 100)
 
 def text_3g(n: int = 3_000_000_000) -> bytes:
     """3 Gbase uniform ACGT (seed 3000000000), generated in 70 Mbase chunks."""
-    rng = random.Random(3000000000)
-    ch = 70 * 1000000
-    return b"".join(rng.randbytes(min(ch, n - off)).translate(TBL) for off in range(0, n, ch))
+    return b"".join(text_chunks(n))
+
+
+def text_chunks(n: int):
+    """The bench texts as a stream of chunks (peak memory one chunk): the 3 Gbase
+    recipe (seed 3000000000, 70 Mbase chunks) for n = 3e9, otherwise
+    random.Random(n) in 2^27-base chunks (bench.py's other sizes)."""
+    if n == 3_000_000_000:
+        rng, ch = random.Random(3000000000), 70 * 1000000
+    else:
+        rng, ch = random.Random(n), 1 << 27      # getrandbits takes < 2^31 bits per call
+    for off in range(0, n, ch):
+        yield rng.randbytes(min(ch, n - off)).translate(TBL)
 
 
 def read_starts(n_text: int, num: int, m: int, seed: int) -> np.ndarray:
