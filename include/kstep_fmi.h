@@ -76,6 +76,17 @@ int32_t initResults(uint32_t numresults, void **results);
  * query on the device; results stay on the device until transferGPUtoCPU.
  * Returns void like the reference; kfmi_last_error() gives the status. */
 void    searchIndexGPU(void *index, void *queries, void *resIntervals);
+/* interface.h:30 / fmIndexCPUBaseline.c:157-292 (tags 100/101) and
+ * fmIndexCPUBaseline-AltCounters.c:145-310 (tags 200/201): the search on the
+ * host, same integers as the reference's CPU searchers.  Like the reference it
+ * is called by every thread of the caller's OpenMP parallel region
+ * (searchQueries.c:84-95) and shares the queries out with an orphaned
+ * `omp for schedule(static)` (GNU OpenMP); called outside a parallel region it
+ * runs on the calling thread.  Results go to the host results array; a later
+ * saveResults writes "<fn>.res.cpu" as the reference's CPU build does.
+ * Returns void like the reference; kfmi_last_error() gives the status (33:
+ * unsupported index or query size -- AltCounters indexes need m % K == 0). */
+void    searchIndexCPU(void *index, void *queries, void *resIntervals);
 /* interface.h:33 / fmIndexCPUBaseline.c:145-155 */
 int32_t freeIndex(void **index);
 /* interface.h:34 / common.c:313-322 */
@@ -101,7 +112,8 @@ int32_t  writeResults(const char *fn, uint32_t *results, uint32_t numqueries);
 int32_t  loadResults(const char *fn, void **results);
 int32_t  freeQueries(void **queries);
 int32_t  freeResults(void **results);
-/* common.c:324-341: "<fn>.res.gpu" */
+/* common.c:324-341: "<fn>.res.gpu", or "<fn>.res.cpu" when searchIndexCPU wrote
+ * the results last (the reference names the file by its build, CUDA or not) */
 int32_t  saveResults(const char *fn, void *results, void *index);
 char    *errorCommon(int32_t e);
 
@@ -147,6 +159,10 @@ int32_t     kfmi_device_pci_bus_id(int32_t device, char *buf, int32_t len);
 int32_t     kfmi_last_error(void);
 /* searchIndexGPU with a status return. */
 int32_t     kfmi_search(void *index, void *queries, void *results);
+/* searchIndexCPU in a parallel region of its own: nthreads threads (0:
+ * OMP_NUM_THREADS when set, else this process's CPUs -- affinity mask capped
+ * by the cgroup quota).  Returns the status. */
+int32_t     kfmi_search_cpu(void *index, void *queries, void *results, int32_t nthreads);
 /* ftab (Bowtie-style jump start; not in the reference): every backend looks
  * up [L, R) after the first `bases` bases of each query in a table of all
  * 4^bases codes (8 B each: 134 MB at 12) built on the device with the search's

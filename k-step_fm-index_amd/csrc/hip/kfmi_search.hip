@@ -1489,6 +1489,7 @@ extern "C" int32_t transferGPUtoCPU(void* results)
 {
   kfmi_res_t* r = (kfmi_res_t*) results;
   DeviceGuard dg;
+  if (r) r->origin = KFMI_RES_FROM_GPU;
   if (r && r->grp) return group_to_host(r);
   if (!r || !r->d_results) return KFMI_E_NOT_ON_DEVICE;
   DevCtx* ctx = nullptr;

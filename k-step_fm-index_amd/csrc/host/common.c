@@ -233,16 +233,11 @@ static void *lq_worker(void *arg)
  * CPU quota (the GPU boxes show 256 cores but grant 16) -- divided among the
  * ranks torchrun started on this host (LOCAL_WORLD_SIZE), 2 to 16.  Eight
  * ranks of 16 threads each on a 16-CPU quota would oversubscribe it 8x. */
-int32_t kfmi_host_threads(void)
+int32_t kfmi_process_cpus(void)
 {
-  const char *e = getenv("KFMI_HOST_THREADS");
-  long cpus = sysconf(_SC_NPROCESSORS_ONLN), ranks = 1;
+  long cpus = sysconf(_SC_NPROCESSORS_ONLN);
   cpu_set_t set;
   FILE *fp;
-  if (e) {
-    int v = atoi(e);
-    return v < 1 ? 1 : (v > 64 ? 64 : v);
-  }
   CPU_ZERO(&set);
   if (sched_getaffinity(0, sizeof(set), &set) == 0 && CPU_COUNT(&set) > 0 && CPU_COUNT(&set) < cpus)
     cpus = CPU_COUNT(&set);
@@ -255,6 +250,18 @@ int32_t kfmi_host_threads(void)
     }
     fclose(fp);
   }
+  return (int32_t) (cpus < 1 ? 1 : cpus);
+}
+
+int32_t kfmi_host_threads(void)
+{
+  const char *e = getenv("KFMI_HOST_THREADS");
+  long cpus, ranks = 1;
+  if (e) {
+    int v = atoi(e);
+    return v < 1 ? 1 : (v > 64 ? 64 : v);
+  }
+  cpus = kfmi_process_cpus();
   if ((e = getenv("LOCAL_WORLD_SIZE")) != NULL && atoi(e) > 0) ranks = atoi(e);
   cpus /= ranks;
   return (int32_t) (cpus < 2 ? 2 : (cpus > 16 ? 16 : cpus));
@@ -455,13 +462,15 @@ int32_t loadResults(const char *fn, void **results)
   return KFMI_SUCCESS;
 }
 
-/* common.c:324-341 (GPU build: "<fn>.res.gpu") */
+/* common.c:324-341: "<fn>.res.gpu" as the reference's GPU build names it, or
+ * "<fn>.res.cpu" (its CPU build) when searchIndexCPU wrote these results last */
 int32_t saveResults(const char *fn, void *results, void *index)
 {
   kfmi_res_t *r = (kfmi_res_t *) results;
   char name[1024];
   (void) index;
-  snprintf(name, sizeof(name), "%s.res.gpu", fn);
+  if (!r) return KFMI_E_BAD_ARGUMENT;
+  snprintf(name, sizeof(name), "%s.res.%s", fn, r->origin == KFMI_RES_FROM_CPU ? "cpu" : "gpu");
   return write_results64(name, r->h_results, r->num);
 }
 

@@ -71,7 +71,13 @@ typedef struct {
   uint32_t *d_results;     /* device copy (hipMalloc), NULL until transfer */
   int32_t   d_device;      /* device holding d_results (valid while d_results != NULL) */
   void     *grp;           /* per-device slices on a device group */
+  int32_t   origin;        /* who wrote h_results last: KFMI_RES_FROM_GPU (transferGPUtoCPU) or
+                              KFMI_RES_FROM_CPU (searchIndexCPU); saveResults names the file by it */
 } kfmi_res_t;
+enum { KFMI_RES_FROM_GPU = 0, KFMI_RES_FROM_CPU = 1 };
+
+/* CPUs this process may use: the affinity mask capped by the cgroup quota (common.c) */
+int32_t kfmi_process_cpus(void);
 
 typedef struct {
   uint64_t size;

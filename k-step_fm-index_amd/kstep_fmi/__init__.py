@@ -82,6 +82,8 @@ def load() -> ctypes.CDLL:
         "kfmi_device_pci_bus_id": (i32, [i32, ctypes.c_char_p, i32]),
         "kfmi_last_error": (i32, []),
         "kfmi_search": (i32, [vp, vp, vp]),
+        "searchIndexCPU": (None, [vp, vp, vp]),
+        "kfmi_search_cpu": (i32, [vp, vp, vp, i32]),
         "kfmi_last_timing": (i32, [ctypes.POINTER(ctypes.c_double)] * 3),
         "kfmi_load_index_tag": (i32, [ctypes.c_char_p, u32, pvp]),
         "kfmi_index_from_image": (i32, [vp, u64, pvp]),
@@ -505,6 +507,23 @@ def search_stream(index: Index, reads: np.ndarray, out: np.ndarray | None = None
     _check(load().kfmi_search_stream(index.ptr, reads.ctypes.data, n, m, out.ctypes.data, int(chunk)),
            "kfmi_search_stream")
     return out
+
+
+def search_cpu(index: Index, queries: Queries, results: Results, nthreads: int = 0) -> None:
+    """searchIndexCPU in its own OpenMP region (kfmi_search_cpu): the host search."""
+    _check(load().kfmi_search_cpu(index.ptr, queries.ptr, results.ptr, int(nthreads)), "searchIndexCPU")
+
+
+def search_cpu_array(index: Index, queries: np.ndarray, nthreads: int = 0) -> np.ndarray:
+    """One-shot host search of uint8 [N, m] reads (searchIndexCPU); uint32[2N]."""
+    q = Queries.from_array(queries)
+    r = Results.alloc(queries.shape[0])
+    try:
+        search_cpu(index, q, r, nthreads)
+        return r.array().copy()
+    finally:
+        q.close()
+        r.close()
 
 
 def search_array(index: Index, queries: np.ndarray, backend: str | None = None) -> np.ndarray:
