@@ -33,10 +33,13 @@ def test_library_exports_every_declared_symbol(kfmi_mod):
     assert not missing, missing
     for n in names:
         getattr(lib, n)   # resolvable through ctypes
-    # the reference's never-defined entry points are not exported,
-    # and the product has no CPU search path
-    for n in ("searchIndex", "errorIndex", "searchIndexCPU"):
+    # the reference's never-defined entry points are not exported;
+    # searchIndexCPU (interface.h:30) is, as the host search the reference's CPU
+    # driver calls (csrc/host/cpu_search.c, tests/test_cpu_search.py) -- never a
+    # fallback of the GPU entry points, which fail without a device
+    for n in ("searchIndex", "errorIndex"):
         assert n not in exported
+    assert "searchIndexCPU" in exported
 
 
 def test_error_strings(kfmi_mod):
@@ -136,3 +139,24 @@ def test_sais_against_bruteforce(kfmi_mod):
             for p in ("A", "C", "G", "T"):
                 res, _ = oracle.search(img, np.frombuffer(p.encode(), dtype=np.uint8).reshape(1, 1))
                 assert (int(res[0]), int(res[1])) == bf.interval(p.encode()), (n, alph, p)
+
+
+def test_gpu_entry_points_fail_without_a_device(kfmi_mod):
+    """No CPU fallback behind the GPU entry points: on a host without a HIP
+    device they return KFMI_E_NO_DEVICE (30) and write no results, even though
+    the library also carries searchIndexCPU."""
+    if kfmi_mod.device_count() > 0:
+        pytest.skip("a HIP device is visible")
+    rng = np.random.default_rng(3)
+    t = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, size=5001)]
+    idx = kfmi_mod.Index.build(t.tobytes(), k=2, d=64)
+    q = kfmi_mod.Queries.from_array(t[:1000].reshape(10, 100).copy())
+    r = kfmi_mod.Results.alloc(10)
+    with pytest.raises(kfmi_mod.KfmiError) as ei:
+        kfmi_mod.transfer_to_gpu(idx, q, r)
+    assert ei.value.code == 30
+    with pytest.raises(kfmi_mod.KfmiError):
+        kfmi_mod.search(idx, q, r)
+    assert not r.array().any()
+    for h in (q, r, idx):
+        h.close()
