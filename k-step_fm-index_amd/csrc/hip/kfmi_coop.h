@@ -31,7 +31,6 @@ namespace kfmi {
 // forward from entry b-1, block b-1's planes -- whose counter word (same
 // 128-B line, merged in L2 with the DMA's request) the lane owning that
 // interval end then loads itself.  No request needs a second line's chunk.
-__host__ __device__ constexpr int ilog2(int x) { int l = 0; while ((1 << (l + 1)) <= x) ++l; return l; }
 
 template <class G>
 struct CoopCfg {
@@ -42,22 +41,12 @@ struct CoopCfg {
   static constexpr int SLOT = TPR * 16;                 // LDS bytes per request slot
   static constexpr int MAXREQ = 128;                    // 64 L + up to 64 R
   static constexpr int MAXR = MAXREQ / RPR;             // staging rounds per K-step, at most
-  using Desc = typename std::conditional<(G::NC > 16), uint64_t, uint32_t>::type;   // b * NC + c
-  // Line geometries (one power-of-two line holds a request's planes and its
-  // counter chunk): a request is posted as its line's address with the planes'
-  // and the counter's 16-byte chunk numbers in the low bits (LCB bits each)
-  static constexpr int LINEB = G::EW * 4;
-  static constexpr int LCB = ilog2(LINEB > 16 ? LINEB / 16 : 1);
-  static constexpr bool LINE = !NBR && (G::MIDLINES || G::LAY == LAY_GRP || G::LAY == LAY_AC128) &&
-                               (LINEB & (LINEB - 1)) == 0 && LINEB >= 64 && 2 * LCB <= ilog2(LINEB);
-  // Pre-addressed issue (IdxArgs::coop_issue): each lane posts its own ends'
-  // addresses (64-bit) and the staging rounds only read them back -- all of a
-  // step's table reads in flight together instead of a read, a decode and a
-  // wait per round (measured neutral against the decoding rounds, DESIGN.md
-  // 5 "Coop issue"; both forms are parity-tested)
-  static constexpr bool PRE = NBR || LINE;
-  static constexpr int TABB = PRE ? 8 : (int) sizeof(Desc);
-  static constexpr int WAVE_LDS = MAXREQ * SLOT + MAXREQ * TABB;
+  // a request's descriptor b * NC + c, posted by its lane; the staging round
+  // that serves it decodes the chunk addresses (round 3 also measured lanes
+  // posting ready-made addresses instead: neutral, removed in round 4,
+  // DESIGN.md 5 "Coop issue")
+  using Desc = typename std::conditional<(G::NC > 16), uint64_t, uint32_t>::type;
+  static constexpr int WAVE_LDS = MAXREQ * SLOT + MAXREQ * (int) sizeof(Desc);
   static constexpr int WPB0 = 65536 / WAVE_LDS;
   static constexpr int WPB = WPB0 < 1 ? 1 : (WPB0 > 4 ? 4 : WPB0);   // waves per block
   static constexpr bool OK = (G::BMW % 4 == 0) && (G::EW % 4 == 0) && (G::BOFF % 4 == 0) &&
@@ -96,47 +85,6 @@ __device__ __forceinline__ const uint8_t* coop_chunk_addr(const IdxArgs& ix, uin
   } else {
     return base + eb + 4 * G::BMW + 2 * (c & ~7u);
   }
-}
-
-// NEIGHBOR geometries: request (b, c) as block b's planes address (below
-// 2^48, checked on the host: IdxArgs::coop_issue), bit 48 = counted forward
-// from block b-1, bits 56-63 = the counter chunk's signed offset from the
-// planes in 16-byte chunks (INTER: 2 .. 5, AC: -2 .. 3)
-static constexpr uint64_t NBR_ADDR = (1ull << 48) - 1;
-
-template <class G>
-__device__ __forceinline__ uint64_t nbr_post(const Where<G>& w)
-{
-  const int64_t off = ((int64_t) (reinterpret_cast<uintptr_t>(w.cnt) & ~(uintptr_t) 15) -
-                       (int64_t) reinterpret_cast<uintptr_t>(w.planes)) >> 4;
-  return reinterpret_cast<uint64_t>(w.planes) | ((uint64_t) (w.prev ? 1u : 0u) << 48) |
-         ((uint64_t) (uint8_t) (int8_t) off << 56);
-}
-
-// LINE geometries: request (b, c) as its line's address | planes chunk |
-// counter chunk << LCB (chunk numbers within the line, as coop_chunk_addr)
-template <class G>
-__device__ __forceinline__ uint64_t coop_line_post(const IdxArgs& ix, uint32_t b, uint32_t c)
-{
-  using C = CoopCfg<G>;
-  const uint8_t* base = reinterpret_cast<const uint8_t*>(ix.ent);
-  uint64_t lb;
-  uint32_t p0, cc;
-  if constexpr (G::MIDLINES) {
-    lb = (uint64_t) (b >> 1) * C::LINEB;
-    p0 = (b & 1u) * (G::BMW / 4);
-    cc = (G::MIDCNT + (c & ~3u)) / 4;
-  } else if constexpr (G::LAY == LAY_GRP) {
-    lb = ((uint64_t) b * G::NGRP + c / G::NCG) * C::LINEB;
-    p0 = 0;
-    cc = (G::BMW + ((c % G::NCG) & ~3u)) / 4;
-  } else {   // LAY_AC128
-    lb = (uint64_t) b * C::LINEB;
-    p0 = 0;
-    const bool e = ((b & 1u) != 0) == (c < (uint32_t) G::HALF);
-    cc = (G::BMW + (e ? G::HALF : 0) + ((c & (G::HALF - 1)) & ~3u)) / 4;
-  }
-  return reinterpret_cast<uint64_t>(base + lb) | p0 | ((uint64_t) cc << C::LCB);
 }
 
 template <class G>
@@ -256,8 +204,6 @@ __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, 
   uint8_t* wl = lds + wave * C::WAVE_LDS;
   using Desc = typename C::Desc;
   Desc* tab = reinterpret_cast<Desc*>(wl + C::MAXREQ * C::SLOT);
-  uint64_t* post = reinterpret_cast<uint64_t*>(wl + C::MAXREQ * C::SLOT);   // PRE: request addresses
-  const bool pre = C::PRE && ix.coop_issue != 0;                            // wave-uniform
   const uint64_t q0 = ((uint64_t) blockIdx.x * C::WPB + wave) * 64;
   if (q0 >= num) return;                       // whole wave idle (wave-uniform)
   const uint64_t q = q0 + lane;
@@ -337,7 +283,6 @@ __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, 
       bool eL = false, eR = false, pL = false, pR = false;
       const uint32_t* acL = nullptr;
       const uint32_t* acR = nullptr;
-      uint64_t postL = 0, postR = 0;
       if constexpr (C::NBR) {   // each end's counter word, loaded by its own lane after the DMA
         Where<G> wL = locate<G>(ix, bl, c);
         Where<G> wR = locate<G>(ix, br, c);
@@ -349,19 +294,9 @@ __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, 
         eR = wR.e;
         pR = wR.prev;
         acR = wR.cnt;
-        postL = nbr_post<G>(wL);
-        postR = nbr_post<G>(wR);
-      } else if constexpr (C::LINE) {
-        postL = coop_line_post<G>(ix, bl, c);
-        postR = coop_line_post<G>(ix, br, c);
       }
-      if (pre) {
-        post[lane] = postL;
-        if (needR) post[slotR] = postR;
-      } else {
-        tab[lane] = (Desc) bl * (Desc) G::NC + c;
-        if (needR) tab[slotR] = (Desc) br * (Desc) G::NC + c;
-      }
+      tab[lane] = (Desc) bl * (Desc) G::NC + c;
+      if (needR) tab[slotR] = (Desc) br * (Desc) G::NC + c;
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       uint32_t sbL = 0, sbR = 0;
       if constexpr (G::LAY == LAY_PACKED) {
@@ -369,40 +304,7 @@ __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, 
         sbR = ix.sb[(uint64_t) (br >> S) * G::NC + c];
       }
       const uint32_t rounds = (nreq + C::RPR - 1) / C::RPR;
-      if constexpr (C::PRE) {
-        if (pre) {
-          /* every round's post read back at once, then the rounds' DMA issued
-           * back to back (requests s >= nreq of the last round masked off) */
-          uint64_t pe[C::MAXR];
-#pragma unroll
-          for (int r = 0; r < C::MAXR; ++r) pe[r] = post[r * C::RPR + g];
-#pragma unroll
-          for (int r = 0; r < C::MAXR; ++r) {
-            if ((uint32_t) r >= rounds) break;
-            const uint32_t s = (uint32_t) r * C::RPR + g;
-            const uint64_t e = pe[r];
-            const uint8_t* p = nullptr;
-            if constexpr (C::NBR) {
-              const uint8_t* pl = reinterpret_cast<const uint8_t*>(e & NBR_ADDR);
-              if (k < C::BC) p = pl + 16 * k;
-              else if ((e >> 48) & 1u) {
-                if (k < 2 * C::BC) p = pl - G::EW * 4 + 16 * (k - C::BC);                  // block b-1
-              } else if (k == C::BC) {
-                p = pl + 16 * (int) (int8_t) (e >> 56);                                     // counter chunk
-              }
-            } else {
-              const uint8_t* ln = reinterpret_cast<const uint8_t*>(e & ~(uint64_t) (C::LINEB - 1));
-              const uint32_t cm = (1u << C::LCB) - 1u;
-              if (k < C::BC) p = ln + 16 * (((uint32_t) e & cm) + k);
-              else if (k == C::BC) p = ln + 16 * (((uint32_t) (e >> C::LCB)) & cm);
-            }
-            if (s < nreq && p)
-              __builtin_amdgcn_global_load_lds((const void*) p,
-                                               (__attribute__((address_space(3))) void*) (wl + r * 1024), 16, 0, 0);
-          }
-        }
-      }
-      for (uint32_t r = 0; !pre && r < rounds; ++r) {
+      for (uint32_t r = 0; r < rounds; ++r) {
         const uint32_t s = r * C::RPR + g;
         if constexpr (C::NBR) {
           if (s < nreq && k < 2 * C::BC) {

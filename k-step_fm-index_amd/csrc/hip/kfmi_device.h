@@ -109,7 +109,6 @@ struct IdxArgs {
   const uint32_t* __restrict__ ent;   // entries / lines (layout per backend)
   const uint32_t* __restrict__ sb;    // packed layout: superblock counters [nsb][NC]
   uint32_t bwtsize;
-  uint32_t nt_from;                   // K-steps >= nt_from load index lines non-temporally
   DollarArgs dl;
   // ftab (Bowtie-style jump start): [L, R) after the first ftab_steps K-steps,
   // indexed by the low 2*K*ftab_steps bits of the query's code stream; null = off
@@ -129,13 +128,7 @@ struct IdxArgs {
   // beyond the translation reach (~3.5 GB) stalls on translation; 16-32 pages
   // per instruction do not (profiles/r02/gather_mask_r2ag.jsonl)
   uint32_t split;
-  // coop kernels: 1 = pre-addressed staging rounds where the geometry allows
-  // (CoopCfg::PRE), 0 = each round decodes its request (KFMI_COOP_ISSUE)
-  uint32_t coop_issue;
 };
-
-// IdxArgs::split: KFMI_SPLIT forced this form (no per-geometry choice)
-#define KFMI_SPLIT_FORCED 0x100u
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 typedef unsigned int v2u __attribute__((ext_vector_type(2)));

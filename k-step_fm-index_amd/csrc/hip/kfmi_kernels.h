@@ -27,16 +27,16 @@ namespace kfmi {
 
 
 /* Both ends' blocks of one step: block(L), and block(R) only when it differs. */
-template <class G, bool NT, int QPT>
+template <class G, int QPT>
 __device__ __forceinline__ void fetch_ends(const IdxArgs& ix, const uint32_t (&L)[QPT], const uint32_t (&R)[QPT],
                                            const uint32_t (&c)[QPT], Blk<G> (&kl)[QPT], Blk<G> (&kr)[QPT])
 {
 #pragma unroll
-  for (int i = 0; i < QPT; ++i) fetch_block<G, NT>(ix, L[i] / (uint32_t) G::D, c[i], kl[i]);
+  for (int i = 0; i < QPT; ++i) fetch_block<G>(ix, L[i] / (uint32_t) G::D, c[i], kl[i]);
 #pragma unroll
   for (int i = 0; i < QPT; ++i) {
     const uint32_t br = R[i] / (uint32_t) G::D;
-    if (br != kl[i].b) fetch_block<G, NT>(ix, br, c[i], kr[i]);
+    if (br != kl[i].b) fetch_block<G>(ix, br, c[i], kr[i]);
     else kr[i] = kl[i];
   }
 }
@@ -51,10 +51,10 @@ __device__ __forceinline__ void fetch_ends(const IdxArgs& ix, const uint32_t (&L
  * A part no lane of a group needs (R where every R shares L's block, the
  * b-1 planes where no lane counts forward) is branched over.  Forms (the
  * SPLIT template value): 8 = one group, 7 = two 32-lane groups (32 pages per
- * instruction at most), 6 = four 16-lane groups.  3 Gbase, 10M x 100 bp,
- * against the C++ four-group split (profiles/r03/sweep_r3n.jsonl): task (tag
- * 101, 4.5 GB) 12.52 -> 10.93 ms with 7 (6: 11.28, 8: 16.11 -- past the
- * translation reach one group stalls); task-ac (tag 201, 3 GB) 11.47 ->
+ * instruction at most).  3 Gbase, 10M x 100 bp, against the C++ four-group
+ * split (profiles/r03/sweep_r3n.jsonl): task (tag 101, 4.5 GB) 12.52 ->
+ * 10.93 ms with 7 (four 16-lane groups: 11.28, removed in round 4; 8: 16.11
+ * -- past the translation reach one group stalls); task-ac (tag 201, 3 GB) 11.47 ->
  * 9.51 (8: 9.79); task-mid 9.46 -> 9.40; 150 bp task-ac 17.01 -> 14.43,
  * task-mid 14.41 -> 14.34.  Issuing every part unconditionally, empty exec
  * or not, cost 15-19 % on task / task-ac (sweep_r3m.jsonl): an instruction
@@ -81,9 +81,6 @@ struct X4 {
   KFMI_X4_SL("r" T)
 #define KFMI_X4_G1 "s_mov_b64 %[gm], -1\n" KFMI_X4_BODY("a")
 #define KFMI_X4_G2 "s_bfm_b64 %[gm], 32, 0\n" KFMI_X4_BODY("a") "s_bfm_b64 %[gm], 32, 32\n" KFMI_X4_BODY("b")
-#define KFMI_X4_G4                                                                          \
-  "s_bfm_b64 %[gm], 16, 0\n" KFMI_X4_BODY("a") "s_bfm_b64 %[gm], 16, 16\n" KFMI_X4_BODY("b") \
-  "s_bfm_b64 %[gm], 16, 32\n" KFMI_X4_BODY("c") "s_bfm_b64 %[gm], 16, 48\n" KFMI_X4_BODY("d")
 #define KFMI_X4_ASM(GROUPS) "s_mov_b64 %[sv], exec\n" GROUPS "s_mov_b64 exec, %[sv]\ns_waitcnt vmcnt(0)\n"
 #define KFMI_X4_OUT                                                                                          \
   [l0] "=&v"(l0), [l1] "=&v"(l1), [r0] "=&v"(r0), [r1] "=&v"(r1), [cl] "=&v"(cl), [cr] "=&v"(cr), [sv] "=&s"(sv), \
@@ -110,7 +107,7 @@ template <class G, int SPLIT>
 __device__ __forceinline__ void fetch_ends_x4(const IdxArgs& ix, uint32_t L, uint32_t R, uint32_t c, Blk<G>& kl,
                                               Blk<G>& kr)
 {
-  static_assert(SPLIT >= 6 && SPLIT <= 8, "fetch form: 6, 7, 8 = four, two, one lane group(s)");
+  static_assert(SPLIT == 7 || SPLIT == 8, "fetch form: 7, 8 = two, one lane group(s)");
   const uint32_t bl = L / (uint32_t) G::D, br = R / (uint32_t) G::D;
   Where<G> wl = locate<G>(ix, bl, c);
   Where<G> wr = locate<G>(ix, br, c);
@@ -129,10 +126,8 @@ __device__ __forceinline__ void fetch_ends_x4(const IdxArgs& ix, uint32_t L, uin
 #define KFMI_X4_PREV_R(T) KFMI_X4_PREV_R_ON(T)
     if constexpr (SPLIT == 8)
       asm volatile(KFMI_X4_ASM(KFMI_X4_G1) : KFMI_X4_OUTP : KFMI_X4_INP : "memory", "scc");
-    else if constexpr (SPLIT == 7)
-      asm volatile(KFMI_X4_ASM(KFMI_X4_G2) : KFMI_X4_OUTP : KFMI_X4_INP : "memory", "scc");
     else
-      asm volatile(KFMI_X4_ASM(KFMI_X4_G4) : KFMI_X4_OUTP : KFMI_X4_INP : "memory", "scc");
+      asm volatile(KFMI_X4_ASM(KFMI_X4_G2) : KFMI_X4_OUTP : KFMI_X4_INP : "memory", "scc");
 #undef KFMI_X4_PREV_L
 #undef KFMI_X4_PREV_R
     const v4u pa = needR ? q0 : p0, pb = needR ? q1 : p1;
@@ -145,10 +140,8 @@ __device__ __forceinline__ void fetch_ends_x4(const IdxArgs& ix, uint32_t L, uin
 #define KFMI_X4_PREV_R(T)
     if constexpr (SPLIT == 8)
       asm volatile(KFMI_X4_ASM(KFMI_X4_G1) : KFMI_X4_OUT : KFMI_X4_IN : "memory", "scc");
-    else if constexpr (SPLIT == 7)
-      asm volatile(KFMI_X4_ASM(KFMI_X4_G2) : KFMI_X4_OUT : KFMI_X4_IN : "memory", "scc");
     else
-      asm volatile(KFMI_X4_ASM(KFMI_X4_G4) : KFMI_X4_OUT : KFMI_X4_IN : "memory", "scc");
+      asm volatile(KFMI_X4_ASM(KFMI_X4_G2) : KFMI_X4_OUT : KFMI_X4_IN : "memory", "scc");
 #undef KFMI_X4_PREV_L
 #undef KFMI_X4_PREV_R
   }
@@ -169,7 +162,6 @@ __device__ __forceinline__ void fetch_ends_x4(const IdxArgs& ix, uint32_t L, uin
 #undef KFMI_X4_BODY
 #undef KFMI_X4_G1
 #undef KFMI_X4_G2
-#undef KFMI_X4_G4
 #undef KFMI_X4_ASM
 #undef KFMI_X4_OUT
 #undef KFMI_X4_IN
@@ -180,22 +172,26 @@ __device__ __forceinline__ void fetch_ends_x4(const IdxArgs& ix, uint32_t L, uin
 #undef KFMI_X4_PREV_L_ON
 #undef KFMI_X4_PREV_R_ON
 
-/* SPLIT > 1: the same loads as SPLIT exec-masked groups of 64/SPLIT lanes, so
- * one wave instruction touches at most 64/SPLIT pages (IdxArgs::split). */
-template <class G, bool NT, int QPT, int SPLIT>
+/* The fetch forms (the SPLIT template value, launch_task): 1 = the C++ fetch
+ * in one group; 4 = the same loads as four exec-masked 16-lane groups, so one
+ * wave instruction touches at most 16 pages (IdxArgs::split); 7 / 8 = the asm
+ * fetch in two / one group(s) (X4 geometries only). */
+template <class G, int QPT, int SPLIT>
 __device__ __forceinline__ void fetch_ends_split(const IdxArgs& ix, const uint32_t (&L)[QPT],
                                                  const uint32_t (&R)[QPT], const uint32_t (&c)[QPT],
                                                  Blk<G> (&kl)[QPT], Blk<G> (&kr)[QPT])
 {
-  if constexpr (SPLIT >= 6 && !NT && QPT == 1 && X4<G>::OK) {
+  static_assert(SPLIT == 1 || SPLIT == 4 || ((SPLIT == 7 || SPLIT == 8) && QPT == 1 && X4<G>::OK),
+                "fetch form: 1 / 4 (C++ fetch), 7 / 8 (asm fetch, X4 geometries)");
+  if constexpr (SPLIT >= 7) {
     fetch_ends_x4<G, SPLIT>(ix, L[0], R[0], c[0], kl[0], kr[0]);
   } else if constexpr (SPLIT == 1) {
-    fetch_ends<G, NT, QPT>(ix, L, R, c, kl, kr);
-  } else {   /* 4 (and 6-8 where the asm form does not apply): four 16-lane groups */
+    fetch_ends<G, QPT>(ix, L, R, c, kl, kr);
+  } else {
     const int grp = (int) (threadIdx.x & 63) / 16;
 #pragma unroll
     for (int g = 0; g < 4; ++g)
-      if (grp == g) fetch_ends<G, NT, QPT>(ix, L, R, c, kl, kr);
+      if (grp == g) fetch_ends<G, QPT>(ix, L, R, c, kl, kr);
   }
 }
 
@@ -273,10 +269,7 @@ __global__ __launch_bounds__(256) void task_kernel(IdxArgs ix, const uint32_t* _
       for (int i = 0; i < QPT; ++i) c[i] = (word[i] >> (2 * G::K * j)) & (uint32_t) (G::NC - 1);
       if constexpr (G::SMALL) {
         Blk<G> kl[QPT], kr[QPT];
-        if (w * SPW + j >= ix.nt_from)   /* wave-uniform: deep steps stream non-temporally */
-          fetch_ends_split<G, true, QPT, SPLIT>(ix, L, R, c, kl, kr);
-        else
-          fetch_ends_split<G, false, QPT, SPLIT>(ix, L, R, c, kl, kr);
+        fetch_ends_split<G, QPT, SPLIT>(ix, L, R, c, kl, kr);
 #pragma unroll
         for (int i = 0; i < QPT; ++i) {
           uint32_t sx[2 * G::K];
@@ -500,13 +493,6 @@ struct SearchLaunch {
   uint32_t rem;
 };
 
-static inline int task_qpt(void)
-{
-  const char* e = getenv("KFMI_QPT");
-  int v = e ? atoi(e) : 1;
-  return v == 2 ? 2 : 1;
-}
-
 template <class G, int SPLIT>
 static void launch_task_split(const SearchLaunch& a)
 {
@@ -521,10 +507,6 @@ static void launch_task_split(const SearchLaunch& a)
     else
       hipLaunchKernelGGL((task_kernel<G, 1, 16, SPLIT>), dim3((uint32_t) blocks), dim3(256), lds, a.st, a.ix, a.qp,
                          a.ascii, a.m, a.num, a.steps, a.nwords, a.res);
-  } else if (SPLIT == 1 && task_qpt() == 2) {
-    const uint64_t blocks = (a.num + 511) / 512;
-    hipLaunchKernelGGL((task_kernel<G, 2, 0>), dim3((uint32_t) blocks), dim3(256), 0, a.st, a.ix, a.qp, a.ascii,
-                       a.m, a.num, a.steps, a.nwords, a.res);
   } else {
     const uint64_t blocks = (a.num + 255) / 256;
     hipLaunchKernelGGL((task_kernel<G, 1, 0, SPLIT>), dim3((uint32_t) blocks), dim3(256), 0, a.st, a.ix, a.qp,
@@ -535,19 +517,13 @@ static void launch_task_split(const SearchLaunch& a)
 template <class G>
 static hipError_t launch_task(const SearchLaunch& a)
 {
-  /* the split only exists for the one-line-per-block path (d <= 128 at K=2) */
+  /* the split only exists for the one-line-per-block path (d <= 128 at K=2);
+   * one fetch form per (geometry, table size class): the asm fetch in one group
+   * below 2 GB, two groups above (X4 geometries); else the C++ fetch, in four
+   * groups where split_for asks for them */
   if constexpr (G::SMALL) {
-    const uint32_t want = a.ix.split & ~KFMI_SPLIT_FORCED;
-    if (a.ix.split & KFMI_SPLIT_FORCED) {   /* KFMI_SPLIT: the form as given */
-      switch (want) {
-        case 4: launch_task_split<G, 4>(a); return hipGetLastError();
-        case 6: launch_task_split<G, 6>(a); return hipGetLastError();
-        case 7: launch_task_split<G, 7>(a); return hipGetLastError();
-        case 8: launch_task_split<G, 8>(a); return hipGetLastError();
-        default: launch_task_split<G, 1>(a); return hipGetLastError();
-      }
-    }
-    if constexpr (X4<G>::OK) {   /* asm fetch: two groups on split tables, else one */
+    const uint32_t want = a.ix.split;
+    if constexpr (X4<G>::OK) {
       if (want == 1) launch_task_split<G, 8>(a);
       else launch_task_split<G, 7>(a);
       return hipGetLastError();

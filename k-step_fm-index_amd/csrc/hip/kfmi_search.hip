@@ -1025,15 +1025,15 @@ int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx, kfmi_dev_
  * profiles/r02/sweep_split_r2ah.jsonl, sweep_split150_r2aj.jsonl; the asm
  * forms: profiles/r03/sweep_r3n.jsonl, sweep150_r3n.jsonl.  The ftab lookup
  * (one gather per read) is never split: that measured slower.
- * KFMI_SPLIT forces a form (KFMI_SPLIT_FORCED set): 1 / 4 = the C++ fetch in
- * one / four groups, 6 / 7 / 8 = the asm fetch in four / two / one group(s)
- * where it applies. */
+ * KFMI_SPLIT=1|2|4 (a test knob) answers in place of the table size, so that
+ * a small test index runs the fetch form a table of that size class gets
+ * (launch_task: one form per geometry and class). */
 static uint32_t split_for(uint64_t table_bytes, int layout)
 {
   const char* e = getenv("KFMI_SPLIT");
   if (e && *e) {
     const int v = atoi(e);
-    return KFMI_SPLIT_FORCED | ((v == 4 || (v >= 6 && v <= 8)) ? (uint32_t) v : 1u);
+    return (v == 2 || v == 4) ? (uint32_t) v : 1u;
   }
   if (table_bytes > 3500000000ull) return 4u;
   if (table_bytes > 2000000000ull) return (layout == LAY_MID || layout == LAY_MIDAC) ? 2u : 4u;
@@ -1046,8 +1046,6 @@ IdxArgs idx_args(const kfmi_dev_index* di)
   ix.ent = di->ent;
   ix.sb = di->sb;
   ix.bwtsize = di->bwtsize;
-  const char* e = getenv("KFMI_NT_FROM");   /* K-step from which index loads are non-temporal */
-  ix.nt_from = e ? (uint32_t) atoi(e) : 0xFFFFFFFFu;
   ix.dl = di->dl;
   ix.ftab = nullptr;
   ix.ftab_steps = 0;
@@ -1057,14 +1055,6 @@ IdxArgs idx_args(const kfmi_dev_index* di)
   ix.rtab = nullptr;
   ix.rem = 0;
   ix.split = split_for(di->ent_bytes + di->sb_bytes, di->layout);
-  e = getenv("KFMI_COOP_ISSUE");   /* 0: coop staging rounds decode their requests */
-  ix.coop_issue = (e && *e) ? (uint32_t) (atoi(e) != 0) : 1u;
-  /* the posts keep flags above bit 47 of the address (reference layouts,
-   * kfmi_coop.h nbr_post) or chunk numbers below the line size (line layouts,
-   * coop_line_post, lines of <= 256 B): a table mapped above 2^48 or not
-   * 256-B aligned decodes its rounds */
-  if ((uint64_t) (uintptr_t) di->ent + di->ent_bytes >= (1ull << 48) || ((uintptr_t) di->ent & 255u) != 0)
-    ix.coop_issue = 0;
   return ix;
 }
 

@@ -338,7 +338,12 @@ int32_t kfmi_index_ref_walk(const char *text, const uint32_t *sa, uint64_t n, ui
   int64_t position, refpos;
   kfmi_fmi_t *f = NULL;
   int32_t err = KFMI_E_ALLOCATING_BWT;
-  if (k < 1 || k > KFMI_MAX_STEPS || d == 0 || d % 32 || rows > 0x7FFFFFFFull || rows < k) return KFMI_E_BAD_ARGUMENT;
+  /* rows up to the builders' own limit (n + 1 <= 2^32 - 2): positions are
+   * int64 and the chunk counters u32.  The reference's int32 mod() (B8) goes
+   * wrong above 2^31 rows only for the last K - 1 walk steps, where it reads
+   * ref[-1] into a '$' row that :505-509 overwrites with 'A' -- the bytes
+   * ref_mod gives -- so no cap of its own is needed here. */
+  if (k < 1 || k > KFMI_MAX_STEPS || d == 0 || d % 32 || rows > 0xFFFFFFFEull || rows < k) return KFMI_E_BAD_ARGUMENT;
   for (s = 0; s < k; s++) {
     bwt[s] = (uint8_t *) malloc(rows);
     if (!bwt[s]) goto done;

@@ -3,8 +3,9 @@
  * built alone with AddressSanitizer + UBSan (gcc), driven over the golden
  * fixtures: index load / transforms / save, the host builder with SA samples,
  * query and result I/O, sample files, and the error paths (missing, wrong-tag
- * and truncated files).  The HIP layer is replaced by the stubs below (the
- * handles never reach a device here).
+ * and truncated files), and searchIndexCPU on every tag against the
+ * reference searchers' result files.  The HIP layer is replaced by the stubs
+ * below (the handles never reach a device here).
  *
  *   host_asan <golden_dir> <tmp_dir> <case> <k> <d> <m> <num>
  * Prints "OK <checks>" and exits 0 when every check passes.
@@ -27,6 +28,9 @@ int32_t kfmi_build_index_gpu_sa(const char *t, uint64_t n, uint32_t k, uint32_t 
 { (void) t; (void) n; (void) k; (void) d; (void) r; (void) i; return KFMI_E_NO_DEVICE; }
 int32_t kfmi_build_index_gpu(const char *t, uint64_t n, uint32_t k, uint32_t d, int32_t h, void **i)
 { (void) h; return kfmi_build_index_gpu_sa(t, n, k, d, 0, i); }
+static __thread int32_t last_error;
+void kfmi_set_last_error(int32_t e) { last_error = e; }
+int32_t kfmi_last_error(void) { return last_error; }
 
 static int checks = 0, failures = 0;
 #define CHECK(cond, ...) do { checks++; if (!(cond)) { failures++; fprintf(stderr, "FAIL %s:%d: ", __FILE__, __LINE__); \
@@ -185,6 +189,25 @@ int main(int argc, char **argv)
     free(w);
   }
   CHECK(kfmi_pack_queries(NULL, 1, 4, NULL) == KFMI_E_BAD_ARGUMENT, "pack null");
+
+  /* 7. searchIndexCPU on every tag: results files equal the reference searchers' */
+  for (tag = 100; tag <= 201; tag += (tag == 101 ? 99 : 1)) {
+    void *x = NULL, *qs = NULL, *rs = NULL;
+    size_t l1 = 0, l2 = 0;
+    unsigned char *a, *b;
+    snprintf(p, sizeof p, "%s/%s/k%u_d%u.%u.fmi", g, cs, k, d, tag);
+    snprintf(q, sizeof q, "%s/%s/q%u.qry", g, cs, m);
+    CHECK(loadIndex(p, &x) == 0 && loadQueries(q, m, num, &qs) == 0 && initResults(num, &rs) == 0, "cpu inputs");
+    CHECK(kfmi_search_cpu(x, qs, rs, 3) == 0, "searchIndexCPU tag %u", tag);
+    snprintf(p, sizeof p, "%s/cpu%u", tmp, tag);
+    CHECK(saveResults(p, rs, x) == 0, "save cpu results");
+    snprintf(p, sizeof p, "%s/cpu%u.res.cpu", tmp, tag);
+    snprintf(q, sizeof q, "%s/%s/k%u_d%u.q%u.%s.res", g, cs, k, d, m, tag < 200 ? "cpu" : "cpuac");
+    a = slurp(q, &l1); b = slurp(p, &l2);
+    CHECK(a && b && l1 == l2 && !memcmp(a, b, l1), "cpu results bytes tag %u", tag);
+    free(a); free(b);
+    freeResults(&rs); freeQueries(&qs); freeIndex(&x);
+  }
 
   freeIndex(&idx); freeIndex(&t101); freeIndex(&t200); freeIndex(&t201);
   printf("%s %d checks, %d failures\n", failures ? "FAILED" : "OK", checks, failures);

@@ -20,7 +20,7 @@ def binary(tmp_path_factory):
         pytest.skip("gcc not available")
     out = tmp_path_factory.mktemp("asan") / "host_asan"
     srcs = sorted(str(p) for p in (PKG / "csrc" / "host").glob("*.c"))
-    cmd = ["gcc", "-g", "-O1", "-std=gnu11", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
+    cmd = ["gcc", "-g", "-O1", "-std=gnu11", "-fopenmp", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
            "-fno-sanitize-recover=undefined", "-o", str(out), str(HARNESS)] + srcs
     subprocess.run(cmd, check=True, capture_output=True, text=True)
     return out

@@ -77,19 +77,13 @@ def k4(kfmi_mod):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("issue", ["1", "0"])
 @pytest.mark.parametrize("split", ["1", "4"])
 @pytest.mark.parametrize("backend", GRP)
-def test_grp_matches_oracle_and_k2(kfmi_mod, oracle_mod, k4, backend, split, issue, monkeypatch):
+def test_grp_matches_oracle_and_k2(kfmi_mod, oracle_mod, k4, backend, split, monkeypatch):
     """split 4: per-lane gathers as 4 exec-masked groups (the default for the
-    96 GB GRP table at 3 Gbase; the coop kernel ignores it).  issue 0: the
-    coop kernel's staging rounds decode their requests instead of reading
-    pre-computed line addresses (KFMI_COOP_ISSUE; the task kernel ignores it)."""
+    96 GB GRP table at 3 Gbase; the coop kernel ignores it)."""
     K = kfmi_mod
-    if issue == "0" and backend != "coop-grp":
-        pytest.skip("KFMI_COOP_ISSUE applies to the coop kernel only")
     monkeypatch.setenv("KFMI_SPLIT", split)
-    monkeypatch.setenv("KFMI_COOP_ISSUE", issue)
     t, i4, i2 = k4
     for m, n in ((100, 20_000), (16, 4_000), (4, 2_000), (256, 1_000), (300, 1_000), (8, 500), (102, 1_001),
                  (150, 777)):
