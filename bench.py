@@ -33,7 +33,7 @@ import kstep_fmi as K  # noqa: E402
 from kstep_fmi import synth  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-PROBE_CEILING_GLINES = 52.7   # gather_probe, 3 GB table, one random line per lane (profiles/r01)
+PROBE_CEILING_GLINES = 56.0   # gather_probe, 200 MB table (Infinity-Cache resident), profiles/r03/gather_probe_r3g.jsonl
 
 
 def log(*a):
@@ -549,36 +549,86 @@ def cpu_reference_baseline(idx, reads, ns, k, d, thr, res_gpu):
 def probe_leg() -> dict | None:
     """The random-line request ceiling on this box, measured beside the kernel:
     bin/gather_probe (csrc/tools/gather_probe.hip) reads uniformly random lines
-    of a 3 GB table -- independent per lane, cooperative, and dependent chains
-    (the LF shape) -- and reports lines/s.  Run as a child process while this
-    one idles.  None when the tool is missing or fails."""
+    -- independent per lane, cooperative, and dependent chains (the LF shape) --
+    of a 3 GB table (every request an L2 and Infinity-Cache miss: HBM) and of
+    a 200 MB one (past the L2s, inside the 256 MB Infinity Cache: the request
+    path's own limit, with no DRAM behind it).  The LF kernel's requests are a
+    mix of both (its early steps' lines stay in the caches), so the ceiling it
+    is held against is the larger rate, the Infinity-Cache-resident one
+    (DESIGN.md 5).  Run as a child process while this one idles.  None when the
+    tool is missing or fails."""
     import subprocess
     exe = ROOT / "k-step_fm-index_amd" / "bin" / "gather_probe"
     if not exe.exists():
         return None
-    try:
-        p = subprocess.run([str(exe), "3", "512"], capture_output=True, text=True, timeout=300)
-    except (OSError, subprocess.SubprocessError):
-        return None
-    if p.returncode != 0:
-        return None
-    rows, table = [], None
-    for ln in p.stdout.splitlines():
+    out = {}
+    for gb, key in (("3", "hbm_3GB"), ("0.2", "infinity_cache_200MB")):
         try:
-            d = json.loads(ln)
-        except ValueError:
-            continue
-        if "table_bytes" in d:
-            table = d["table_bytes"]
-        elif "kind" in d and table == 3_000_000_000:
-            rows.append(d)
-    if not rows:
+            p = subprocess.run([str(exe), gb, "512"], capture_output=True, text=True, timeout=300)
+        except (OSError, subprocess.SubprocessError):
+            return None
+        if p.returncode != 0:
+            return None
+        rows, table = [], None
+        for ln in p.stdout.splitlines():
+            try:
+                d = json.loads(ln)
+            except ValueError:
+                continue
+            if "table_bytes" in d:
+                table = d["table_bytes"]
+            elif "kind" in d and table is not None:
+                rows.append(d)
+        if not rows:
+            return None
+        best = max(rows, key=lambda x: x["Glines_s"])
+        chain = [x for x in rows if x["kind"].startswith("chain")]
+        out[key] = {"best_G_lines_per_s": best["Glines_s"], "best_kind": f"{best['kind']} {best['line_B']} B",
+                    "chain_G_lines_per_s": max(x["Glines_s"] for x in chain) if chain else None,
+                    "table_bytes": table, "rows": rows}
+    ceil_key = max(out, key=lambda k: out[k]["best_G_lines_per_s"])
+    return dict(out, ceiling_G_lines_per_s=out[ceil_key]["best_G_lines_per_s"], ceiling_from=ceil_key)
+
+
+VARIANTS_PMC = ROOT / "profiles" / "r04" / "traffic_variants.json"
+
+
+def load_variants_pmc(a) -> dict | None:
+    """Per-backend fabric read requests per launch (TCC_EA0_RDREQ) of the 3 Gbase
+    / 10M x 100 bp LF kernels, from the committed PMC pass
+    (scripts/traffic_variants.py over scripts/pmc_variants.py under rocprofv3);
+    None unless it was taken on this bench's config."""
+    try:
+        tv = json.loads(VARIANTS_PMC.read_text())
+    except (OSError, ValueError):
         return None
-    best = max(rows, key=lambda x: x["Glines_s"])
-    chain = [x for x in rows if x["kind"].startswith("chain")]
-    return {"best_G_lines_per_s": best["Glines_s"], "best_kind": f"{best['kind']} {best['line_B']} B",
-            "chain_G_lines_per_s": max(x["Glines_s"] for x in chain) if chain else None,
-            "table_bytes": 3_000_000_000, "rows": rows}
+    cfg = tv.get("config", {})
+    if (cfg.get("queries") != a.queries or cfg.get("ref_size") != a.ref_size or cfg.get("qlen") != a.qlen
+            or cfg.get("d") != a.d):
+        return None
+    return tv
+
+
+def variant_roofline(blocks: int, b_lf: int, lf_ms: float, a, backend: str, pmc: dict | None,
+                     ceiling: float, k: int | None = None) -> dict:
+    """Roofline of one backend's LF launch on the bench batch: SURVEY 8(d)
+    algorithmic bytes (K*d/4 + 4 B per distinct block) over its HIP-event time,
+    against the HBM peak; and, when the committed PMC pass holds this backend,
+    its fabric read requests per launch and per query, their rate, and that
+    rate against the random-line request ceiling."""
+    bytes_alg = blocks * b_lf
+    out = {"distinct_blocks": int(blocks), "bytes_per_block": b_lf, "bytes_per_launch": int(bytes_alg),
+           "achieved_GBs": round(bytes_alg / (lf_ms / 1e3) / 1e9, 1),
+           "frac": round(bytes_alg / (lf_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
+    row = (pmc or {}).get("backends", {}).get(f"{backend}@k{k or a.k}")
+    if row:
+        req = row["rdreq_per_launch"]
+        out.update({"fabric_read_requests_per_launch": req, "line_requests_per_query": round(req / a.queries, 2),
+                    "line_requests_G_per_s": round(req / (lf_ms / 1e3) / 1e9, 2),
+                    "line_request_frac": round(req / (lf_ms / 1e3) / 1e9 / ceiling, 3),
+                    "l2_requests_per_launch": row.get("tcc_req_per_launch"),
+                    "pmc_kernel_ms": row.get("kernel_ms_under_pmc"), "pmc_source": pmc.get("source")})
+    return out
 
 
 def config1_leg(backend: str, thr: int, steps: int = 5) -> dict:
@@ -725,7 +775,7 @@ def config5_leg(D, idx, text: bytes, backend: str, qlen: int, nq: int, steps: in
 
 
 def kstep4_leg(D, text: bytes, reads: np.ndarray, res: np.ndarray, img2, steps: int, pinned_md5: str | None,
-               c5_qlen: int, c5_queries: int) -> dict:
+               c5_qlen: int, c5_queries: int, a=None, pmc: dict | None = None, ceiling: float | None = None) -> dict:
     """Every rank's reads on a K = 4 index (the reference's K_STEPS parameter;
     its GPU files stop at K = 2): built on the device with no host image (the
     51 GB of tag-100 entries stay in HBM), laid out as LAY_GRP -- one 128-B line
@@ -787,11 +837,9 @@ def kstep4_leg(D, text: bytes, reads: np.ndarray, res: np.ndarray, img2, steps: 
             out["results_md5_pinned"] = synth.results_md5(got) == pinned_md5
         blocks = S.run(K.count_blocks, h["i4"], h["q"])
         if blocks is not None and lf:
-            bytes_alg = blocks * (4 * 64 // 4 + 4)              # K*d/4 + 4 B per distinct block
-            out["roofline"] = {"distinct_blocks": blocks, "bytes_per_block": 68, "bytes_per_launch": bytes_alg,
-                               "achieved_GBs": round(bytes_alg / (lfm / 1e3) / 1e9, 1),
-                               "frac": round(bytes_alg / (lfm / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-                               "note": "rank 0's launch"}
+            # K*d/4 + 4 = 68 B per distinct block at K = 4
+            out["roofline"] = dict(variant_roofline(blocks, 4 * 64 // 4 + 4, lfm, a, "coop-grp", pmc,
+                                                    ceiling or PROBE_CEILING_GLINES, k=4), note="rank 0's launch")
         if D.world == 1 and S.ok:
             i4, q, r = h["i4"], h["q"], h["r"]
             # opt-in jump start on the K = 4 index: the first 16 bases
@@ -1057,7 +1105,8 @@ def main():
         # ---- K = 4 on every rank's reads (LAY_GRP, coop kernel) --------------
         k4 = kstep4_leg(D, text, reads, res, img, a.steps,
                         synth.MD5["res3g.q10M"] if (pinned and a.qlen == 100 and a.queries == 10_000_000)
-                        else None, a.config5_qlen, a.config5_queries)
+                        else None, a.config5_qlen, a.config5_queries, a=a,
+                        pmc=load_variants_pmc(a) if D.world == 1 else None)
         log(f"rank {D.rank}: K=4 leg {k4}")
         ph.mark("kstep4")
     rank_rows = D.gather({"ingest": ingest, "rank": D.rank, "device": dev,
@@ -1071,9 +1120,10 @@ def main():
     extra = {}
     ph.mark("gather")
     probe = probe_leg() if D.world == 1 and D.rank == 0 else None
+    ceiling = probe["ceiling_G_lines_per_s"] if probe else PROBE_CEILING_GLINES
     if probe:
         extra["line_request_probe"] = probe
-        log(f"gather probe: best {probe['best_G_lines_per_s']} G lines/s ({probe['best_kind']})")
+        log(f"gather probe: ceiling {ceiling} G lines/s ({probe['ceiling_from']})")
     if c5 is not None:
         extra["config5"] = c5
     if k4 is not None:
@@ -1115,6 +1165,7 @@ def main():
                                    "to a sampled row (kernel_ms = walk kernel, call_ms = incl. D2H of positions)"}
         log(f"locate {extra['locate']}")
         loc.close()
+    variants_pmc = load_variants_pmc(a) if D.world == 1 else None
     if D.rank == 0 and D.world == 1:
         # ---- other backends (same index, same reads) ------------------------
         for b in [x for x in a.variants.split(",") if x and x != a.backend]:
@@ -1128,6 +1179,13 @@ def main():
                             "mqps_mean_wall": round(reads.shape[0] * len(walls) / float(np.sum(walls)) / 1e6, 2),
                             "lf_ms": round(lf, 3), "step_ms": round(tot, 3), "results_equal": ok,
                             "device_index_bytes": idx.device_bytes()}
+                if "+" not in b:
+                    # the row's own roofline: algorithmic bytes of this backend's
+                    # launch (36 B x distinct blocks, counted on the device with
+                    # the backend's own LF semantics), its HIP-event LF time, and
+                    # its fabric read requests from the committed PMC pass
+                    extra[b]["roofline"] = variant_roofline(K.count_blocks(idx, q), b_lf, lf, a, b, variants_pmc,
+                                                            ceiling)
                 log(f"variant {b}: {extra[b]}")
             except K.KfmiError as e:
                 extra[b] = {"error": str(e)}
@@ -1296,12 +1354,12 @@ def main():
                          "fabric_request_bytes_upper_bound": rdreq * 128 if rdreq else None,
                          "line_requests_per_query": round(rdreq / a.queries, 2) if rdreq else None,
                          "line_requests_G_per_s": round(rdreq / (lf_avg_ms / 1e3) / 1e9, 2) if rdreq else None,
-                         "line_request_ceiling_G_per_s": probe["best_G_lines_per_s"] if probe else PROBE_CEILING_GLINES,
-                         "line_request_ceiling_source": "gather_probe on this box, this run" if probe else
-                         "profiles/r01/gather_probe_table_size.txt (another box)",
-                         "line_request_frac": round(rdreq / (lf_avg_ms / 1e3) / 1e9 /
-                                                    (probe["best_G_lines_per_s"] if probe else PROBE_CEILING_GLINES), 3)
-                         if rdreq else None},
+                         "line_request_ceiling_G_per_s": ceiling,
+                         "line_request_ceiling_source": (f"gather_probe on this box, this run: the larger of the "
+                                                         f"3 GB (HBM) and 200 MB (Infinity-Cache-resident) random-line "
+                                                         f"rates ({probe['ceiling_from']})") if probe else
+                         "profiles/r03/gather_probe_r3g.jsonl: 200 MB table, Infinity-Cache resident (another box)",
+                         "line_request_frac": round(rdreq / (lf_avg_ms / 1e3) / 1e9 / ceiling, 3) if rdreq else None},
             "cpu_baseline": cpu,
             "parity": {"index_md5_pinned": index_md5_ok, "results_md5_pinned": results_md5_ok,
                        "oracle_sample_ok": ranks["parity_ok_all"], "oracle_sample_per_rank": int(ns_par)},
