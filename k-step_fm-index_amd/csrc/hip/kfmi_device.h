@@ -103,6 +103,8 @@ struct DollarArgs {
   uint32_t dpos[4];   // dollarPositionBWT[s], s < K <= 4
   uint32_t dbase[4];  // dollarBaseBWT[s]
   uint32_t dblk[4];   // dollarPositionBWT[s] / d (modposdollarBWT)
+  uint32_t duniq;     // bit s: dpos[s] differs from every dpos[s'] with s' < s (a 'ref'-mode
+                      // index can put two D_s on one row; its counters exclude that row once)
 };
 
 struct IdxArgs {
@@ -426,6 +428,28 @@ __device__ __forceinline__ uint32_t ac_clamp(const IdxArgs& ix, uint32_t v)
   return v > cap ? cap : v;
 }
 
+// '$' rows of block b with code c that share their row with an earlier D_s
+// (DollarArgs::duniq; only a 'ref'-mode index built from a text with non-ACGT
+// bytes has them).  The reference's rule discounts one per s, its builder's
+// counters one per row, so a step taken backward from cnt_{b+1} -- as the
+// AltCounters searcher takes them (-AltCounters.c:254-266) -- lands this many
+// rows above the forward step from cnt_b (fmIndexCPUBaseline.c:252-256).
+template <int K>
+__device__ __forceinline__ uint32_t dollar_dup(const DollarArgs& dl, uint32_t b, uint32_t c)
+{
+  uint32_t n = 0;
+#pragma unroll
+  for (int s = 1; s < K; ++s) n += (dl.dblk[s] == b && dl.dbase[s] == c && !((dl.duniq >> s) & 1u)) ? 1u : 0u;
+  return n;
+}
+
+// the AltCounters direction of (b, c): backward from entry b+1
+template <class G>
+__device__ __forceinline__ bool ac_rule_e(uint32_t b, uint32_t c)
+{
+  return ((b & 1u) != 0) == (c < (uint32_t) G::HALF);
+}
+
 template <class G>
 __device__ __forceinline__ uint32_t finish(const IdxArgs& ix, uint32_t cnt, uint32_t pop, uint32_t b, uint32_t c,
                                           uint32_t X, bool e)
@@ -433,6 +457,18 @@ __device__ __forceinline__ uint32_t finish(const IdxArgs& ix, uint32_t cnt, uint
   const int corr = dollar_fix<G::K, G::TWO_SIDED>(ix.dl, b, c, X, e);
   const uint32_t bc = pop - (uint32_t) corr;
   if constexpr (G::ACRULE) return ac_clamp<G>(ix, e ? cnt - bc : cnt + bc);
+  if constexpr (G::MIDLINES) {
+    // the MID direction is the block parity, not the semantics' own: give
+    // back the forward step (MID) or the AltCounters one (MIDAC) where a
+    // duplicated '$' row makes them differ (dollar_dup, nearly always 0)
+    uint32_t v = e ? cnt - bc : cnt + bc;
+    if (G::K > 1 && ix.dl.duniq != (1u << G::K) - 1u) {
+      const uint32_t dup = dollar_dup<G::K>(ix.dl, b, c);
+      const bool want = G::LAY == LAY_MIDAC && ac_rule_e<G>(b, c);
+      v = v - (e ? dup : 0u) + (want ? dup : 0u);
+    }
+    return v;
+  }
   if constexpr (G::TWO_SIDED) return e ? cnt - bc : cnt + bc;
   return cnt + bc;
 }
@@ -445,10 +481,18 @@ __device__ __forceinline__ uint32_t finish_prev(const IdxArgs& ix, uint32_t cnt,
 {
   int corr = 0;
 #pragma unroll
-  for (int s = 0; s < G::K; ++s)
-    corr += ((ix.dl.dblk[s] == b || ix.dl.dblk[s] + 1u == b) && ix.dl.dbase[s] == c && X > ix.dl.dpos[s]) ? 1 : 0;
-  const uint32_t v = cnt + pop - (uint32_t) corr;
-  if constexpr (G::ACRULE) return ac_clamp<G>(ix, v);
+  for (int s = 0; s < G::K; ++s) {
+    if (ix.dl.dbase[s] != c) continue;
+    if (ix.dl.dblk[s] == b) corr += X > ix.dl.dpos[s] ? 1 : 0;   // block b: the reference's own rule, per s
+    else if (ix.dl.dblk[s] + 1u == b) corr += (ix.dl.duniq >> s) & 1u;   // block b-1: each '$' row once, as
+  }                                                                  // the builder's counters exclude it
+  uint32_t v = cnt + pop - (uint32_t) corr;
+  // the AltCounters searcher takes this step backward from entry b+1: a
+  // duplicated '$' row of block b lands it dollar_dup rows higher
+  if constexpr (G::ACRULE) {
+    if (G::K > 1 && ac_rule_e<G>(b, c)) v += dollar_dup<G::K>(ix.dl, b, c);
+    return ac_clamp<G>(ix, v);
+  }
   return v;
 }
 

@@ -845,6 +845,12 @@ int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx, kfmi_dev_
     di->dl.dbase[s] = s < f->steps ? f->dollarBaseBWT[s] : 0xFFFFFFFFu;
     di->dl.dblk[s] = s < f->steps ? f->dollarPositionBWT[s] / f->chunk : 0xFFFFFFFFu;
   }
+  di->dl.duniq = 0;
+  for (uint32_t s = 0; s < f->steps && s < 4; ++s) {
+    bool first = true;
+    for (uint32_t t = 0; t < s; ++t) first = first && f->dollarPositionBWT[t] != f->dollarPositionBWT[s];
+    if (first) di->dl.duniq |= 1u << s;
+  }
   const uint64_t ew = src->entry_words;
   const uint64_t body = 4ull * ew * src->nentries;
   const uint32_t nc = 1u << (2 * f->steps);

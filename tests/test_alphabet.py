@@ -188,3 +188,92 @@ def test_gpu_search_on_reference_indexes(ref_mode, monkeypatch, key, ent):
             got = K.search_array(idx, reads, be)
             assert np.array_equal(got, want), (key, rk, be)
     idx.close()
+
+
+def dup_dollar_indexes(K, want=6):
+    """'ref'-mode indexes whose dollarPositionBWT repeats a row: a text with
+    non-ACGT bytes makes the reference's LF walk revisit rows (genFMindex.c
+    :347-400), and two D_s on one row are excluded once by its counters but
+    discounted once per s by its searchers (fmIndexCPUBaseline.c:252-256).
+    Seeded search over small N-rich texts, K = 2, 3, 4, d = 64; each returned
+    index has a duplicate, and together they put one in block 0 and in a
+    later block."""
+    out, blocks = [], set()
+    rng = np.random.default_rng(2024)
+    alpha = np.frombuffer(b"ACGTN", np.uint8)
+    for _ in range(20000):
+        n = int(rng.integers(150, 2500))
+        t = alpha[rng.choice(5, size=n, p=rng.dirichlet(np.ones(5)))].tobytes()
+        for k in (2, 3, 4):
+            try:
+                idx = K.Index.build(t, k=k, d=64)
+            except K.KfmiError:
+                continue
+            dp = idx.header()["dollar_pos"]
+            dups = {p for p in dp if dp.count(p) > 1}
+            if dups and (len(out) < want // 2 or any(p // 64 not in blocks for p in dups)):
+                blocks |= {p // 64 for p in dups}
+                out.append((t, k, idx))
+            else:
+                idx.close()
+        if len(out) >= want and len(blocks) > 1:
+            break
+    assert len(out) >= want and len(blocks) > 1, (len(out), blocks)
+    return out
+
+
+def _all_reads(t, k, rng):
+    """Every 2K-mer and 4-mer over ACGT, plus substrings of the text (N kept)."""
+    import itertools
+    rows = [np.frombuffer(bytes(p), np.uint8) for m in (2 * k, 4 * k if k < 3 else k)
+            for p in itertools.product(b"ACGT", repeat=m)]
+    tt = np.frombuffer(t, np.uint8)
+    out = {}
+    for r in rows:
+        out.setdefault(r.size, []).append(r)
+    for m in (k, 2 * k, 3 * k, 6 * k):
+        st = rng.integers(0, len(t) - m, size=300)
+        out.setdefault(m, []).extend(tt[st[:, None] + np.arange(m)[None, :]])
+    return {m: np.stack(v) for m, v in out.items()}
+
+
+def test_cpu_search_on_duplicate_dollar_rows(ref_mode, oracle_mod):
+    """searchIndexCPU equals the reference searchers (the oracle restates
+    them) on indexes with a repeated '$' row, every tag."""
+    K = ref_mode
+    rng = np.random.default_rng(5)
+    for t, k, idx in dup_dollar_indexes(K):
+        i101 = idx.interleave()
+        i200, i201 = idx.alt_counters()
+        for m, q in _all_reads(t, k, rng).items():
+            for tagged, img in ((idx, idx), (i101, idx), (i200, i200), (i201, i200)):
+                want, _ = oracle_mod.search(img.image(), q)
+                assert np.array_equal(K.search_cpu_array(tagged, q, 2), want), (k, m, tagged.header()["tag"])
+        for x in (idx, i101, i200, i201):
+            x.close()
+
+
+@pytest.mark.gpu
+def test_gpu_search_on_duplicate_dollar_rows(ref_mode, oracle_mod):
+    """Every backend on indexes with a repeated '$' row equals the reference
+    searchers: the line-local step from block b-1 discounts each '$' row of
+    b-1 once (as the builder's counters), and the steps whose direction
+    differs from the semantics' own (MID lines backward where the reference
+    steps forward; MIDAC, task-ac/coop-ac from b-1, forward where the
+    AltCounters searcher steps backward) are corrected by the duplicate count
+    (kfmi_device.h dollar_dup)."""
+    K = ref_mode
+    K.set_device(0)
+    rng = np.random.default_rng(6)
+    for t, k, idx in dup_dollar_indexes(K):
+        img200 = idx.alt_counters()[0].image()
+        for m, q in _all_reads(t, k, rng).items():
+            want, _ = oracle_mod.search(idx.image(), q)
+            want_ac, _ = oracle_mod.search(img200, q)
+            backends = (PLAIN + AC) if k == 2 else ("coop-grp", "task-grp")
+            for be in backends:
+                if not coop_supported(be, k, 64):
+                    continue
+                got = K.search_array(idx, q, be)
+                assert np.array_equal(got, want_ac if be in AC else want), (k, m, be, idx.header()["dollar_pos"])
+        idx.close()
