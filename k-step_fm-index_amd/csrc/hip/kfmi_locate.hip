@@ -217,9 +217,9 @@ extern "C" int32_t kfmi_locate(void* index, void* results, uint32_t max_occ, voi
   DeviceGuard dg;
   /* the handle's lock shared; exclusive when a device copy still needs this
    * index's samples (locate_on uploads them into the copy) */
-  std::shared_mutex& mu = index_lock(f);
-  std::shared_lock<std::shared_mutex> sl(mu);
-  std::unique_lock<std::shared_mutex> ul;
+  RwLock& mu = index_lock(f);
+  std::shared_lock<RwLock> sl(mu);
+  std::unique_lock<RwLock> ul;
   auto stale = [&] {
     const GroupIndex* g = (const GroupIndex*) f->grp;
     if (!g) return f->dev && (!f->dev->sa || f->dev->sa_gen != f->sa_gen);
@@ -229,7 +229,7 @@ extern "C" int32_t kfmi_locate(void* index, void* results, uint32_t max_occ, voi
   };
   if (stale()) {
     sl.unlock();
-    ul = std::unique_lock<std::shared_mutex>(mu);
+    ul = std::unique_lock<RwLock>(mu);
   }
   if (!f->grp && !r->grp) {
     if (!f->dev || !r->d_results) return KFMI_E_NOT_ON_DEVICE;

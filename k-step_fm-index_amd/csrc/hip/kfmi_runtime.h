@@ -12,6 +12,7 @@
 #include <stdio.h>
 #include <mutex>
 #include <shared_mutex>
+#include <pthread.h>
 
 #include "../kfmi_internal.h"
 #include "kfmi_devguard.h"
@@ -78,9 +79,20 @@ namespace kfmi {
  * locates, block counts and streamed searches hold it shared for as long as
  * they use the device copy; an upload that replaces it (another backend or
  * device, a new device group) or freeIndexGPU holds it exclusively, so a
- * search running on another thread never sees its tables freed.  Striped by
- * handle address. */
-std::shared_mutex& index_lock(const void* f);
+ * search running on another thread never sees its tables freed.  One
+ * writer-preferring lock per handle (kfmi_fmi_t::rw), so a writer is not
+ * starved by a stream of searches and unrelated handles never wait on each
+ * other.  RwLock is that pthread lock seen as a SharedMutex. */
+struct RwLock {
+  pthread_rwlock_t rw;
+  void lock() { pthread_rwlock_wrlock(&rw); }
+  void unlock() { pthread_rwlock_unlock(&rw); }
+  bool try_lock() { return pthread_rwlock_trywrlock(&rw) == 0; }
+  void lock_shared() { pthread_rwlock_rdlock(&rw); }
+  void unlock_shared() { pthread_rwlock_unlock(&rw); }
+  bool try_lock_shared() { return pthread_rwlock_tryrdlock(&rw) == 0; }
+};
+RwLock& index_lock(const void* f);
 
 /* One non-blocking stream per device, shared by the threads that use it (their
  * work is serialised on it).  Timing events are per calling thread. */

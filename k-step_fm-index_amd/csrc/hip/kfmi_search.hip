@@ -134,11 +134,10 @@ extern "C" int32_t kfmi_device_pci_bus_id(int32_t device, char* buf, int32_t len
   return KFMI_SUCCESS;
 }
 
-std::shared_mutex& index_lock(const void* f)
+RwLock& index_lock(const void* f)
 {
-  static std::shared_mutex stripes[64];
-  const uintptr_t h = (uintptr_t) f;
-  return stripes[(h >> 6 ^ h >> 12) & 63];
+  static_assert(sizeof(RwLock) == sizeof(pthread_rwlock_t), "RwLock is the handle's pthread lock");
+  return *reinterpret_cast<RwLock*>(&static_cast<kfmi_fmi_t*>(const_cast<void*>(f))->rw);
 }
 
 extern "C" void kfmi_set_last_error(int32_t e) { t_last_error = e; }
@@ -1227,8 +1226,8 @@ extern "C" int32_t transferCPUtoGPU(void* index, void* queries, void* results)
   int devs[KFMI_MAX_GROUP];
   const int ng = group_devices(devs);
   if (ng > 1) {
-    std::unique_lock<std::shared_mutex> lk;
-    if (f) lk = std::unique_lock<std::shared_mutex>(index_lock(f));
+    std::unique_lock<RwLock> lk;
+    if (f) lk = std::unique_lock<RwLock>(index_lock(f));
     return group_transfer(f, q, r, devs, ng);
   }
   if (q) group_free_queries(q);
@@ -1245,11 +1244,11 @@ extern "C" int32_t transferCPUtoGPU(void* index, void* queries, void* results)
     auto fits = [&] { return !f->grp && f->dev && f->dev->backend == backend && f->dev->device == dev; };
     bool ok;
     {
-      std::shared_lock<std::shared_mutex> sl(index_lock(f));
+      std::shared_lock<RwLock> sl(index_lock(f));
       ok = fits();
     }
     if (!ok) {
-      std::unique_lock<std::shared_mutex> ul(index_lock(f));
+      std::unique_lock<RwLock> ul(index_lock(f));
       if (!fits()) {
         group_free_index(f);   /* one mode per handle */
         err = upload_index(f, backend, dev, ctx);
@@ -1392,7 +1391,7 @@ extern "C" int32_t kfmi_search(void* index, void* queries, void* results)
   if (!f || !q || !r) return KFMI_E_BAD_ARGUMENT;
   if (q->num != r->num) return KFMI_E_BAD_ARGUMENT;
   DeviceGuard dg;
-  std::shared_lock<std::shared_mutex> lk(index_lock(f));
+  std::shared_lock<RwLock> lk(index_lock(f));
   if (f->grp || q->grp || r->grp) return group_search(f, q, r);
   if (!f->dev || !q->dev || !r->d_results) return KFMI_E_NOT_ON_DEVICE;
   kfmi_dev_index* di = f->dev;
@@ -1427,7 +1426,7 @@ extern "C" int32_t kfmi_count_blocks(void* index, void* queries, uint64_t* block
   kfmi_qrys_t* q = (kfmi_qrys_t*) queries;
   if (!f || !q || !blocks) return KFMI_E_BAD_ARGUMENT;
   DeviceGuard dg;
-  std::shared_lock<std::shared_mutex> lk(index_lock(f));
+  std::shared_lock<RwLock> lk(index_lock(f));
   if (f->grp || q->grp) {
     GroupIndex* gi = (GroupIndex*) f->grp;
     GroupSlices* gq = (GroupSlices*) q->grp;
@@ -1502,7 +1501,7 @@ extern "C" int32_t freeIndexGPU(void** index)
   kfmi_fmi_t* f = index ? (kfmi_fmi_t*) *index : nullptr;
   if (!f) return KFMI_SUCCESS;
   DeviceGuard dg;
-  std::unique_lock<std::shared_mutex> lk(index_lock(f));
+  std::unique_lock<RwLock> lk(index_lock(f));
   group_free_index(f);
   if (f->dev) {
     free_dev_index(f->dev);
@@ -1540,7 +1539,7 @@ extern "C" uint64_t kfmi_device_index_bytes(void* index)
 {
   kfmi_fmi_t* f = (kfmi_fmi_t*) index;
   if (!f) return 0;
-  std::shared_lock<std::shared_mutex> lk(index_lock(f));
+  std::shared_lock<RwLock> lk(index_lock(f));
   if (f->grp) {   /* all replicas of a device group */
     const GroupIndex* g = (const GroupIndex*) f->grp;
     uint64_t b = 0;

@@ -488,7 +488,7 @@ extern "C" int32_t kfmi_search_stream(void* index, const char* ascii, uint64_t n
   kfmi_fmi_t* f = (kfmi_fmi_t*) index;
   if (!f || (!ascii && num) || (!results && num)) return KFMI_E_BAD_ARGUMENT;
   DeviceGuard dg;
-  std::shared_lock<std::shared_mutex> lk(index_lock(f));
+  std::shared_lock<RwLock> lk(index_lock(f));
   GroupIndex* g = (GroupIndex*) f->grp;
   if (!g && !f->dev) return KFMI_E_NOT_ON_DEVICE;
   const kfmi_dev_index* d0 = g ? g->di[0] : f->dev;

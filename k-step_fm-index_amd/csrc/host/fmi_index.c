@@ -62,13 +62,20 @@ int32_t kfmi_index_alloc_ex(uint32_t tag, uint32_t steps, uint32_t bwtsize, uint
   if (!valid_geometry(tag, steps, chunk, ncounters)) return KFMI_E_BAD_ARGUMENT;
   f = (kfmi_fmi_t *) calloc(1, sizeof(*f));
   if (!f) return KFMI_E_ALLOCATING_FMI;
+  {
+    pthread_rwlockattr_t at;
+    pthread_rwlockattr_init(&at);
+    pthread_rwlockattr_setkind_np(&at, PTHREAD_RWLOCK_PREFER_WRITER_NONRECURSIVE_NP);
+    pthread_rwlock_init(&f->rw, &at);
+    pthread_rwlockattr_destroy(&at);
+  }
   f->tag = tag; f->steps = steps; f->bwtsize = bwtsize; f->ncounters = ncounters;
   f->nentries = nentries; f->chunk = chunk; f->nbitmaps = chunk / 32;
   f->entry_words = kfmi_entry_words(tag, steps, chunk);
   f->header_bytes = 24 + 8 * steps;
   f->image_bytes = f->header_bytes + 4ull * f->entry_words * nentries;
   f->image = (uint8_t *) calloc(1, (with_entries ? f->image_bytes : f->header_bytes) + 64);
-  if (!f->image) { free(f); return KFMI_E_ALLOCATING_FMI; }
+  if (!f->image) { pthread_rwlock_destroy(&f->rw); free(f); return KFMI_E_ALLOCATING_FMI; }
   h = (uint32_t *) f->image;
   h[0] = tag; h[1] = steps; h[2] = bwtsize; h[3] = ncounters; h[4] = nentries; h[5] = chunk;
   for (s = 0; s < steps; s++) {
@@ -222,6 +229,7 @@ int32_t freeIndex(void **index)
   free(f->h_sa);
   free(f->image);
   free(f->image_retired);
+  pthread_rwlock_destroy(&f->rw);
   free(f);
   *index = NULL;
   return KFMI_SUCCESS;

@@ -11,6 +11,7 @@
 
 #include <stdint.h>
 #include <stddef.h>
+#include <pthread.h>
 #include "../../include/kstep_fmi.h"
 
 #ifdef __cplusplus
@@ -55,6 +56,11 @@ typedef struct {
   uint64_t  sa_count;
   uint32_t *h_sa;
   void     *grp;           /* replicas on a device group (KFMI_DEVICES, kfmi_set_devices) */
+  /* guards dev / grp (kfmi_runtime.h index_lock): searches hold it shared,
+   * uploads that replace the device copy and freeIndexGPU exclusively;
+   * writer-preferring, one per handle (so unrelated handles never wait on
+   * each other); initialised by kfmi_index_alloc_ex, destroyed by freeIndex */
+  pthread_rwlock_t rw;
 } kfmi_fmi_t;
 
 typedef struct {
