@@ -221,14 +221,16 @@ def rem_setup(kfmi_mod):
 
 @pytest.mark.parametrize("group", [[], [0, 0]])
 @pytest.mark.parametrize("hostpack", ["1", "0", "2", "3"])
-@pytest.mark.parametrize("k", [2, 4])
+@pytest.mark.parametrize("k,backend", [(2, "task-mid"), (2, "task"), (2, "coop"), (4, "coop-grp")])
 @pytest.mark.parametrize("m", [101, 150, 151])
-def test_stream_remainder_reads(rem_setup, oracle_mod, k, m, hostpack, group, monkeypatch):
+def test_stream_remainder_reads(rem_setup, oracle_mod, k, backend, m, hostpack, group, monkeypatch):
     """m % K != 0 streamed: the last m % K bases of every read come
     from the remainder table -- host packing writes their codes as one more
     word row, ASCII chunks are packed in the kernel -- on one device and on a
     device group; results equal the K = 1 oracle (true suffix-array
-    intervals) and the resident-batch search."""
+    intervals) and the resident-batch search.  task and coop on the reference
+    tag-101 layout take the line-local (NEIGHBOR) fetch paths at K = 2 d = 64
+    (ADVICE r3)."""
     K, text, img1, idx = rem_setup
     monkeypatch.setenv("KFMI_STREAM_HOSTPACK", hostpack)
     rng = np.random.default_rng(m * 7 + k)
@@ -239,7 +241,6 @@ def test_stream_remainder_reads(rem_setup, oracle_mod, k, m, hostpack, group, mo
     reads[0] = t[len(text) - m:]
     reads[1, :] = t[:m]
     want, _ = oracle_mod.search(img1, reads, 8)
-    backend = "task-mid" if k == 2 else "coop-grp"
     try:
         K.set_devices(group)
         K.set_backend(backend)
