@@ -1083,6 +1083,14 @@ def main():
                 rdreq = tr.get("rdreq_per_launch")
         except Exception:
             traffic = None
+    # the kernel's own request stream replayed without its LF dependence
+    # (kfmi_probe_replay: MID layouts): a measured ceiling for that exact mix
+    replay = None
+    if D.world == 1 and D.rank == 0 and a.backend in ("task-mid", "coop-mid") and a.k == 2 and a.d == 64:
+        try:
+            replay = [K.probe_replay(idx, q, unroll=u, reps=5) for u in (1, 2, 4, 8)]
+        except K.KfmiError as e:
+            log(f"replay probe unavailable: {e}")
     ph.mark("count_blocks")
     # ---- auxiliary legs: each makes the same collective calls on every rank
     # whatever fails locally (Steps), so one failing rank never hangs the rest
@@ -1359,7 +1367,21 @@ def main():
                                                          f"3 GB (HBM) and 200 MB (Infinity-Cache-resident) random-line "
                                                          f"rates ({probe['ceiling_from']})") if probe else
                          "profiles/r03/gather_probe_r3g.jsonl: 200 MB table, Infinity-Cache resident (another box)",
-                         "line_request_frac": round(rdreq / (lf_avg_ms / 1e3) / 1e9 / ceiling, 3) if rdreq else None},
+                         "line_request_frac": round(rdreq / (lf_avg_ms / 1e3) / 1e9 / ceiling, 3) if rdreq else None,
+                         # the same question on the kernel's own fetches (distinct blocks = lines it loads):
+                         # its rate against the fastest replay of the identical request stream
+                         "replay": None if not replay else {
+                             "kernel_G_lines_per_s": round(blocks / (lf_avg_ms / 1e3) / 1e9, 2),
+                             "replay_G_lines_per_s_by_unroll": {str(x["unroll"]): round(x["G_lines_per_s"], 2)
+                                                                for x in replay},
+                             "replay_ms_by_unroll": {str(x["unroll"]): round(x["ms"], 4) for x in replay},
+                             "lines_per_launch": replay[0]["lines"], "trace_bytes_per_launch": replay[0]["trace_bytes"],
+                             "frac_of_best_replay": round(blocks / (lf_avg_ms / 1e3) / 1e9 /
+                                                          max(x["G_lines_per_s"] for x in replay), 3),
+                             "what": "kfmi_probe_replay: every (K-step, read) end's MID128 line recorded by a trace "
+                                     "launch, then the task kernel's loads for them issued from the trace with "
+                                     "`unroll` K-steps in flight per lane (no LF dependence); rate = lines / replay "
+                                     "time (the trace itself, 8 B per read per K-step, is streamed beside them)"}},
             "cpu_baseline": cpu,
             "parity": {"index_md5_pinned": index_md5_ok, "results_md5_pinned": results_md5_ok,
                        "oracle_sample_ok": ranks["parity_ok_all"], "oracle_sample_per_rank": int(ns_par)},
