@@ -631,6 +631,19 @@ def variant_roofline(blocks: int, b_lf: int, lf_ms: float, a, backend: str, pmc:
     return out
 
 
+def cpu_product_rows(idx, reads: np.ndarray, want: np.ndarray, thrs: list) -> list:
+    """searchIndexCPU of the library (kfmi_search_cpu) on `reads` at each
+    thread count: rate and equality with the GPU results."""
+    rows = []
+    for thr in thrs:
+        t = time.perf_counter()
+        got = K.search_cpu_array(idx, reads, nthreads=thr)
+        s_ = time.perf_counter() - t
+        rows.append({"value": round(reads.shape[0] / s_ / 1e6, 4), "unit": "Mqueries/s", "cores": thr,
+                     "kind": "product (searchIndexCPU)", "equal_gpu": bool(np.array_equal(got, want))})
+    return rows
+
+
 def config1_leg(backend: str, thr: int, steps: int = 5) -> dict:
     """BASELINE config #1 (64 Mbase recipe text, 2^20 x 100 bp reads): GPU
     search rate on the md5-pinned inputs and the reference's CPU searcher on
@@ -647,6 +660,8 @@ def config1_leg(backend: str, thr: int, steps: int = 5) -> dict:
     ref = cpu_reference_baseline(idx, reads, reads.shape[0], 2, 64, thr, res)
     if ref:
         out["cpu_reference"] = {k: ref[k] for k in ("value", "unit", "cores", "parity_with_gpu")}
+    # config #1 is the reference's CPU searcher: the product's searchIndexCPU beside it
+    out["cpu_product"] = cpu_product_rows(idx, reads, res, [thr])[0]
     q.close()
     r.close()
     idx.close()
@@ -1303,6 +1318,10 @@ def main():
         oracle.search(img, reads[:n1], nthreads=1)
         extra["cpu_port_1thread"] = {"value": round(n1 / (time.perf_counter() - t) / 1e6, 4),
                                      "unit": "Mqueries/s", "cores": 1, "sample": f"first {n1} reads"}
+        # the product's own host search (searchIndexCPU, csrc/host/cpu_search.c: batched
+        # prefetch, the reference CPU driver's drop-in) on the same sample and cores
+        extra["cpu_product"] = cpu_product_rows(idx, reads[:ns], res[:2 * ns], thrs)
+        log(f"cpu product {extra['cpu_product']}")
         log(f"cpu baseline {cpu}")
     ph.mark("rank0_n1_legs_and_cpu_baseline")
     # per-rank phase wall times and peak host RSS (the N = 8 budget: DESIGN.md 7)
