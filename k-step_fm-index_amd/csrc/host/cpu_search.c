@@ -75,9 +75,11 @@ CS_INLINE uint32_t cs_plane(uint32_t K, uint32_t NB, int inter, uint32_t s, uint
 CS_INLINE uint32_t cs_count(uint32_t K, uint32_t NB, int inter, const uint32_t *pl, uint32_t o, uint32_t c, int inv)
 {
   uint32_t pop = 0, w, s;
-  int sh = (int) o;
-  for (w = 0; w < NB; ++w, sh -= 32) {
-    uint32_t m = sh >= 32 ? 0xFFFFFFFFu : (sh > 0 ? 0xFFFFFFFFu << (32 - sh) : 0u);
+  for (w = 0; w < NB; ++w) {
+    /* the top clamp(o - 32w, 0, 32) bits, without a branch on the (random) offset */
+    const int64_t sh = (int64_t) o - 32 * (int64_t) w;
+    const uint32_t bits = (uint32_t) (sh < 0 ? 0 : (sh > 32 ? 32 : sh));
+    uint32_t m = (uint32_t) (~(~0ull >> bits) >> 32);
     if (inv) m = ~m;
     for (s = 0; s < K; ++s) {
       const uint32_t cs = (c >> (2u * s)) & 3u;
