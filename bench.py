@@ -321,34 +321,45 @@ def bench_text(D, n: int):
     rank maps that file read-only -- one copy in the node's page cache instead
     of one 3 GB object per rank -- and the file is unlinked once every rank
     holds its mapping."""
-    if D.world == 1:
-        buf = bytearray(n)
-        off = 0
-        for ch in synth.text_chunks(n):
-            buf[off:off + len(ch)] = ch
-            off += len(ch)
-        return buf
-    return _node_shared(D, f"text_{n}", lambda f: [f.write(ch) for ch in synth.text_chunks(n)])
+    if D.world > 1:
+        mm = _node_shared(D, f"text_{n}", n, lambda f: [f.write(ch) for ch in synth.text_chunks(n)])
+        if mm is not None:
+            return mm
+        log(f"rank {D.rank}: no room for the node-shared text: generating it in this process")
+    buf = bytearray(n)
+    off = 0
+    for ch in synth.text_chunks(n):
+        buf[off:off + len(ch)] = ch
+        off += len(ch)
+    return buf
 
 
-def _node_shared(D, name: str, write):
-    """A file written once per node by local rank 0 (`write(f)`), then mapped
-    read-only by every rank of the node; returns the mmap.  Collective: every
-    rank calls it; a failed write fails every rank together."""
+def _node_shared(D, name: str, nbytes: int, write):
+    """A file of `nbytes` written once per node by local rank 0 (`write(f)`) in
+    TMPDIR, then mapped read-only by every rank of the node; returns the mmap,
+    or None on every rank when local rank 0 could not write it (no room: the
+    caller then keeps a private copy per rank).  Collective: every rank calls
+    it."""
     import mmap
+    import shutil
     d = Path(os.environ.get("TMPDIR") or "/tmp")
     fn = d / f"kfmi_bench_{name}_{os.environ.get('MASTER_PORT', '0')}.bin"
     err = None
     if D.local == 0:
+        tmp = fn.with_suffix(".part")
         try:
-            tmp = fn.with_suffix(".part")
+            if shutil.disk_usage(d).free < nbytes + (1 << 30):
+                raise OSError(f"{d}: {shutil.disk_usage(d).free} bytes free, {nbytes} needed")
             with open(tmp, "wb") as f:
                 write(f)
             os.replace(tmp, fn)
         except OSError as e:
             err = f"{type(e).__name__}: {e}"
+            tmp.unlink(missing_ok=True)
     if not D.all_ok(err is None):
-        raise SystemExit(f"bench.py: node-shared file {fn} could not be written ({err})")
+        if err:
+            log(f"node-shared {name}: {err}")
+        return None
     with open(fn, "rb") as f:
         mm = mmap.mmap(f.fileno(), 0, access=mmap.ACCESS_READ)
     D.barrier()                      # every rank holds its mapping: the name can go
@@ -365,7 +376,11 @@ def shared_image(D, idx) -> np.ndarray:
     each rank's GPU results against that image)."""
     if D.world == 1:
         return idx.image()
-    mm = _node_shared(D, "image", lambda f: idx.image().tofile(f))
+    h = idx.header()
+    nbytes = 24 + 8 * h["steps"] + 4 * h["nentries"] * ((2 * h["chunk"] // 32 * h["steps"]) + h["ncounters"])
+    mm = _node_shared(D, "image", nbytes, lambda f: idx.image().tofile(f))
+    if mm is None:
+        return idx.image()           # no room on the node: each rank fetches its own
     return np.frombuffer(mm, dtype=np.uint8)
 
 
