@@ -21,3 +21,73 @@ def test_reference_cpu_baseline_matches_oracle(kfmi_mod, k):
     out = bench.cpu_reference_baseline(idx, reads, 2000, k, 64, 2, want)
     assert out is not None and out["kind"] == "reference" and out["parity_with_gpu"]
     assert out["value"] > 0
+
+
+def test_cpu_product_rows_equal_oracle(kfmi_mod):
+    """bench.cpu_product_rows: the library's searchIndexCPU timed on a sample,
+    equal to the oracle's results at every thread count."""
+    rng = np.random.default_rng(9)
+    t = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), size=100_001)
+    idx = kfmi_mod.Index.build(t.tobytes(), k=2, d=64)
+    reads = t[rng.integers(0, len(t) - 100, size=2000)[:, None] + np.arange(100)]
+    want, _ = oracle.search(idx.image(), reads)
+    rows = bench.cpu_product_rows(idx, reads, want, [1, 3])
+    assert [r["cores"] for r in rows] == [1, 3] and all(r["equal_gpu"] and r["value"] > 0 for r in rows)
+
+
+def test_variant_roofline_and_pmc_file(tmp_path, monkeypatch):
+    """A variant row's roofline: 36 B x distinct blocks over its LF time against
+    8 TB/s, plus its fabric read requests when the committed PMC file
+    (scripts/traffic_variants.py output) was taken on the same config."""
+    import argparse
+    import json
+    a = argparse.Namespace(queries=10_000_000, ref_size=3_000_000_000, qlen=100, d=64, k=2)
+    pmc = {"config": {"queries": 10_000_000, "ref_size": 3_000_000_000, "qlen": 100, "d": 64},
+           "source": "x.csv", "backends": {"coop@k2": {"rdreq_per_launch": 582_000_000, "tcc_req_per_launch": 672_000_000,
+                                                      "kernel_ms_under_pmc": 10.9}}}
+    fn = tmp_path / "tv.json"
+    fn.write_text(json.dumps(pmc))
+    monkeypatch.setattr(bench, "VARIANTS_PMC", fn)
+    got = bench.load_variants_pmc(a)
+    assert got == pmc
+    r = bench.variant_roofline(578_600_000, 36, 10.9, a, "coop", got, 56.0)
+    assert r["bytes_per_launch"] == 578_600_000 * 36
+    assert abs(r["frac"] - 578_600_000 * 36 / 10.9e-3 / 8e12) < 1e-4
+    assert r["line_requests_per_query"] == 58.2 and r["line_request_frac"] < 1.0
+    assert "fabric_read_requests_per_launch" not in bench.variant_roofline(1, 36, 1.0, a, "task", got, 56.0)
+    a.queries = 1_000_000                                # another config: the file does not apply
+    assert bench.load_variants_pmc(a) is None
+
+
+def test_traffic_variants_parser(tmp_path):
+    """scripts/traffic_variants.py cuts the LF launches of a PMC pass into the
+    order file's runs and checks each run's kernel against its backend."""
+    import csv
+    import json
+    import subprocess
+    import sys
+    from util import REPO
+    order = {"queries": 1000, "ref_size": 5000, "qlen": 100, "d": 64,
+             "order": [{"backend": "task-mid", "k": 2, "launches": 3, "warmup": 1, "lf_ms_hip_events": 1.0,
+                        "distinct_blocks": 5},
+                       {"backend": "coop-grp", "k": 4, "launches": 2, "warmup": 1, "lf_ms_hip_events": 0.5,
+                        "distinct_blocks": 4}]}
+    (tmp_path / "order.json").write_text(json.dumps(order))
+    names = ["void kfmi::task_kernel<kfmi::Geo<2, 2, 3>, 1, 8, 8>(kfmi::IdxArgs)"] * 3 + \
+            ["void kfmi::coop_kernel<kfmi::Geo<4, 2, 6>, 8>(kfmi::IdxArgs)"] * 2
+    with open(tmp_path / "p.csv", "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=["Dispatch_Id", "Kernel_Name", "Grid_Size", "Counter_Name", "Counter_Value",
+                                          "Start_Timestamp", "End_Timestamp"])
+        w.writeheader()
+        for i, n in enumerate(names):
+            for cn, v in (("TCC_EA0_RDREQ_sum", 100 + i), ("TCC_REQ_sum", 200 + i)):
+                w.writerow({"Dispatch_Id": 10 + i, "Kernel_Name": n, "Grid_Size": 1024, "Counter_Name": cn,
+                            "Counter_Value": v, "Start_Timestamp": 0, "End_Timestamp": 1_000_000})
+        w.writerow({"Dispatch_Id": 99, "Kernel_Name": "void kfmi::build_mid_kernel<2, 2>()", "Grid_Size": 1024,
+                    "Counter_Name": "TCC_EA0_RDREQ_sum", "Counter_Value": 1, "Start_Timestamp": 0, "End_Timestamp": 1})
+    p = subprocess.run([sys.executable, str(REPO / "scripts" / "traffic_variants.py"), str(tmp_path / "p.csv"),
+                        str(tmp_path / "order.json"), "--source", "t"], capture_output=True, text=True)
+    assert p.returncode == 0, p.stderr
+    out = json.loads(p.stdout)
+    assert out["backends"]["task-mid@k2"]["rdreq_per_launch"] == 101      # median of launches 2, 3 (101, 102)
+    assert out["backends"]["coop-grp@k4"]["rdreq_per_launch"] == 104 and out["backends"]["coop-grp@k4"]["launches_timed"] == 1
