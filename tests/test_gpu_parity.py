@@ -319,7 +319,7 @@ def test_ac_tail_blocks(gpu, oracle_mod, n, tail):
 
 
 @pytest.mark.parametrize("backend", ["coop", "coop-packed", "coop-mid", "coop-ac", "coop-ac128", "coop-ac-mid"])
-def test_coop_backends_equal_oracle(gpu, oracle_mod, random_index, backend):
+def test_coop_backends_equal_oracle(gpu, oracle_mod, random_index, backend, monkeypatch):
     """The coop kernel's staging rounds (each round decodes its requests'
     chunk addresses; the pre-addressed form measured neutral and was removed,
     DESIGN 5 "Coop issue") on every coop backend and geometry: the same results
