@@ -584,7 +584,7 @@ def probe_leg() -> dict | None:
             return None
         if p.returncode != 0:
             return None
-        rows, table = [], None
+        rows, table, want = [], None, int(float(gb) * 1e9) & ~127
         for ln in p.stdout.splitlines():
             try:
                 d = json.loads(ln)
@@ -592,7 +592,7 @@ def probe_leg() -> dict | None:
                 continue
             if "table_bytes" in d:
                 table = d["table_bytes"]
-            elif "kind" in d and table is not None:
+            elif "kind" in d and table == want:   # the tool also probes 4 MB / 200 MB tables after the main one
                 rows.append(d)
         if not rows:
             return None
@@ -1118,7 +1118,8 @@ def main():
     replay = None
     if D.world == 1 and D.rank == 0 and a.backend in ("task-mid", "coop-mid") and a.k == 2 and a.d == 64:
         try:
-            replay = [K.probe_replay(idx, q, unroll=u, reps=5) for u in (1, 2, 4, 8)]
+            replay = [K.probe_replay(idx, q, unroll=u, groups=g, reps=5)
+                      for u, g in ((0, 1), (0, 2), (1, 1), (1, 2), (2, 2), (4, 2), (8, 2))]
         except K.KfmiError as e:
             log(f"replay probe unavailable: {e}")
     ph.mark("count_blocks")
@@ -1406,16 +1407,17 @@ def main():
                          # its rate against the fastest replay of the identical request stream
                          "replay": None if not replay else {
                              "kernel_G_lines_per_s": round(blocks / (lf_avg_ms / 1e3) / 1e9, 2),
-                             "replay_G_lines_per_s_by_unroll": {str(x["unroll"]): round(x["G_lines_per_s"], 2)
-                                                                for x in replay},
-                             "replay_ms_by_unroll": {str(x["unroll"]): round(x["ms"], 4) for x in replay},
+                             "replay_G_lines_per_s": {f"u{x['unroll']}g{x['groups']}": round(x["G_lines_per_s"], 2)
+                                                      for x in replay},
+                             "replay_ms": {f"u{x['unroll']}g{x['groups']}": round(x["ms"], 4) for x in replay},
                              "lines_per_launch": replay[0]["lines"], "trace_bytes_per_launch": replay[0]["trace_bytes"],
                              "frac_of_best_replay": round(blocks / (lf_avg_ms / 1e3) / 1e9 /
                                                           max(x["G_lines_per_s"] for x in replay), 3),
                              "what": "kfmi_probe_replay: every (K-step, read) end's MID128 line recorded by a trace "
-                                     "launch, then the task kernel's loads for them issued from the trace with "
-                                     "`unroll` K-steps in flight per lane (no LF dependence); rate = lines / replay "
-                                     "time (the trace itself, 8 B per read per K-step, is streamed beside them)"}},
+                                     "launch, then the task kernel's loads for them issued from the trace (no LF "
+                                     "dependence): uU = U K-steps of C++ loads in flight per lane, u0 = the kernel's "
+                                     "own asm fetch (one K-step in flight); gG = G exec-masked lane groups; rate = "
+                                     "lines / replay time (the trace, 8 B per read per K-step, streams beside them)"}},
             "cpu_baseline": cpu,
             "parity": {"index_md5_pinned": index_md5_ok, "results_md5_pinned": results_md5_ok,
                        "oracle_sample_ok": ranks["parity_ok_all"], "oracle_sample_per_rank": int(ns_par)},

@@ -306,10 +306,11 @@ double  kfmi_stream_hostpacked_fraction(void);
  * m % K == 0, both uploaded) without the LF chain's dependence: a trace launch
  * records every (K-step, read) end's line, then `reps` timed replay launches
  * issue the task kernel's loads for them with `unroll` (1, 2, 4, 8) K-steps in
- * flight per lane.  *ms: mean replay launch time; *lines: lines fetched per
+ * flight per lane, as `groups` (1, 2) exec-masked lane groups (unroll 0: the
+ * task kernel's own asm fetch, one K-step in flight).  *ms: mean replay launch time; *lines: lines fetched per
  * launch (= kfmi_count_blocks); *trace_bytes: the trace streamed beside them. */
-int32_t kfmi_probe_replay(void *index, void *queries, int32_t unroll, int32_t reps, double *ms, uint64_t *lines,
-                          uint64_t *trace_bytes);
+int32_t kfmi_probe_replay(void *index, void *queries, int32_t unroll, int32_t groups, int32_t reps, double *ms,
+                          uint64_t *lines, uint64_t *trace_bytes);
 
 /* Bytes of the device-resident index for the current backend (incl. SA samples). */
 uint64_t kfmi_device_index_bytes(void *index);

@@ -100,7 +100,7 @@ def load() -> ctypes.CDLL:
         "kfmi_build_index_gpu": (i32, [vp, u64, u32, u32, i32, pvp]),
         "kfmi_build_stats": (i32, [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32)]),
         "kfmi_count_blocks": (i32, [vp, vp, ctypes.POINTER(ctypes.c_uint64)]),
-        "kfmi_probe_replay": (i32, [vp, vp, i32, i32, ctypes.POINTER(ctypes.c_double),
+        "kfmi_probe_replay": (i32, [vp, vp, i32, i32, i32, ctypes.POINTER(ctypes.c_double),
                                     ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
         "kfmi_device_index_bytes": (u64, [vp]),
         "kfmi_search_stream": (i32, [vp, vp, u64, u32, vp, u64]),
@@ -407,14 +407,14 @@ def count_blocks(index: Index, queries: Queries) -> int:
     return int(n.value)
 
 
-def probe_replay(index: Index, queries: Queries, unroll: int = 1, reps: int = 5) -> dict:
+def probe_replay(index: Index, queries: Queries, unroll: int = 1, reps: int = 5, groups: int = 1) -> dict:
     """kfmi_probe_replay: the search's own line requests replayed without the
     LF dependence (MID layouts, K = 2); returns ms per launch, lines per
     launch, trace bytes and the line rate."""
     ms, lines, tb = ctypes.c_double(), ctypes.c_uint64(), ctypes.c_uint64()
-    _check(load().kfmi_probe_replay(index.ptr, queries.ptr, int(unroll), int(reps), ctypes.byref(ms),
+    _check(load().kfmi_probe_replay(index.ptr, queries.ptr, int(unroll), int(groups), int(reps), ctypes.byref(ms),
                                     ctypes.byref(lines), ctypes.byref(tb)), "kfmi_probe_replay")
-    return {"unroll": int(unroll), "ms": ms.value, "lines": int(lines.value), "trace_bytes": int(tb.value),
+    return {"unroll": int(unroll), "groups": int(groups), "ms": ms.value, "lines": int(lines.value), "trace_bytes": int(tb.value),
             "G_lines_per_s": lines.value / (ms.value / 1e3) / 1e9 if ms.value > 0 else None}
 
 

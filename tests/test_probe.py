@@ -24,9 +24,10 @@ def test_replay_probe_counts_and_rejects(kfmi_mod):
         K.set_backend(backend)
         K.transfer_to_gpu(idx, q, r)
         blocks = K.count_blocks(idx, q)
-        for u in (1, 2, 4, 8):
-            p = K.probe_replay(idx, q, unroll=u, reps=2)
-            assert p["lines"] == blocks and p["ms"] > 0 and p["trace_bytes"] == 8 * 50 * reads.shape[0], (backend, u, p)
+        for u, g in ((0, 1), (0, 2), (1, 1), (1, 2), (2, 2), (4, 1), (8, 2)):
+            p = K.probe_replay(idx, q, unroll=u, groups=g, reps=2)
+            assert p["lines"] == blocks and p["ms"] > 0, (backend, u, g, p)
+            assert p["trace_bytes"] == 8 * 50 * ((reads.shape[0] + 63) // 64 * 64), p
         K.search(idx, q, r)                          # the index and reads are untouched by the probe
         K.transfer_to_cpu(r)
         assert np.array_equal(r.array(), K.search_array(idx, reads, "task"))
@@ -36,7 +37,8 @@ def test_replay_probe_counts_and_rejects(kfmi_mod):
         with pytest.raises(K.KfmiError) as e:
             K.probe_replay(idx, q)
         assert e.value.code == 33
-    with pytest.raises(K.KfmiError):
-        K.probe_replay(idx, q, unroll=3)
+    for u, g in ((3, 1), (1, 3)):
+        with pytest.raises(K.KfmiError):
+            K.probe_replay(idx, q, unroll=u, groups=g)
     for h in (q, r, idx):
         h.close()
