@@ -24,7 +24,8 @@ STUB = textwrap.dedent(r"""
     txt = bench.bench_text(D, 50_000)
     env = {k: os.environ[k] for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR",
                                       "MASTER_PORT", "KFMI_BENCH_LAUNCHER")}
-    rows = D.gather(dict(env, pid=os.getpid(), text_head=bytes(txt[:32]).decode(), text_len=len(txt)))
+    rows = D.gather(dict(env, pid=os.getpid(), text_head=bytes(txt[:32]).decode(), text_len=len(txt),
+                         shared=type(txt).__name__ == "mmap"))
     if D.rank == 0:
         print(json.dumps({"rows": rows}), flush=True)
     else:
@@ -39,11 +40,11 @@ def _stub(tmp_path):
     return s
 
 
-def _spawn(tmp_path, n, mode, timeout=180):
+def _spawn(tmp_path, n, mode, timeout=180, extra_env=None):
     drv = (f"import sys; sys.path.insert(0, {str(REPO)!r}); sys.path.insert(0, {str(REPO / 'k-step_fm-index_amd')!r});"
            f"import bench; sys.exit(bench.spawn_ranks({n}, [{mode!r}], script={str(_stub(tmp_path))!r}, grace_s=5))")
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
-    env.update(OMP_NUM_THREADS="1", TMPDIR=str(tmp_path))
+    env.update(OMP_NUM_THREADS="1", TMPDIR=str(tmp_path), **(extra_env or {}))
     return subprocess.run([sys.executable, "-c", drv], capture_output=True, text=True, env=env, timeout=timeout,
                           cwd=str(tmp_path))
 
@@ -63,7 +64,18 @@ def test_spawn_ranks_starts_n_ranks_and_relays_rank0(tmp_path):
     # one text for the node, the same bytes on every rank, file gone afterwards
     assert len({r["text_head"] for r in rows}) == 1 and {r["text_len"] for r in rows} == {50_000}
     assert not list(tmp_path.glob("kfmi_bench_*"))
+    assert all(r["shared"] for r in rows)
     assert "rank 1 stdout line" in p.stderr and "rank 2 stdout line" in p.stderr
+
+
+def test_node_shared_text_falls_back_to_private_copies(tmp_path):
+    """No room for the node-shared file (forced here): every rank keeps its own
+    copy of the same text, and the run goes on."""
+    p = _spawn(tmp_path, 2, "ok", extra_env={"KFMI_BENCH_NODE_SHARED": "0"})
+    assert p.returncode == 0, p.stderr[-2000:]
+    rows = json.loads([ln for ln in p.stdout.splitlines() if ln.strip()][0])["rows"]
+    assert not any(r["shared"] for r in rows) and len({r["text_head"] for r in rows}) == 1
+    assert "KFMI_BENCH_NODE_SHARED=0" in p.stderr
 
 
 def test_spawn_ranks_fails_when_a_rank_fails(tmp_path):
