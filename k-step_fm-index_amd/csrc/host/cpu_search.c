@@ -69,6 +69,15 @@ CS_INLINE uint32_t cs_plane(uint32_t K, uint32_t NB, int inter, uint32_t s, uint
   return inter ? w * 2u * K + 2u * s + t : s * 2u * NB + t * NB + w;
 }
 
+/* cs_top_bits[k]: the k most significant bits of a word (row p of a 32-row
+ * word is bit 31 - p, MSB first) */
+static const uint32_t cs_top_bits[33] = {
+  0x00000000u, 0x80000000u, 0xC0000000u, 0xE0000000u, 0xF0000000u, 0xF8000000u, 0xFC000000u, 0xFE000000u,
+  0xFF000000u, 0xFF800000u, 0xFFC00000u, 0xFFE00000u, 0xFFF00000u, 0xFFF80000u, 0xFFFC0000u, 0xFFFE0000u,
+  0xFFFF0000u, 0xFFFF8000u, 0xFFFFC000u, 0xFFFFE000u, 0xFFFFF000u, 0xFFFFF800u, 0xFFFFFC00u, 0xFFFFFE00u,
+  0xFFFFFF00u, 0xFFFFFF80u, 0xFFFFFFC0u, 0xFFFFFFE0u, 0xFFFFFFF0u, 0xFFFFFFF8u, 0xFFFFFFFCu, 0xFFFFFFFEu,
+  0xFFFFFFFFu};
+
 /* rows of code c among the first o rows of the block at pl (or among the
  * others when inv): the bit-plane count of the reference's inner loop.
  * sel(p, bit) = bit ? p : ~p is p ^ (bit - 1). */
@@ -76,10 +85,10 @@ CS_INLINE uint32_t cs_count(uint32_t K, uint32_t NB, int inter, const uint32_t *
 {
   uint32_t pop = 0, w, s;
   for (w = 0; w < NB; ++w) {
-    /* the top clamp(o - 32w, 0, 32) bits, without a branch on the (random) offset */
-    const int64_t sh = (int64_t) o - 32 * (int64_t) w;
-    const uint32_t bits = (uint32_t) (sh < 0 ? 0 : (sh > 32 ? 32 : sh));
-    uint32_t m = (uint32_t) (~(~0ull >> bits) >> 32);
+    /* the top clamp(o - 32w, 0, 32) bits, from a table: no branch on the
+     * (random) offset, which a compare-and-shift turns into one */
+    const int32_t sh = (int32_t) o - 32 * (int32_t) w;
+    uint32_t m = cs_top_bits[sh < 0 ? 0 : (sh > 32 ? 32 : sh)];
     if (inv) m = ~m;
     for (s = 0; s < K; ++s) {
       const uint32_t cs = (c >> (2u * s)) & 3u;
