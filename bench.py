@@ -640,9 +640,12 @@ def variant_roofline(blocks: int, b_lf: int, lf_ms: float, a, backend: str, pmc:
     row = (pmc or {}).get("backends", {}).get(f"{backend}@k{k or a.k}")
     if row:
         req = row["rdreq_per_launch"]
+        # no ceiling fraction here: the probe's ceiling is measured on uniformly
+        # random 64/128-B lines, and other layouts' request mixes (64-B lines,
+        # an L2-resident superblock table, 96 GB tables) sit on either side of
+        # it -- coop-packed issues 58.6 G/s, coop-grp 49.9
         out.update({"fabric_read_requests_per_launch": req, "line_requests_per_query": round(req / a.queries, 2),
                     "line_requests_G_per_s": round(req / (lf_ms / 1e3) / 1e9, 2),
-                    "line_request_frac": round(req / (lf_ms / 1e3) / 1e9 / ceiling, 3),
                     "l2_requests_per_launch": row.get("tcc_req_per_launch"),
                     "pmc_kernel_ms": row.get("kernel_ms_under_pmc"), "pmc_source": pmc.get("source")})
     return out
