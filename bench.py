@@ -1416,8 +1416,15 @@ def main():
                                                       for x in replay},
                              "replay_ms": {f"u{x['unroll']}g{x['groups']}": round(x["ms"], 4) for x in replay},
                              "lines_per_launch": replay[0]["lines"], "trace_bytes_per_launch": replay[0]["trace_bytes"],
-                             "frac_of_best_replay": round(blocks / (lf_avg_ms / 1e3) / 1e9 /
-                                                          max(x["G_lines_per_s"] for x in replay), 3),
+                             # requests: the replay's lines plus its trace stream (8 B per read per
+                             # K-step, sequential 128-B requests), scaled by the kernel's measured
+                             # requests per line (PMC) -- an estimate, shown beside the kernel's own
+                             "replay_best_G_requests_per_s_est": round(
+                                 ((rdreq or blocks) + replay[0]["trace_bytes"] / 128) /
+                                 (min(x["ms"] for x in replay) / 1e3) / 1e9, 2),
+                             "note": "not a ceiling: the replay streams its trace beside the lines; it shows "
+                                     "whether lifting the LF dependence (1-8 K-steps of loads in flight per "
+                                     "lane) raises the request rate (DESIGN.md 5)",
                              "what": "kfmi_probe_replay: every (K-step, read) end's MID128 line recorded by a trace "
                                      "launch, then the task kernel's loads for them issued from the trace (no LF "
                                      "dependence): uU = U K-steps of C++ loads in flight per lane, u0 = the kernel's "
