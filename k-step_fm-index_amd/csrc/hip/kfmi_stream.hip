@@ -42,7 +42,6 @@ struct StreamSlot {
   hipEvent_t done = nullptr;
   hipEvent_t x0 = nullptr, x1 = nullptr;   /* bracket the chunk's H2D (link time of its mode) */
   bool packed_mode = false;                /* this chunk's reads went over PCIe as host-packed words */
-  int inflight = 1;                        /* copies queued on the link with this one (busy slots, incl. it) */
   kfmi_dev_queries dq;         /* device ascii + packed of one chunk */
   uint32_t* d_res = nullptr;
   uint8_t* h_in = nullptr;     /* pinned staging */
@@ -60,9 +59,11 @@ struct StreamPool {
    * (0 = not measured yet).  Host: EMA of packing / staging time per ASCII
    * byte.  Link: the fastest H2D seen per byte sent (r_xa, r_xp; the events
    * bracketing a copy also count time queued behind other slots' copies), and
-   * an EMA of the bracketed time per byte divided by the copies that were in
-   * flight with it (q_xa, q_xp): on a link other processes share, the fastest
-   * copy ever seen is an idle-link figure, and the model takes the larger. */
+   * an EMA of the bracketed time per byte (q_xa, q_xp): on a link other
+   * processes share, the fastest copy ever seen is an idle-link figure, and
+   * the model takes the larger -- which also charges a copy for the queue
+   * ahead of it, so it leans to packing exactly when the link is the bound
+   * (profiles/r04/stream_contention_r4f*.jsonl). */
   double r_pack = 0, r_stage = 0, r_xa = 0, r_xp = 0, q_xa = 0, q_xp = 0;
 };
 /* One pool per (device, group member): a single-device search uses member 0;
@@ -399,10 +400,10 @@ static int32_t stream_on(kfmi_dev_index* di, int member, const char* ascii, uint
       if (hipEventElapsedTime(&x, s.x0, s.x1) == hipSuccess && s.n && x > 0) {
         if (s.packed_mode) {
           keep_min(pool.r_xp, x / (s.n * pbytes));
-          ema(pool.q_xp, x / (s.n * pbytes) / s.inflight);
+          ema(pool.q_xp, x / (s.n * pbytes));
         } else {
           keep_min(pool.r_xa, x / (s.n * abytes));
-          ema(pool.q_xa, x / (s.n * abytes) / s.inflight);
+          ema(pool.q_xa, x / (s.n * abytes));
         }
       }
     }
@@ -434,8 +435,6 @@ static int32_t stream_on(kfmi_dev_index* di, int member, const char* ascii, uint
       t_link = host_pack ? done_p : done_a;
     }
     s.packed_mode = host_pack;
-    s.inflight = 1;
-    for (int k = 0; k < nslot; ++k) s.inflight += (&pool.slot[k] != &s && pool.slot[k].busy) ? 1 : 0;
     npacked += host_pack ? s.n : 0;
     const auto th = clk::now();
     if (host_pack) par_pack(src, s.n, size, rem, s.h_pk);
