@@ -984,6 +984,11 @@ def main():
     if dev_agg["shared_devices"] and D.rank == 0:
         log(f"WARNING: {D.world} ranks on {dev_agg['distinct_devices']} distinct GPU(s) -- a rehearsal, "
             "not a multi-GPU measurement (n_gpus reports distinct devices, no scaling claim)")
+    if dev_agg["shared_devices"]:
+        # ranks rehearsing on one card share its PCIe link: the streamed
+        # search's transfer-mode model charges its link by that many
+        # (kfmi_search_stream, KFMI_LINK_SHARERS)
+        os.environ.setdefault("KFMI_LINK_SHARERS", str(max(dev_agg["ranks_per_device"])))
     ingest_on = a.ingest == "on" or (a.ingest == "auto" and D.world <= 2)
     ph.mark("init")
 

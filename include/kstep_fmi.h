@@ -256,7 +256,8 @@ int32_t kfmi_count_blocks(void *index, void *queries, uint64_t *blocks);
  * carries 4 bytes per 16 bases) or goes as ASCII (pinned: DMA'd directly;
  * pageable: staged through pinned buffers) and is packed on the device.  By
  * default the choice is made per chunk from the measured host-packing and
- * link rates (whichever finishes first); KFMI_STREAM_HOSTPACK=1 packs every
+ * link rates (whichever finishes first; KFMI_LINK_SHARERS=n when n processes
+ * share the device's PCIe link); KFMI_STREAM_HOSTPACK=1 packs every
  * chunk on the host, =0 sends every chunk as ASCII.  Host work runs on KFMI_HOST_THREADS threads (default min(16,
  * cores)).  Blocking; kfmi_last_timing: total = wall time of the call, pack =
  * host packing / staging time, lf = time blocked on chunks in flight.

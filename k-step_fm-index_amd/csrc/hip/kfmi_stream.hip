@@ -57,14 +57,12 @@ struct StreamPool {
   StreamSlot slot[NSLOT_MAX];
   /* adaptive transfer mode: measured costs in ms per byte, kept across calls
    * (0 = not measured yet).  Host: EMA of packing / staging time per ASCII
-   * byte.  Link: the fastest H2D seen per byte sent (r_xa, r_xp; the events
-   * bracketing a copy also count time queued behind other slots' copies), and
-   * an EMA of the bracketed time per byte (q_xa, q_xp): on a link other
-   * processes share, the fastest copy ever seen is an idle-link figure, and
-   * the model takes the larger -- which also charges a copy for the queue
-   * ahead of it, so it leans to packing exactly when the link is the bound
-   * (profiles/r04/stream_contention_r4f*.jsonl). */
-  double r_pack = 0, r_stage = 0, r_xa = 0, r_xp = 0, q_xa = 0, q_xp = 0;
+   * byte.  Link: the fastest H2D seen per byte sent (the events bracketing a
+   * copy also count time queued behind other slots' copies) -- an idle-link
+   * figure, which the model multiplies by the processes that share this
+   * device's link (KFMI_LINK_SHARERS, default 1: one GPU per rank; ranks
+   * rehearsing on one card set it; profiles/r04/stream_contention_r4*.jsonl). */
+  double r_pack = 0, r_stage = 0, r_xa = 0, r_xp = 0;
 };
 /* One pool per (device, group member): a single-device search uses member 0;
  * the members of a device group stream from pools of their own, so two
@@ -374,6 +372,8 @@ static int32_t stream_on(kfmi_dev_index* di, int member, const char* ascii, uint
   }
   /* cost model: pool.r_* per byte (see StreamPool) -> ms per read */
   const double abytes = (double) size, pbytes = 4.0 * rows;
+  const char* ls = getenv("KFMI_LINK_SHARERS");
+  const double sharers = ls && atoi(ls) > 1 ? (double) atoi(ls) : 1.0;
   uint64_t npacked = 0;
   double t_host = 0, t_link = 0;                      /* model clocks of this call */
   auto ema = [](double& v, double x) { v = v > 0 ? 0.6 * v + 0.4 * x : x; };
@@ -398,13 +398,8 @@ static int32_t stream_on(kfmi_dev_index* di, int member, const char* ascii, uint
       if (!pin_out) par_copy(results + 2 * s.q0, s.h_out, 8ull * s.n);
       float x = 0;
       if (hipEventElapsedTime(&x, s.x0, s.x1) == hipSuccess && s.n && x > 0) {
-        if (s.packed_mode) {
-          keep_min(pool.r_xp, x / (s.n * pbytes));
-          ema(pool.q_xp, x / (s.n * pbytes));
-        } else {
-          keep_min(pool.r_xa, x / (s.n * abytes));
-          ema(pool.q_xa, x / (s.n * abytes));
-        }
+        if (s.packed_mode) keep_min(pool.r_xp, x / (s.n * pbytes));
+        else keep_min(pool.r_xa, x / (s.n * abytes));
       }
     }
     s.busy = false;
@@ -427,7 +422,7 @@ static int32_t stream_on(kfmi_dev_index* di, int member, const char* ascii, uint
     else {
       const double dn = (double) s.n;
       const double hp_ms = pool.r_pack * abytes * dn, st_ms = pin_in ? 0.0 : pool.r_stage * abytes * dn;
-      const double xp = std::max(pool.r_xp, pool.q_xp), xa = std::max(pool.r_xa, pool.q_xa);
+      const double xp = pool.r_xp * sharers, xa = pool.r_xa * sharers;
       const double done_p = std::max(t_host + hp_ms, t_link) + xp * pbytes * dn;
       const double done_a = std::max(t_host + st_ms, t_link) + xa * abytes * dn;
       host_pack = done_p <= done_a;

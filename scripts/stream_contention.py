@@ -11,7 +11,8 @@ library then splits the host's CPU share among the ranks, kfmi_host_threads).
 
 On a one-GPU box the P processes also share the card and its PCIe link, so
 the ASCII mode is charged more than on an 8-GPU node (one link per rank);
-the host-side numbers (packing time, staging) are what this measures.
+the workers say so to the library's cost model (KFMI_LINK_SHARERS=P); the
+host-side numbers (packing time, staging) are what this measures.
 Summary per (P, input, mode): every rank's median wall over rounds 1.. (round
 0 -- first-touch of the output arrays and staging buffers -- excluded), then
 the slowest rank.
@@ -97,7 +98,9 @@ def main() -> int:
                 for rank in range(P):
                     code = WORKER % {"root": str(ROOT), "pkg": str(ROOT / "k-step_fm-index_amd"),
                                      "args": repr((rank, P, bdir, a.rounds, a.ref_size, a.queries, a.qlen))}
-                    env = dict(os.environ, LOCAL_WORLD_SIZE=str(P), LOCAL_RANK=str(rank))
+                    # the P processes share this one card's PCIe link (KFMI_LINK_SHARERS: the
+                    # streamed search's link cost model; on an 8-GPU node each rank has its own)
+                    env = dict(os.environ, LOCAL_WORLD_SIZE=str(P), LOCAL_RANK=str(rank), KFMI_LINK_SHARERS=str(P))
                     ps.append(subprocess.Popen([sys.executable, "-c", code], env=env, stdout=subprocess.PIPE,
                                                stderr=subprocess.PIPE, text=True))
                 rows = []
