@@ -241,7 +241,10 @@ void par_copy(void* dst, const void* src, uint64_t bytes)
 {
   HostPool& hp = HostPool::get();
   const int nt = hp.size();
-  if (nt == 1 || bytes < (8u << 20)) {
+  /* a streamed chunk's results (8 B x 2^19 reads = 4 MB) are copied here one
+   * by one: one thread at ~8 GB/s made them 10 of the 21 ms a 10M-read
+   * pageable batch took (profiles/r04/bench_r4c.json end_to_end) */
+  if (nt == 1 || bytes < (1u << 20)) {
     memcpy(dst, src, bytes);
     return;
   }
