@@ -169,3 +169,21 @@ def test_cpu_search_argument_errors(kfmi_mod):
     assert np.array_equal(r.array(), kfmi_mod.search_cpu_array(I, t[:20].reshape(2, 10).copy()))
     for h in (q, r, I):
         h.close()
+
+
+@pytest.mark.gpu
+def test_cpu_search_on_a_device_resident_index(kfmi_mod):
+    """An index built on the device without a host image: searchIndexCPU
+    fetches its entries once (kfmi_host_entries, one thread of the team) and
+    returns what the GPU backends return."""
+    K = kfmi_mod
+    if K.device_count() < 1:
+        pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
+    K.set_device(0)
+    t, text, rng = _random_case(300_001, 12)
+    idx = K.Index.build(text, k=2, d=64, gpu=True, host_image=False)
+    st = rng.integers(0, len(text) - 100, size=20_000)
+    q = np.ascontiguousarray(t[st[:, None] + np.arange(100)[None, :]])
+    want = K.search_array(idx, q, "task-mid")
+    assert np.array_equal(K.search_cpu_array(idx, q, nthreads=4), want)
+    idx.close()
