@@ -563,7 +563,35 @@ def cpu_reference_baseline(idx, reads, ns, k, d, thr, res_gpu):
     return best
 
 
-def probe_leg() -> dict | None:
+def probe_rows(stdout: str, gb: str) -> tuple[int | None, list]:
+    """gather_probe's JSON rows for its main table of `gb` GB (the tool also
+    probes 4 MB / 200 MB tables after the main one; those rows are dropped)."""
+    rows, table, want = [], None, int(float(gb) * 1e9) & ~127
+    for ln in stdout.splitlines():
+        try:
+            d = json.loads(ln)
+        except ValueError:
+            continue
+        if "table_bytes" in d:
+            table = d["table_bytes"]
+        elif "kind" in d and table == want:
+            rows.append(d)
+    return (want if rows else None), rows
+
+
+def best_of_runs(runs: list) -> list:
+    """Per (kind, line size), the fastest of several runs' rows (a ceiling is
+    the rate the path can reach: the max over repeats, not their mean)."""
+    best = {}
+    for rows in runs:
+        for r in rows:
+            k = (r["kind"], r["line_B"])
+            if k not in best or r["Glines_s"] > best[k]["Glines_s"]:
+                best[k] = dict(r)
+    return list(best.values())
+
+
+def probe_leg(ic_runs: int = 2) -> dict | None:
     """The random-line request ceiling on this box, measured beside the kernel:
     bin/gather_probe (csrc/tools/gather_probe.hip) reads uniformly random lines
     -- independent per lane, cooperative, and dependent chains (the LF shape) --
@@ -572,37 +600,34 @@ def probe_leg() -> dict | None:
     path's own limit, with no DRAM behind it).  The LF kernel's requests are a
     mix of both (its early steps' lines stay in the caches), so the ceiling it
     is held against is the larger rate, the Infinity-Cache-resident one
-    (DESIGN.md 5).  Run as a child process while this one idles.  None when the
-    tool is missing or fails."""
+    (DESIGN.md 5); that table is probed `ic_runs` times and each kind keeps
+    its best run, so one slow run does not put the ceiling under the kernel.
+    Run as a child process while this one idles.  None when the tool is
+    missing or fails."""
     import subprocess
     exe = ROOT / "k-step_fm-index_amd" / "bin" / "gather_probe"
     if not exe.exists():
         return None
     out = {}
-    for gb, key in (("3", "hbm_3GB"), ("0.2", "infinity_cache_200MB")):
-        try:
-            p = subprocess.run([str(exe), gb, "512"], capture_output=True, text=True, timeout=300)
-        except (OSError, subprocess.SubprocessError):
-            return None
-        if p.returncode != 0:
-            return None
-        rows, table, want = [], None, int(float(gb) * 1e9) & ~127
-        for ln in p.stdout.splitlines():
+    for gb, key, n in (("3", "hbm_3GB", 1), ("0.2", "infinity_cache_200MB", max(1, ic_runs))):
+        runs, table = [], None
+        for _ in range(n):
             try:
-                d = json.loads(ln)
-            except ValueError:
-                continue
-            if "table_bytes" in d:
-                table = d["table_bytes"]
-            elif "kind" in d and table == want:   # the tool also probes 4 MB / 200 MB tables after the main one
-                rows.append(d)
-        if not rows:
-            return None
+                p = subprocess.run([str(exe), gb, "512"], capture_output=True, text=True, timeout=300)
+            except (OSError, subprocess.SubprocessError):
+                return None
+            if p.returncode != 0:
+                return None
+            table, rows = probe_rows(p.stdout, gb)
+            if not rows:
+                return None
+            runs.append(rows)
+        rows = best_of_runs(runs)
         best = max(rows, key=lambda x: x["Glines_s"])
         chain = [x for x in rows if x["kind"].startswith("chain")]
         out[key] = {"best_G_lines_per_s": best["Glines_s"], "best_kind": f"{best['kind']} {best['line_B']} B",
                     "chain_G_lines_per_s": max(x["Glines_s"] for x in chain) if chain else None,
-                    "table_bytes": table, "rows": rows}
+                    "table_bytes": table, "runs": n, "rows": rows}
     ceil_key = max(out, key=lambda k: out[k]["best_G_lines_per_s"])
     return dict(out, ceiling_G_lines_per_s=out[ceil_key]["best_G_lines_per_s"], ceiling_from=ceil_key)
 
@@ -1409,8 +1434,9 @@ def main():
                          "line_requests_G_per_s": round(rdreq / (lf_avg_ms / 1e3) / 1e9, 2) if rdreq else None,
                          "line_request_ceiling_G_per_s": ceiling,
                          "line_request_ceiling_source": (f"gather_probe on this box, this run: the larger of the "
-                                                         f"3 GB (HBM) and 200 MB (Infinity-Cache-resident) random-line "
-                                                         f"rates ({probe['ceiling_from']})") if probe else
+                                                         f"3 GB (HBM) and 200 MB (Infinity-Cache-resident, best of "
+                                                         f"{probe['infinity_cache_200MB']['runs']} runs per kind) "
+                                                         f"random-line rates ({probe['ceiling_from']})") if probe else
                          "profiles/r03/gather_probe_r3g.jsonl: 200 MB table, Infinity-Cache resident (another box)",
                          "line_request_frac": round(rdreq / (lf_avg_ms / 1e3) / 1e9 / ceiling, 3) if rdreq else None,
                          # the same question on the kernel's own fetches (distinct blocks = lines it loads):

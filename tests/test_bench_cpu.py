@@ -91,3 +91,25 @@ def test_traffic_variants_parser(tmp_path):
     out = json.loads(p.stdout)
     assert out["backends"]["task-mid@k2"]["rdreq_per_launch"] == 101      # median of launches 2, 3 (101, 102)
     assert out["backends"]["coop-grp@k4"]["rdreq_per_launch"] == 104 and out["backends"]["coop-grp@k4"]["launches_timed"] == 1
+
+
+def test_probe_rows_and_best_of_runs():
+    """gather_probe output: only the main table's rows count (the 4 MB / 200 MB
+    tables the tool probes afterwards are dropped), and repeated runs keep each
+    kind's fastest row -- the ceiling is the max over repeats."""
+    import json
+    want = int(0.2e9) & ~127
+
+    def out(rate_a, rate_b):
+        return "\n".join([json.dumps({"table_bytes": want}),
+                          json.dumps({"kind": "chain1", "line_B": 128, "Glines_s": rate_a}),
+                          "not json",
+                          json.dumps({"kind": "indep", "line_B": 64, "Glines_s": rate_b}),
+                          json.dumps({"table_bytes": 4 << 20}),
+                          json.dumps({"kind": "indep", "line_B": 64, "Glines_s": 172.0})])
+    t1, r1 = bench.probe_rows(out(54.1, 54.3), "0.2")
+    t2, r2 = bench.probe_rows(out(54.9, 53.9), "0.2")
+    assert t1 == t2 == want and len(r1) == len(r2) == 2
+    best = {(r["kind"], r["line_B"]): r["Glines_s"] for r in bench.best_of_runs([r1, r2])}
+    assert best == {("chain1", 128): 54.9, ("indep", 64): 54.3}
+    assert bench.probe_rows(out(1, 1), "3") == (None, [])
