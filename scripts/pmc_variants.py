@@ -54,6 +54,8 @@ def main():
     r = K.Results.alloc(a.queries)
     order, first = [], None
     for k, names in ((2, a.backends), (4, a.k4_backends)):
+        if not [x for x in names.split(",") if x]:
+            continue
         idx = K.Index.build(text, k=k, d=64, gpu=True, host_image=False)
         for b in [x for x in names.split(",") if x]:
             K.set_backend(b)
