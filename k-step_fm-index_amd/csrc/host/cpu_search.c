@@ -193,7 +193,7 @@ static int32_t cs_setup(kfmi_fmi_t *f, const kfmi_qrys_t *q, const kfmi_res_t *r
   if (!f || !q || !r || !f->h_index) return KFMI_E_BAD_ARGUMENT;
   if (f->steps < 1 || f->steps > KFMI_MAX_STEPS || f->chunk < 32 || f->chunk % 32 || f->nentries < 1)
     return KFMI_E_BAD_ARGUMENT;
-  if (r->num < q->num || (q->num && !q->h_queries)) return KFMI_E_BAD_ARGUMENT;
+  if (r->num < q->num || (q->num && (!q->h_queries || !r->h_results))) return KFMI_E_BAD_ARGUMENT;
   memset(ix, 0, sizeof(*ix));
   ix->ent = f->h_index;
   ix->ew = f->entry_words;
