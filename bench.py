@@ -632,6 +632,25 @@ def probe_leg(ic_runs: int = 2) -> dict | None:
     return dict(out, ceiling_G_lines_per_s=out[ceil_key]["best_G_lines_per_s"], ceiling_from=ceil_key)
 
 
+def replay_requests(replay: list | None, pmc: dict | None) -> dict | None:
+    """The replay probe's fabric request rate per mode: requests per launch
+    from the committed PMC pass of kfmi_probe_replay on the bench batch
+    (scripts/pmc_replay.py; the line stream is the same in every mode, so a
+    mode the pass did not cover takes the median of the measured ones) over
+    this run's replay time.  None without the probe or the counts."""
+    if not replay or not pmc or not pmc.get("rdreq_per_launch"):
+        return None
+    counts = pmc["rdreq_per_launch"]
+    med = float(np.median(list(counts.values())))
+    req, rate = {}, {}
+    for x in replay:
+        m = f"u{x['unroll']}g{x['groups']}"
+        req[m] = int(counts.get(m, med))
+        rate[m] = round(req[m] / (x["ms"] / 1e3) / 1e9, 2)
+    best = max(rate, key=rate.get)
+    return {"requests": req, "G_requests_per_s": rate, "best_G_requests_per_s": rate[best], "best_mode": best}
+
+
 VARIANTS_PMC = ROOT / "profiles" / "r04" / "traffic_variants.json"
 
 
@@ -1137,7 +1156,7 @@ def main():
     # hits included (MI355X_MICROARCH.md HBM section), so requests x 128 B is an
     # UPPER BOUND on HBM bytes, not HBM bytes: roofline.traffic stays null unless
     # the profile carries a counter that excludes Infinity-Cache hits.
-    traffic, traffic_src, rdreq = None, None, None
+    traffic, traffic_src, rdreq, replay_pmc = None, None, None, None
     tj = Path(a.traffic_json)
     if tj.exists() and D.world == 1:   # a one-GPU PMC profile says nothing about N > 1 runs
         try:
@@ -1146,6 +1165,7 @@ def main():
                     and tr.get("qlen", 100) == a.qlen and tr.get("k", 2) == a.k and tr.get("d", 64) == a.d):
                 traffic, traffic_src = tr.get("hbm_bytes_per_launch_excl_infinity_cache"), tr.get("source")
                 rdreq = tr.get("rdreq_per_launch")
+                replay_pmc = tr.get("replay")
         except Exception:
             traffic = None
     # the kernel's own request stream replayed without its LF dependence
@@ -1195,9 +1215,21 @@ def main():
     ph.mark("gather")
     probe = probe_leg() if D.world == 1 and D.rank == 0 else None
     ceiling = probe["ceiling_G_lines_per_s"] if probe else PROBE_CEILING_GLINES
+    ceiling_src = ((f"gather_probe on this box, this run: the larger of the 3 GB (HBM) and 200 MB "
+                    f"(Infinity-Cache-resident, best of {probe['infinity_cache_200MB']['runs']} runs per kind) "
+                    f"random-line rates ({probe['ceiling_from']})") if probe else
+                   "profiles/r03/gather_probe_r3g.jsonl: 200 MB table, Infinity-Cache resident (another box)")
     if probe:
         extra["line_request_probe"] = probe
         log(f"gather probe: ceiling {ceiling} G lines/s ({probe['ceiling_from']})")
+    rp = replay_requests(replay, replay_pmc)
+    if rp and rp["best_G_requests_per_s"] > ceiling:
+        # the kernel's own line stream without its dependence issued faster than
+        # the probe's uniform lines: that rate is the ceiling for this mix
+        ceiling = rp["best_G_requests_per_s"]
+        ceiling_src = (f"kfmi_probe_replay on this box, this run: the kernel's own line stream re-issued without "
+                       f"its LF dependence ({rp['best_mode']}), fabric requests per launch from "
+                       f"{replay_pmc.get('source', 'the committed PMC pass')}; above the gather_probe rate")
     if c5 is not None:
         extra["config5"] = c5
     if k4 is not None:
@@ -1433,11 +1465,7 @@ def main():
                          "line_requests_per_query": round(rdreq / a.queries, 2) if rdreq else None,
                          "line_requests_G_per_s": round(rdreq / (lf_avg_ms / 1e3) / 1e9, 2) if rdreq else None,
                          "line_request_ceiling_G_per_s": ceiling,
-                         "line_request_ceiling_source": (f"gather_probe on this box, this run: the larger of the "
-                                                         f"3 GB (HBM) and 200 MB (Infinity-Cache-resident, best of "
-                                                         f"{probe['infinity_cache_200MB']['runs']} runs per kind) "
-                                                         f"random-line rates ({probe['ceiling_from']})") if probe else
-                         "profiles/r03/gather_probe_r3g.jsonl: 200 MB table, Infinity-Cache resident (another box)",
+                         "line_request_ceiling_source": ceiling_src,
                          "line_request_frac": round(rdreq / (lf_avg_ms / 1e3) / 1e9 / ceiling, 3) if rdreq else None,
                          # the same question on the kernel's own fetches (distinct blocks = lines it loads):
                          # its rate against the fastest replay of the identical request stream
@@ -1447,15 +1475,19 @@ def main():
                                                       for x in replay},
                              "replay_ms": {f"u{x['unroll']}g{x['groups']}": round(x["ms"], 4) for x in replay},
                              "lines_per_launch": replay[0]["lines"], "trace_bytes_per_launch": replay[0]["trace_bytes"],
-                             # requests: the replay's lines plus its trace stream (8 B per read per
-                             # K-step, sequential 128-B requests), scaled by the kernel's measured
-                             # requests per line (PMC) -- an estimate, shown beside the kernel's own
-                             "replay_best_G_requests_per_s_est": round(
-                                 ((rdreq or blocks) + replay[0]["trace_bytes"] / 128) /
-                                 (min(x["ms"] for x in replay) / 1e3) / 1e9, 2),
-                             "note": "not a ceiling: the replay streams its trace beside the lines; it shows "
-                                     "whether lifting the LF dependence (1-8 K-steps of loads in flight per "
-                                     "lane) raises the request rate (DESIGN.md 5)",
+                             # requests: the replay's lines plus its trace stream, counted by the
+                             # committed PMC pass of the same kernels on the same batch (rocprofv3
+                             # TCC_EA0_RDREQ; modes that pass did not cover take the median count)
+                             "kernel_G_requests_per_s": round(rdreq / (lf_avg_ms / 1e3) / 1e9, 2) if rdreq else None,
+                             **({"replay_requests_per_launch": rp["requests"],
+                                 "replay_G_requests_per_s": rp["G_requests_per_s"],
+                                 "replay_best_G_requests_per_s": rp["best_G_requests_per_s"],
+                                 "replay_best_mode": rp["best_mode"],
+                                 "replay_requests_source": replay_pmc.get("source")} if rp else {}),
+                             "note": "the replay streams its trace beside the lines (its requests include "
+                                     "it); it shows whether lifting the LF dependence (1-8 K-steps of loads in "
+                                     "flight per lane) raises the request rate, and when its rate is above the "
+                                     "gather_probe's it is the stated ceiling (DESIGN.md 5)",
                              "what": "kfmi_probe_replay: every (K-step, read) end's MID128 line recorded by a trace "
                                      "launch, then the task kernel's loads for them issued from the trace (no LF "
                                      "dependence): uU = U K-steps of C++ loads in flight per lane, u0 = the kernel's "

@@ -50,25 +50,21 @@ def run():
 
 
 def summarize(fn: str):
-    disp = {}
-    for row in csv.DictReader(open(fn)):
-        d = disp.setdefault(int(row["Dispatch_Id"]), {"name": row["Kernel_Name"].split("(")[0],
-                                                      "ms": (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e6})
-        d[row["Counter_Name"]] = float(row["Counter_Value"])
-    by = {}
-    for k in sorted(disp):
-        d = disp[k]
-        by.setdefault(d["name"], []).append(d)
-    for name, rows in by.items():
-        if len(rows) > 1:
-            rows = rows[1:]          # the first launch of each kernel is its warm-up
-        req = statistics.median(x.get("TCC_EA0_RDREQ_sum", 0) for x in rows)
-        l2 = statistics.median(x.get("TCC_REQ_sum", 0) for x in rows)
+    """Per run of consecutive dispatches (the LF kernel's searches, then each
+    replay mode's launches in MODES order): medians of the counters, the first
+    launch of each run (its warm-up) dropped, and the request rate."""
+    sys.path.insert(0, str(ROOT / "scripts"))
+    from pmc_summary import runs
+    names = ["lf"] + [f"u{u}g{g}" for u, g in MODES]
+    for i, run in enumerate(runs(fn)):
+        rows = run[1:] if len(run) > 1 else run
+        req = statistics.median(x["c"].get("TCC_EA0_RDREQ_sum", 0) for x in rows)
+        l2 = statistics.median(x["c"].get("TCC_REQ_sum", 0) for x in rows)
         ms = statistics.median(x["ms"] for x in rows)
-        short = re.sub(r"\(anonymous namespace\)::", "", name)
-        print(json.dumps({"kernel": short, "launches": len(rows), "rdreq_per_launch": int(req),
-                          "tcc_req_per_launch": int(l2), "ms": round(ms, 4),
-                          "G_requests_per_s": round(req / (ms / 1e3) / 1e9, 2)}))
+        print(json.dumps({"run": names[i] if i < len(names) else i,
+                          "kernel": re.sub(r"\(anonymous namespace\)::|kfmi::", "", run[0]["name"]).split("(")[0],
+                          "launches": len(rows), "rdreq_per_launch": int(req), "tcc_req_per_launch": int(l2),
+                          "ms": round(ms, 4), "G_requests_per_s": round(req / (ms / 1e3) / 1e9, 2)}))
 
 
 if __name__ == "__main__":

@@ -41,7 +41,7 @@ def main():
     for i, run in enumerate(runs(a.csv)):
         rows = run[1:] if a.skip_first and len(run) > 1 else run
         names = sorted({c for x in rows for c in x["c"]})
-        short = re.sub(r"\(anonymous namespace\)::|kfmi::", "", run[0]["name"].split("(")[0])
+        short = re.sub(r"\(anonymous namespace\)::|kfmi::", "", run[0]["name"]).split("(")[0]
         print(json.dumps({"run": i, "kernel": short, "grid": run[0]["grid"], "dispatches": len(rows),
                           "ms": round(statistics.median(x["ms"] for x in rows), 4),
                           **{c: statistics.median(x["c"].get(c, 0.0) for x in rows) for c in names}}))

@@ -113,3 +113,25 @@ def test_probe_rows_and_best_of_runs():
     best = {(r["kind"], r["line_B"]): r["Glines_s"] for r in bench.best_of_runs([r1, r2])}
     assert best == {("chain1", 128): 54.9, ("indep", 64): 54.3}
     assert bench.probe_rows(out(1, 1), "3") == (None, [])
+
+
+def test_replay_requests_from_committed_counts():
+    """Replay request rates: a mode the PMC pass counted uses its count, the
+    others the median of the counted modes; the best mode is the fastest rate."""
+    replay = [{"unroll": 1, "groups": 1, "ms": 10.0}, {"unroll": 4, "groups": 2, "ms": 9.5},
+              {"unroll": 8, "groups": 2, "ms": 9.0}]
+    pmc = {"rdreq_per_launch": {"u1g1": 540_000_000, "u4g2": 538_000_000, "u0g2": 539_000_000}}
+    rp = bench.replay_requests(replay, pmc)
+    assert rp["requests"] == {"u1g1": 540_000_000, "u4g2": 538_000_000, "u8g2": 539_000_000}
+    assert rp["G_requests_per_s"]["u1g1"] == 54.0 and rp["best_mode"] == "u8g2"
+    assert rp["best_G_requests_per_s"] == round(539e6 / 9.0e-3 / 1e9, 2)
+    assert bench.replay_requests(None, pmc) is None and bench.replay_requests(replay, {}) is None
+
+
+def test_committed_traffic_profile_carries_replay_counts():
+    import json
+    tr = json.loads((bench.ROOT / "profiles" / "traffic.json").read_text())
+    assert tr["backend"] == "task-mid" and tr["rdreq_per_launch"] > 0
+    c = tr["replay"]["rdreq_per_launch"]
+    # every replay mode re-issues the kernel's lines plus its trace stream
+    assert all(v > tr["rdreq_per_launch"] for v in c.values())
