@@ -1150,20 +1150,21 @@ def main():
     bytes_io = reads.shape[0] * (q_in + 8)
     lf_avg_ms = float(np.mean(lf_ms))
     achieved = bytes_alg / (lf_avg_ms / 1e3) / 1e9
-    # fabric read requests per launch from the committed PMC profile of the same
-    # config (scripts/traffic_from_pmc.py: TCC_EA0_RDREQ, one request per random
-    # line of up to 128 B on gfx950).  These count every L2 miss, Infinity-Cache
-    # hits included (MI355X_MICROARCH.md HBM section), so requests x 128 B is an
-    # UPPER BOUND on HBM bytes, not HBM bytes: roofline.traffic stays null unless
-    # the profile carries a counter that excludes Infinity-Cache hits.
-    traffic, traffic_src, rdreq, replay_pmc = None, None, None, None
+    # traffic per launch from the committed PMC profile of the same config, by
+    # the guide's recipe (MI355X_MICROARCH.md HBM section): FETCH_SIZE in its own
+    # pass, doubled (gfx950 tallies a 128-B request at 64 B; every request here
+    # is 128 B, TCC_EA0_RDREQ_128B).  It counts every L2 miss, Infinity-Cache
+    # hits included, so it is the L2/fabric traffic and bounds the HBM bytes
+    # from above; no gfx950 counter separates the Infinity-Cache hits.
+    traffic, traffic_src, traffic_note, rdreq, replay_pmc = None, None, None, None, None
     tj = Path(a.traffic_json)
     if tj.exists() and D.world == 1:   # a one-GPU PMC profile says nothing about N > 1 runs
         try:
             tr = json.loads(tj.read_text())
             if (tr.get("backend") == a.backend and tr.get("queries") == a.queries and tr.get("ref_size") == a.ref_size
                     and tr.get("qlen", 100) == a.qlen and tr.get("k", 2) == a.k and tr.get("d", 64) == a.d):
-                traffic, traffic_src = tr.get("hbm_bytes_per_launch_excl_infinity_cache"), tr.get("source")
+                traffic = tr.get("fetch_size_corrected_bytes_per_launch")
+                traffic_src, traffic_note = tr.get("fetch_size_source"), tr.get("fetch_size_correction")
                 rdreq = tr.get("rdreq_per_launch")
                 replay_pmc = tr.get("replay")
         except Exception:
@@ -1456,6 +1457,12 @@ def main():
                          "lf_ms": round(lf_avg_ms, 4), "pack_ms": round(float(np.mean(pack_ms)), 4),
                          "naive_bytes_per_launch": 2 * (a.qlen // a.k) * b_lf * a.queries,
                          "traffic_source": traffic_src,
+                         "traffic_method": traffic_note,
+                         # the L2/fabric bytes per second the kernel moves (whole 128-B lines), and
+                         # how many of them per algorithmic byte: a random LF reads 36 B of a line
+                         # that can only be fetched whole, not a re-read
+                         "traffic_GB_per_s": round(traffic / (lf_avg_ms / 1e3) / 1e9, 1) if traffic else None,
+                         "traffic_over_algorithmic": round(traffic / bytes_alg, 3) if traffic else None,
                          # every LF is a random 128-B line: the binding limit is the rate of random line
                          # requests at the L2/fabric boundary, calibrated by gather_probe on the same 3 GB
                          # table size.  Requests x 128 B includes Infinity-Cache hits: an upper bound on HBM

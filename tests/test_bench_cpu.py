@@ -135,3 +135,17 @@ def test_committed_traffic_profile_carries_replay_counts():
     c = tr["replay"]["rdreq_per_launch"]
     # every replay mode re-issues the kernel's lines plus its trace stream
     assert all(v > tr["rdreq_per_launch"] for v in c.values())
+
+
+def test_committed_traffic_is_the_guides_fetch_size_recipe():
+    """roofline.traffic: FETCH_SIZE (KB) x 1024 x 2 (gfx950 tallies a 128-B
+    request at 64 B), consistent with the request-size pass: every request of
+    the LF kernel is 128 B, so the bytes equal TCC_EA0_RDREQ x 128 within 0.1 %."""
+    import json
+    tr = json.loads((bench.ROOT / "profiles" / "traffic.json").read_text())
+    b = tr["fetch_size_corrected_bytes_per_launch"]
+    assert b == round(tr["fetch_size_kb_per_launch"] * 2048)
+    sz = tr["request_sizes_per_launch"]
+    assert sz["TCC_EA0_RDREQ_128B"] / sz["TCC_EA0_RDREQ"] > 0.9999
+    assert abs(b - sz["TCC_EA0_RDREQ"] * 128) / b < 1e-3
+    assert abs(sz["TCC_EA0_RDREQ"] - tr["rdreq_per_launch"]) / tr["rdreq_per_launch"] < 1e-3
