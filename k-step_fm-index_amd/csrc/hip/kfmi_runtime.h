@@ -59,7 +59,8 @@ struct kfmi_dev_index {
 
 struct kfmi_dev_queries {
   int device = -1;
-  uint8_t* ascii = nullptr;    /* num*size bytes, plain layout */
+  uint8_t* ascii = nullptr;    /* num*size bytes, plain layout; null when the host packed the
+                                  reads on upload (`packed` is then already valid) */
   uint32_t* packed = nullptr;  /* (nwords + 1) x num u32 codes; row nwords: remainder codes */
   /* in-call reorder (KFMI_REORDER=1): keys/reads double buffers, row-major
    * code words, rocPRIM temporary storage; allocated on first use */
@@ -99,7 +100,14 @@ RwLock& index_lock(const void* f);
 struct DevCtx {
   bool init = false;
   hipStream_t st = nullptr;
+  /* pinned chunk buffers of host-packed query uploads (upload_queries), kept
+   * between calls; one upload at a time per device uses them */
+  std::mutex up_mu;
+  void* up_buf[2] = {nullptr, nullptr};
+  hipEvent_t up_ev[2] = {nullptr, nullptr};
+  uint64_t up_cap = 0;
 };
+void release_upload_staging();   /* kfmi_stream_release */
 int32_t ctx_for(int dev, DevCtx** out);   /* selects `dev`, creates its stream once */
 /* The calling thread's three timing events on device `dev` (current device). */
 hipEvent_t* thread_events(int dev);
@@ -143,6 +151,10 @@ int32_t search_finish(hipStream_t st, hipEvent_t* ev, double* ms);
 /* host memory helpers (kfmi_stream.hip) */
 bool host_pinned(const void* p);
 void par_copy(void* dst, const void* src, uint64_t bytes);
+/* n ASCII rows of `size` bases -> word-major 2-bit code words (row stride n;
+ * row ceil((size - rem) / 16) holds the remainder codes), over the host workers;
+ * K in {1, 2, 4} (qpack.c) */
+void par_pack(const char* src, uint64_t n, uint32_t size, uint32_t rem, uint32_t* out);
 bool par_pread(int fd, void* dst, uint64_t off, uint64_t bytes);
 
 /* device groups (kfmi_group.hip) */

@@ -685,36 +685,15 @@ void free_dev_index(kfmi_dev_index* di)
   delete di;
 }
 
-/* Large host-to-device copy.  hipMemcpy from pageable memory runs at a few
- * GB/s; above 256 MB the source is staged through two pinned 64 MB buffers
- * (filled by the host workers) so that the copy runs at PCIe speed.  Returns
- * with the copy complete when staged, else queued on `st`. */
+/* Host-to-device copy of a whole buffer, queued on `st`.  Pageable and pinned
+ * sources alike go straight to hipMemcpyAsync: on this ROCm a 1.5 GB copy
+ * from pageable memory runs at 56.5 GB/s against 57.6 from pinned memory,
+ * while staging through two pinned 64 MB buffers allocated per call (the
+ * earlier form) paid 42 ms for the allocation alone
+ * (`bin/copy_probe`, profiles/r04/copy_probe_r4m.jsonl). */
 hipError_t h2d(void* dst, const void* src, uint64_t bytes, hipStream_t st)
 {
-  constexpr uint64_t CH = 64ull << 20;
-  if (bytes < (256ull << 20) || host_pinned(src)) return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st);
-  void* buf[2] = {nullptr, nullptr};
-  hipEvent_t ev[2] = {nullptr, nullptr};
-  hipError_t e = hipSuccess;
-  for (int b = 0; b < 2 && e == hipSuccess; ++b) {
-    e = hipHostMalloc(&buf[b], CH, hipHostMallocDefault);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&ev[b], hipEventDisableTiming);
-  }
-  for (uint64_t off = 0, i = 0; off < bytes && e == hipSuccess; off += CH, ++i) {
-    const int b = (int) (i & 1);
-    if (i >= 2) e = hipEventSynchronize(ev[b]);
-    if (e != hipSuccess) break;
-    const uint64_t len = bytes - off < CH ? bytes - off : CH;
-    par_copy(buf[b], (const uint8_t*) src + off, len);
-    e = hipMemcpyAsync((uint8_t*) dst + off, buf[b], len, hipMemcpyHostToDevice, st);
-    if (e == hipSuccess) e = hipEventRecord(ev[b], st);
-  }
-  const hipError_t es = hipStreamSynchronize(st);
-  for (int b = 0; b < 2; ++b) {
-    if (ev[b]) (void) hipEventDestroy(ev[b]);
-    if (buf[b]) (void) hipHostFree(buf[b]);
-  }
-  return e != hipSuccess ? e : es;
+  return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st);
 }
 
 /* tag-100 -> tag-101 entries (kfmi_transform_interleave's plane order,
@@ -1161,6 +1140,80 @@ void query_geometry(kfmi_dev_queries* dq, uint32_t K)
   dq->nwords = (dq->steps + spw - 1) / spw;
 }
 
+/* Host-packed upload (DESIGN.md 6a "Pageable uploads"): a pageable batch has
+ * to pass through the host once anyway (staged into pinned buffers, h2d), so
+ * for K in {1, 2, 4} that pass packs it instead -- the streamed search's packer
+ * (qpack.c) over the host workers, chunk by chunk into pinned buffers while the
+ * previous chunks' DMAs run -- and a quarter of the bytes cross PCIe.  The
+ * device then holds only the code words the LF kernels read when packing is
+ * not fused.  KFMI_UPLOAD=ascii keeps the ASCII upload, =packed forces this
+ * one; by default it is taken for pageable batches of 64 MB and more. */
+static bool upload_host_packed(const kfmi_qrys_t* q, uint32_t K)
+{
+  const char* e = getenv("KFMI_UPLOAD");
+  if (e && !strcmp(e, "ascii")) return false;
+  if ((K != 1 && K != 2 && K != 4) || !q->num || !q->h_queries) return false;
+  if (e && !strcmp(e, "packed")) return true;
+  return q->num * (uint64_t) q->size >= (64ull << 20) && !host_pinned(q->h_queries);
+}
+
+/* Two pinned chunk buffers per device, kept between uploads: pinning costs
+ * ~0.3 ms per MB (copy_probe), more than packing the chunk. */
+static hipError_t h2d_packed(kfmi_dev_queries* dq, const char* src, DevCtx* ctx)
+{
+  /* reads per chunk: 100 MB of 100-bp ASCII in, 28 MB of words out (KFMI_UPLOAD_CHUNK: tests) */
+  const char* ce = getenv("KFMI_UPLOAD_CHUNK");
+  const uint64_t CQ = ce && atoll(ce) > 0 ? (uint64_t) atoll(ce) : 1ull << 20;
+  const uint64_t rows = dq->nwords + (dq->rem ? 1 : 0), cq = dq->num < CQ ? dq->num : CQ;
+  const uint64_t need = 4 * rows * cq;
+  hipStream_t st = ctx->st;
+  std::lock_guard<std::mutex> lk(ctx->up_mu);
+  hipError_t e = hipSuccess;
+  if (ctx->up_cap < need) {
+    for (int b = 0; b < 2; ++b)
+      if (ctx->up_buf[b]) {
+        (void) hipHostFree(ctx->up_buf[b]);
+        ctx->up_buf[b] = nullptr;
+      }
+    ctx->up_cap = 0;
+    for (int b = 0; b < 2 && e == hipSuccess; ++b) e = hipHostMalloc(&ctx->up_buf[b], need, hipHostMallocDefault);
+    if (e != hipSuccess) return e;
+    ctx->up_cap = need;
+  }
+  for (int b = 0; b < 2 && e == hipSuccess; ++b)
+    if (!ctx->up_ev[b]) e = hipEventCreateWithFlags(&ctx->up_ev[b], hipEventDisableTiming);
+  for (uint64_t q0 = 0, i = 0; q0 < dq->num && e == hipSuccess; q0 += cq, ++i) {
+    const int b = (int) (i & 1);
+    if (i >= 2) e = hipEventSynchronize(ctx->up_ev[b]);
+    if (e != hipSuccess) break;
+    const uint64_t n = dq->num - q0 < cq ? dq->num - q0 : cq;
+    par_pack(src + q0 * dq->size, n, dq->size, dq->rem, (uint32_t*) ctx->up_buf[b]);
+    /* chunk rows (stride n) into the batch's word-major rows (stride num) */
+    e = hipMemcpy2DAsync(dq->packed + q0, 4 * dq->num, ctx->up_buf[b], 4 * n, 4 * n, rows, hipMemcpyHostToDevice,
+                         st);
+    if (e == hipSuccess) e = hipEventRecord(ctx->up_ev[b], st);
+  }
+  const hipError_t es = hipStreamSynchronize(st);   /* the buffers are free again before the lock goes */
+  return e != hipSuccess ? e : es;
+}
+
+/* kfmi_stream_release: the upload staging of every device */
+void release_upload_staging()
+{
+  DeviceGuard dg;
+  for (int dev = 0; dev < 64; ++dev) {
+    DevCtx& c = g_ctx[dev];
+    std::lock_guard<std::mutex> lk(c.up_mu);
+    if (!c.up_cap) continue;
+    (void) hipSetDevice(dev);
+    for (int b = 0; b < 2; ++b) {
+      if (c.up_buf[b]) (void) hipHostFree(c.up_buf[b]);
+      c.up_buf[b] = nullptr;
+    }
+    c.up_cap = 0;
+  }
+}
+
 int32_t upload_queries(kfmi_qrys_t* q, uint32_t K, int dev, DevCtx* ctx)
 {
   if (q->size == 0 || K == 0) return KFMI_E_BAD_ARGUMENT;
@@ -1172,13 +1225,15 @@ int32_t upload_queries(kfmi_qrys_t* q, uint32_t K, int dev, DevCtx* ctx)
   dq->size = q->size;
   query_geometry(dq, K);
   const uint64_t abytes = q->num * (uint64_t) q->size;
-  if (hipMalloc((void**) &dq->ascii, abytes + 16) != hipSuccess ||
+  const bool hp = upload_host_packed(q, K);
+  if ((!hp && hipMalloc((void**) &dq->ascii, abytes + 16) != hipSuccess) ||
       hipMalloc((void**) &dq->packed, 4ull * (dq->nwords + 1) * (q->num ? q->num : 1)) != hipSuccess) {
     free_dev_queries(dq);
     return KFMI_E_DEVICE_ALLOC;
   }
   dq->packed_rows = dq->nwords + 1;
-  if (abytes && (h2d(dq->ascii, q->h_queries, abytes, ctx->st) != hipSuccess ||
+  if (abytes && ((hp ? h2d_packed(dq, q->h_queries, ctx) : h2d(dq->ascii, q->h_queries, abytes, ctx->st)) !=
+                     hipSuccess ||
                  hipStreamSynchronize(ctx->st) != hipSuccess)) {
     free_dev_queries(dq);
     return KFMI_E_KERNEL;
@@ -1190,7 +1245,7 @@ int32_t upload_queries(kfmi_qrys_t* q, uint32_t K, int dev, DevCtx* ctx)
 
 hipError_t launch_pack(const kfmi_dev_queries* dq, hipStream_t st)
 {
-  if (dq->num == 0) return hipSuccess;
+  if (dq->num == 0 || !dq->ascii) return hipSuccess;   /* no ASCII: packed by the host on upload */
   uint32_t tq = 256;
   while ((uint64_t) tq * dq->size > 64 * 1024 && tq > 64) tq >>= 1;
   const uint64_t blocks = (dq->num + tq - 1) / tq;
@@ -1350,7 +1405,7 @@ int32_t search_enqueue(kfmi_dev_index* di, kfmi_dev_queries* dq, uint32_t* d_res
   a.qp = dq->packed;
   a.ascii = dq->ascii;
   a.m = dq->size;
-  a.maxw = fused_maxw(di->backend, dq->K * dq->steps);
+  a.maxw = dq->ascii ? fused_maxw(di->backend, dq->K * dq->steps) : 0;
   a.num = dq->num;
   a.steps = dq->steps;
   a.nwords = dq->nwords;

@@ -278,7 +278,7 @@ bool par_pread(int fd, void* dst, uint64_t off, uint64_t bytes)
 }
 
 /* ASCII rows -> word-major code words of one chunk, over the host workers */
-static void par_pack(const char* src, uint64_t n, uint32_t size, uint32_t rem, uint32_t* out)
+void par_pack(const char* src, uint64_t n, uint32_t size, uint32_t rem, uint32_t* out)
 {
   HostPool& hp = HostPool::get();
   const int parts = n < 4096 ? 1 : hp.size();
@@ -316,6 +316,7 @@ extern "C" int32_t kfmi_stream_release(void)
       std::lock_guard<std::mutex> lk(g_pool_mu[dev][m]);
       pool_free(dev, m);
     }
+  release_upload_staging();
   return KFMI_SUCCESS;
 }
 
