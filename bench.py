@@ -765,9 +765,15 @@ def config5_leg(D, idx, text: bytes, backend: str, qlen: int, nq: int, steps: in
         h["res"] = h["r"].array().copy()
 
     def host_to_host():
-        K.transfer_to_gpu(idx, h["q"], h["r"])
-        K.search(idx, h["q"], h["r"])
-        K.transfer_to_cpu(h["r"])
+        # the library's default upload (host-packed at this size)
+        form = os.environ.pop("KFMI_UPLOAD", None)
+        try:
+            K.transfer_to_gpu(idx, h["q"], h["r"])
+            K.search(idx, h["q"], h["r"])
+            K.transfer_to_cpu(h["r"])
+        finally:
+            if form is not None:
+                os.environ["KFMI_UPLOAD"] = form
 
     S.run(setup)
     out = {"what": f"config #5 shape: {nq // 1_000_000}M x {qlen} bp reads per GPU (seed 20 + rank), "
@@ -796,7 +802,8 @@ def config5_leg(D, idx, text: bytes, backend: str, qlen: int, nq: int, steps: in
         out["host_to_host"] = {"wall_s": round(e2e, 4), "mqps": round(D.sum(float(nq)) / e2e / 1e6, 2),
                                "results_equal_per_rank": e2e_eq,
                                "what": "every rank: its reads (pageable host memory) H2D + search + results D2H "
-                                       "on the resident index, barriers around, max over ranks"}
+                                       "on the resident index through the reference's trio with the library's "
+                                       "default upload, barriers around, max over ranks"}
         # the same through kfmi_search_stream (chunks packed to 2-bit words on the
         # host, H2D / LF / D2H overlapped): one warm-up call, then one timed call
         outb = np.empty(2 * nq, dtype=np.uint32)
@@ -1034,6 +1041,12 @@ def main():
         # (kfmi_search_stream, KFMI_LINK_SHARERS)
         os.environ.setdefault("KFMI_LINK_SHARERS", str(max(dev_agg["ranks_per_device"])))
     ingest_on = a.ingest == "on" or (a.ingest == "auto" and D.world <= 2)
+    # the reads sit in HBM as ASCII, as the reference's transferCPUtoGPU leaves
+    # them, so the timed search packs them (fused into the LF kernel); the
+    # library's default for large pageable batches -- packing on the host
+    # during the upload (KFMI_UPLOAD) -- is timed in the
+    # end-to-end leg's trio instead
+    upload_form = os.environ.setdefault("KFMI_UPLOAD", "ascii")
     ph.mark("init")
 
     # ---- inputs: reference text, index replica, this rank's reads ----------
@@ -1350,6 +1363,44 @@ def main():
                               "per chunk host 2-bit packing (qpack.c, KFMI_HOST_THREADS) + code-word H2D, or " \
                               "ASCII H2D + device packing, chosen from measured rates; LF / D2H of successive " \
                               "chunks overlapped on KFMI_STREAM_SLOTS (default 6) HIP streams"
+                # the reference's own trio from pageable memory (transferCPUtoGPU,
+                # searchIndexGPU, transferGPUtoCPU on the resident index): ASCII
+                # upload, and the library default (host-packed at this size)
+                trio = {}
+                for form in ("ascii", "default"):
+                    if form == "ascii":
+                        os.environ["KFMI_UPLOAD"] = "ascii"
+                    else:
+                        os.environ.pop("KFMI_UPLOAD", None)
+                    tq = K.Queries.from_array(reads)
+                    tr = K.Results.alloc(reads.shape[0])
+                    walls, parts = [], []
+                    for i in range(a.e2e_steps + 1):
+                        t0 = time.perf_counter()
+                        K.transfer_to_gpu(idx, tq, tr)
+                        t1 = time.perf_counter()
+                        K.search(idx, tq, tr)
+                        t2 = time.perf_counter()
+                        K.transfer_to_cpu(tr)
+                        t3 = time.perf_counter()
+                        if i:                               # the first round allocates
+                            walls.append(t3 - t0)
+                            parts.append((t1 - t0, t2 - t1, t3 - t2))
+                    w = float(np.median(walls))
+                    med = np.median(np.array(parts), axis=0) * 1e3
+                    trio[form] = {"mqps": round(reads.shape[0] / w / 1e6, 2), "ms": round(w * 1e3, 3),
+                                  "transfer_to_gpu_ms": round(float(med[0]), 3), "search_ms": round(float(med[1]), 3),
+                                  "lf_ms": round(K.last_timing()["lf_ms"], 4),
+                                  "transfer_to_cpu_ms": round(float(med[2]), 3),
+                                  "results_equal": bool(np.array_equal(tr.array(), res))}
+                    tq.close()
+                    tr.close()
+                os.environ["KFMI_UPLOAD"] = upload_form
+                trio["what"] = ("the reference's transfer/search/transfer trio from pageable host memory, "
+                                "median of e2e_steps rounds: `ascii` uploads the reads as they are (packed "
+                                "inside the search), `default` is KFMI_UPLOAD unset (packed to 2-bit words on "
+                                "the host during the upload for batches of 64 MB and more, DESIGN.md 6a)")
+                e2e["trio"] = trio
                 extra["end_to_end"] = e2e
                 log(f"end to end {e2e}")
                 del pin, pout
@@ -1441,7 +1492,7 @@ def main():
             "config": {"workload": f"{'Task' if a.backend.startswith('task') else 'Coop'}-{a.k}Step backward search, "
                                    f"{a.ref_size / 1e9:g} Gbase index, {a.queries // 1_000_000}M x {a.qlen} bp reads per GPU",
                        "backend": a.backend, "k": a.k, "d": a.d, "ref_size": a.ref_size,
-                       "queries_per_gpu": a.queries, "qlen": a.qlen,
+                       "queries_per_gpu": a.queries, "qlen": a.qlen, "query_upload": upload_form,
                        "parallelism": f"query-sharded dp{D.world}, index replicated per GPU, no collective"
                                       + (f" (REHEARSAL: {D.world} ranks on {dev_agg['distinct_devices']} GPU(s))"
                                          if dev_agg["shared_devices"] else "")},
