@@ -100,6 +100,9 @@ int32_t freeQueriesGPU(void **queries);
 int32_t freeResultsGPU(void **results);
 int32_t freeIndexGPU(void **index);
 int32_t transferGPUtoCPU(void *results);
+/* The reads go up as ASCII, or -- pageable batches of 64 MB and more at K in
+ * {1, 2, 4}, unless KFMI_UPLOAD=ascii -- packed to 2-bit code words on the
+ * host during the upload (KFMI_UPLOAD=packed: any batch); same results. */
 int32_t transferCPUtoGPU(void *index, void *queries, void *results);
 
 /* common.h:87-96 / common.c */
