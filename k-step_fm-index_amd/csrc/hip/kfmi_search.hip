@@ -1147,13 +1147,20 @@ void query_geometry(kfmi_dev_queries* dq, uint32_t K)
  * previous chunks' DMAs run -- and a quarter of the bytes cross PCIe.  The
  * device then holds only the code words the LF kernels read when packing is
  * not fused.  KFMI_UPLOAD=ascii keeps the ASCII upload, =packed forces this
- * one; by default it is taken for pageable batches of 64 MB and more. */
-static bool upload_host_packed(const kfmi_qrys_t* q, uint32_t K)
+ * one; by default it is taken for pageable batches of 64 MB and more when
+ * the host workers out-pack the link: ~8 GB/s of reads per worker (qpack's
+ * AVX-512 path, 16 workers: 1 GB in 7.5 ms) against ~55 GB/s of ASCII per
+ * link (copy_probe), the link shared by KFMI_LINK_SHARERS processes and the
+ * workers by the `links` members uploading at once. */
+static bool upload_host_packed(const kfmi_qrys_t* q, uint32_t K, int links)
 {
   const char* e = getenv("KFMI_UPLOAD");
   if (e && !strcmp(e, "ascii")) return false;
   if ((K != 1 && K != 2 && K != 4) || !q->num || !q->h_queries) return false;
   if (e && !strcmp(e, "packed")) return true;
+  const char* ls = getenv("KFMI_LINK_SHARERS");
+  const int sharers = ls && atoi(ls) > 1 ? atoi(ls) : 1;
+  if (8 * kfmi_host_threads() * sharers < 55 * (links > 1 ? links : 1)) return false;
   return q->num * (uint64_t) q->size >= (64ull << 20) && !host_pinned(q->h_queries);
 }
 
@@ -1214,7 +1221,7 @@ void release_upload_staging()
   }
 }
 
-int32_t upload_queries(kfmi_qrys_t* q, uint32_t K, int dev, DevCtx* ctx)
+int32_t upload_queries(kfmi_qrys_t* q, uint32_t K, int dev, DevCtx* ctx, int links)
 {
   if (q->size == 0 || K == 0) return KFMI_E_BAD_ARGUMENT;
   if (64ull * q->size + 16 > 160ull * 1024) return KFMI_E_BAD_ARGUMENT;   /* pack tile (64 rows + 16 B) must fit LDS */
@@ -1225,7 +1232,7 @@ int32_t upload_queries(kfmi_qrys_t* q, uint32_t K, int dev, DevCtx* ctx)
   dq->size = q->size;
   query_geometry(dq, K);
   const uint64_t abytes = q->num * (uint64_t) q->size;
-  const bool hp = upload_host_packed(q, K);
+  const bool hp = upload_host_packed(q, K, links);
   if ((!hp && hipMalloc((void**) &dq->ascii, abytes + 16) != hipSuccess) ||
       hipMalloc((void**) &dq->packed, 4ull * (dq->nwords + 1) * (q->num ? q->num : 1)) != hipSuccess) {
     free_dev_queries(dq);
@@ -1532,6 +1539,19 @@ static int32_t count_on(kfmi_dev_index* di, kfmi_dev_queries* dq, uint64_t* bloc
   if (!ok) return KFMI_E_KERNEL;
   *blocks = total;
   return KFMI_SUCCESS;
+}
+
+/* How the reads of `queries` sit on the device: 0 not there, 1 ASCII, 2 code
+ * words packed by the host on upload (of the first member for a group). */
+extern "C" int32_t kfmi_queries_upload_form(void* queries)
+{
+  const kfmi_qrys_t* q = (const kfmi_qrys_t*) queries;
+  if (!q) return 0;
+  const kfmi_dev_queries* dq = q->dev;
+  const GroupSlices* g = (const GroupSlices*) q->grp;
+  if (g && g->n > 0) dq = g->dq[0];
+  if (!dq) return 0;
+  return dq->ascii ? 1 : 2;
 }
 
 /* interface.h:39, Coop-2Step.cu:287-293 */

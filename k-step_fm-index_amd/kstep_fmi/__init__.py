@@ -111,6 +111,7 @@ def load() -> ctypes.CDLL:
         "kfmi_stream_hostpacked_fraction": (ctypes.c_double, []),
         "kfmi_pack_queries": (i32, [vp, u64, u32, vp]),
         "kfmi_pack_queries_k": (i32, [vp, u64, u32, u32, vp]),
+        "kfmi_queries_upload_form": (i32, [vp]),
         "kfmi_set_devices": (i32, [ctypes.POINTER(ctypes.c_int32), i32]),
         "kfmi_get_devices": (i32, [ctypes.POINTER(ctypes.c_int32), i32]),
         "kfmi_build_index_ex": (i32, [vp, u64, u32, u32, u32, i32, pvp]),
@@ -202,6 +203,12 @@ def device_pci_bus_id(dev: int) -> str:
     buf = ctypes.create_string_buffer(64)
     _check(load().kfmi_device_pci_bus_id(int(dev), buf, 64), f"device_pci_bus_id({dev})")
     return buf.value.decode()
+
+
+def upload_form(queries) -> str:
+    """How transfer_to_gpu left the reads (kfmi_queries_upload_form):
+    "none", "ascii" or "packed" (packed to 2-bit words by the host)."""
+    return ("none", "ascii", "packed")[load().kfmi_queries_upload_form(queries.ptr)]
 
 
 def last_timing():

@@ -72,10 +72,12 @@ def test_ascii_and_packed_uploads_agree(gpu, oracle_mod, data, monkeypatch):
     R = gpu.Results.alloc(q.shape[0])
     gpu.set_backend("task-mid")
     monkeypatch.setenv("KFMI_UPLOAD_CHUNK", "1000")
+    assert gpu.upload_form(Q) == "none"
     for form in ("ascii", "packed", "ascii", "packed"):
         monkeypatch.setenv("KFMI_UPLOAD", form)
         for kd in ((1, 64), (2, 64)):
             gpu.transfer_to_gpu(idx[kd], Q, R)
+            assert gpu.upload_form(Q) == form
             gpu.search(idx[kd], Q, R)
             gpu.transfer_to_cpu(R)
             w = want if kd == (2, 64) else oracle_mod.search(idx[kd].image(), q)[0]
@@ -103,19 +105,57 @@ def test_packed_upload_k4_and_groups(gpu, oracle_mod, data, monkeypatch):
     gpu.set_devices([0, 0, 0])                                      # every member packs its own slice
     try:
         assert np.array_equal(gpu.search_array(idx[(2, 64)], q, "task-mid"), want)
+        Q = gpu.Queries.from_array(q)
+        R = gpu.Results.alloc(q.shape[0])
+        gpu.transfer_to_gpu(idx[(2, 64)], Q, R)
+        assert gpu.upload_form(Q) == "packed"
+        Q.close()
+        R.close()
     finally:
         gpu.set_devices([])
 
 
 def test_default_upload_of_a_large_pageable_batch(gpu, oracle_mod, data, monkeypatch):
-    """No KFMI_UPLOAD: a 70 MB pageable batch takes the host-packed upload;
-    results equal the forced-ASCII upload's and the oracle on a sample."""
+    """No KFMI_UPLOAD: a 70 MB pageable batch takes the host-packed upload when
+    the host workers out-pack the link (8 GB/s per worker vs 55 GB/s; the box
+    grants 16), ASCII below 64 MB; results equal the forced-ASCII upload's and
+    the oracle on a sample."""
     text, idx = data
     monkeypatch.delenv("KFMI_UPLOAD", raising=False)
     q = _reads(text, 583_333, 100, seed=11)                        # 70 MB with the random fifth
+    Q = gpu.Queries.from_array(q)
+    R = gpu.Results.alloc(q.shape[0])
+    gpu.set_backend("task-mid")
+    gpu.transfer_to_gpu(idx[(2, 64)], Q, R)
+    assert gpu.upload_form(Q) == ("packed" if gpu.host_threads() >= 7 else "ascii")
+    small = gpu.Queries.from_array(q[:100_000])
+    gpu.transfer_to_gpu(idx[(2, 64)], small, None)
+    assert gpu.upload_form(small) == "ascii"
+    small.close()
+    Q.close()
+    R.close()
     got = gpu.search_array(idx[(2, 64)], q, "task-mid")
     monkeypatch.setenv("KFMI_UPLOAD", "ascii")
     assert np.array_equal(gpu.search_array(idx[(2, 64)], q, "task-mid"), got)
     s = np.arange(0, q.shape[0], 97)
     want, _ = oracle_mod.search(idx[(2, 64)].image(), q[s])
     assert np.array_equal(got.reshape(-1, 2)[s].ravel(), want)
+
+
+def test_default_upload_with_few_host_workers(gpu):
+    """Two host workers pack ~16 GB/s, under the link's 55: the default keeps
+    the ASCII upload (a fresh process: the worker count is fixed per process)."""
+    import subprocess
+    import sys
+    import util
+    code = ("import sys; sys.path[:0] = {p!r}; import numpy as np, kstep_fmi as K; K.set_device(0); "
+            "rng = np.random.default_rng(3); t = rng.choice(np.frombuffer(b'ACGT', np.uint8), size=100_001); "
+            "I = K.Index.build(t.tobytes(), k=2, d=64); "
+            "q = K.Queries.from_array(rng.choice(np.frombuffer(b'ACGT', np.uint8), size=(700_000, 100))); "
+            "K.transfer_to_gpu(I, q, None); print(K.host_threads(), K.upload_form(q))"
+            ).format(p=[str(util.REPO), str(util.PKG)])
+    env = {k: v for k, v in __import__("os").environ.items() if k not in ("KFMI_UPLOAD", "KFMI_LINK_SHARERS")}
+    env["KFMI_HOST_THREADS"] = "2"
+    p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert p.stdout.split() == ["2", "ascii"], p.stdout
