@@ -21,6 +21,7 @@
  * Addresses come from a per-lane xorshift generator (no index array traffic).
  */
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include <stdio.h>
 #include <stdlib.h>
 #include <stdint.h>
@@ -75,6 +76,29 @@ __global__ __launch_bounds__(256) void k_coop(const uint4* __restrict__ t, uint6
     for (int j = 0; j < 4; ++j) v[j] = t[(pick(xs(s), nlines)) * TPR + k];
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc ^= v[j].x ^ v[j].w;
+  }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
+/* cooperative 128-B lines with W bytes per lane: 128 / W lanes per line, so
+ * one wave instruction touches W / 2 lines (pages) -- 8 (W = 16, k_coop<128>),
+ * 4 (W = 8) or 2 (W = 4) */
+template <int W>
+__global__ __launch_bounds__(256) void k_coopw(const uint8_t* __restrict__ t, uint64_t nlines, uint64_t per_group,
+                                               uint32_t* __restrict__ sink)
+{
+  using E = typename std::conditional<W == 16, uint4, typename std::conditional<W == 8, uint2, uint32_t>::type>::type;
+  constexpr int TPR = 128 / W;
+  const int lane = threadIdx.x & 63, k = lane % TPR;
+  uint64_t s = 0x9E3779B97F4A7C15ull ^ (((uint64_t) blockIdx.x * 256 + threadIdx.x) / TPR) * 0xBF58476D1CE4E5B9ull;
+  const E* te = reinterpret_cast<const E*>(t);
+  uint32_t acc = 0;
+  for (uint64_t i = 0; i < per_group; i += 4) {
+    E v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = te[(pick(xs(s), nlines)) * TPR + k];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc ^= reinterpret_cast<const uint32_t*>(&v[j])[0];
   }
   if (acc == 0x12345678u) sink[0] = acc;
 }
@@ -292,6 +316,21 @@ int main(int argc, char** argv)
     run("coop_sc1_nt", 128, [&] { hipLaunchKernelGGL((k_coop_pol<18>), grid, blk, 0, 0, t, bytes / 128, pg, sink); }, nl);
     run("coop_sc0_sc1_nt", 128, [&] { hipLaunchKernelGGL((k_coop_pol<19>), grid, blk, 0, 0, t, bytes / 128, pg, sink); }, nl);
     run("coop_ref", 128, [&] { hipLaunchKernelGGL((k_coop<128>), grid, blk, 0, 0, t, bytes / 128, pg, sink); }, nl);
+    if (strcmp(mode, "vmm")) CHECK(hipFree(t));
+    return 0;
+  }
+  if (getenv("PROBE_PAGES")) {
+    /* lines (pages) per wave instruction for cooperative 128-B lines */
+    const uint64_t nl = bytes / 128;
+    const uint8_t* tb = reinterpret_cast<const uint8_t*>(t);
+    for (int rep = 0; rep < 2; ++rep) {
+      const uint64_t g16 = (lines_target / (threads / 8) + 3) & ~3ull;
+      const uint64_t g8 = (lines_target / (threads / 16) + 3) & ~3ull;
+      const uint64_t g4 = (lines_target / (threads / 32) + 3) & ~3ull;
+      run("coopw16_8lines", 128, [&] { hipLaunchKernelGGL((k_coopw<16>), grid, blk, 0, 0, tb, nl, g16, sink); }, (double) g16 * (threads / 8));
+      run("coopw8_4lines", 128, [&] { hipLaunchKernelGGL((k_coopw<8>), grid, blk, 0, 0, tb, nl, g8, sink); }, (double) g8 * (threads / 16));
+      run("coopw4_2lines", 128, [&] { hipLaunchKernelGGL((k_coopw<4>), grid, blk, 0, 0, tb, nl, g4, sink); }, (double) g4 * (threads / 32));
+    }
     if (strcmp(mode, "vmm")) CHECK(hipFree(t));
     return 0;
   }
