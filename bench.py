@@ -765,15 +765,9 @@ def config5_leg(D, idx, text: bytes, backend: str, qlen: int, nq: int, steps: in
         h["res"] = h["r"].array().copy()
 
     def host_to_host():
-        # the library's default upload (host-packed at this size)
-        form = os.environ.pop("KFMI_UPLOAD", None)
-        try:
-            K.transfer_to_gpu(idx, h["q"], h["r"])
-            K.search(idx, h["q"], h["r"])
-            K.transfer_to_cpu(h["r"])
-        finally:
-            if form is not None:
-                os.environ["KFMI_UPLOAD"] = form
+        K.transfer_to_gpu(idx, h["q"], h["r"])
+        K.search(idx, h["q"], h["r"])
+        K.transfer_to_cpu(h["r"])
 
     S.run(setup)
     out = {"what": f"config #5 shape: {nq // 1_000_000}M x {qlen} bp reads per GPU (seed 20 + rank), "
@@ -802,8 +796,8 @@ def config5_leg(D, idx, text: bytes, backend: str, qlen: int, nq: int, steps: in
         out["host_to_host"] = {"wall_s": round(e2e, 4), "mqps": round(D.sum(float(nq)) / e2e / 1e6, 2),
                                "results_equal_per_rank": e2e_eq,
                                "what": "every rank: its reads (pageable host memory) H2D + search + results D2H "
-                                       "on the resident index through the reference's trio with the library's "
-                                       "default upload, barriers around, max over ranks"}
+                                       "on the resident index through the reference's trio (ASCII upload), "
+                                       "barriers around, max over ranks"}
         # the same through kfmi_search_stream (chunks packed to 2-bit words on the
         # host, H2D / LF / D2H overlapped): one warm-up call, then one timed call
         outb = np.empty(2 * nq, dtype=np.uint32)
@@ -1041,12 +1035,11 @@ def main():
         # (kfmi_search_stream, KFMI_LINK_SHARERS)
         os.environ.setdefault("KFMI_LINK_SHARERS", str(max(dev_agg["ranks_per_device"])))
     ingest_on = a.ingest == "on" or (a.ingest == "auto" and D.world <= 2)
-    # the reads sit in HBM as ASCII, as the reference's transferCPUtoGPU leaves
-    # them, so the timed search packs them (fused into the LF kernel); the
-    # library's default for large pageable batches -- packing on the host
-    # during the upload (KFMI_UPLOAD) -- is timed in the
-    # end-to-end leg's trio instead
-    upload_form = os.environ.setdefault("KFMI_UPLOAD", "ascii")
+    # the reads sit in HBM as ASCII (the library's default upload, as the
+    # reference's transferCPUtoGPU leaves them), so the timed search packs them
+    # (fused into the LF kernel); the opt-in host-packed upload
+    # (KFMI_UPLOAD=packed, DESIGN.md 6a') is timed in the end-to-end trio
+    upload_form = os.environ.get("KFMI_UPLOAD", "ascii")
     ph.mark("init")
 
     # ---- inputs: reference text, index replica, this rank's reads ----------
@@ -1364,14 +1357,11 @@ def main():
                               "ASCII H2D + device packing, chosen from measured rates; LF / D2H of successive " \
                               "chunks overlapped on KFMI_STREAM_SLOTS (default 6) HIP streams"
                 # the reference's own trio from pageable memory (transferCPUtoGPU,
-                # searchIndexGPU, transferGPUtoCPU on the resident index): ASCII
-                # upload, and the library default (host-packed at this size)
-                trio = {}
-                for form in ("ascii", "default"):
-                    if form == "ascii":
-                        os.environ["KFMI_UPLOAD"] = "ascii"
-                    else:
-                        os.environ.pop("KFMI_UPLOAD", None)
+                # searchIndexGPU, transferGPUtoCPU on the resident index): the
+                # ASCII upload (default) and the opt-in host-packed one
+                trio, prev_upload = {}, os.environ.get("KFMI_UPLOAD")
+                for form in ("ascii", "packed"):
+                    os.environ["KFMI_UPLOAD"] = form
                     tq = K.Queries.from_array(reads)
                     tr = K.Results.alloc(reads.shape[0])
                     walls, parts = [], []
@@ -1395,11 +1385,14 @@ def main():
                                   "results_equal": bool(np.array_equal(tr.array(), res))}
                     tq.close()
                     tr.close()
-                os.environ["KFMI_UPLOAD"] = upload_form
+                if prev_upload is None:
+                    os.environ.pop("KFMI_UPLOAD", None)
+                else:
+                    os.environ["KFMI_UPLOAD"] = prev_upload
                 trio["what"] = ("the reference's transfer/search/transfer trio from pageable host memory, "
-                                "median of e2e_steps rounds: `ascii` uploads the reads as they are (packed "
-                                "inside the search), `default` is KFMI_UPLOAD unset (packed to 2-bit words on "
-                                "the host during the upload for batches of 64 MB and more, DESIGN.md 6a)")
+                                "median of e2e_steps rounds: `ascii` (the default) uploads the reads as they "
+                                "are (packed inside the search), `packed` (KFMI_UPLOAD=packed) packs them to "
+                                "2-bit words on the host during the upload (DESIGN.md 6a')")
                 e2e["trio"] = trio
                 extra["end_to_end"] = e2e
                 log(f"end to end {e2e}")

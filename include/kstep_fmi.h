@@ -100,10 +100,10 @@ int32_t freeQueriesGPU(void **queries);
 int32_t freeResultsGPU(void **results);
 int32_t freeIndexGPU(void **index);
 int32_t transferGPUtoCPU(void *results);
-/* The reads go up as ASCII, or -- pageable batches of 64 MB and more at K in
- * {1, 2, 4}, unless KFMI_UPLOAD=ascii, when the host workers out-pack the
- * PCIe link -- packed to 2-bit code words on the host during the upload
- * (KFMI_UPLOAD=packed: any batch); same results. */
+/* The reads go up as ASCII (the reference's form); KFMI_UPLOAD=packed (K in
+ * {1, 2, 4}) packs them to 2-bit code words on the host during the upload
+ * instead -- a quarter of the PCIe bytes, a win where the host workers
+ * out-pack the link; same results. */
 int32_t transferCPUtoGPU(void *index, void *queries, void *results);
 /* How transferCPUtoGPU left the reads: 0 not on a device, 1 ASCII, 2 code
  * words packed by the host (a device group: its first member's slice). */

@@ -284,7 +284,7 @@ int32_t group_transfer(kfmi_fmi_t* f, kfmi_qrys_t* q, kfmi_res_t* r, const int* 
       sh.num = g->num[i];
       sh.size = q->size;
       sh.h_queries = q->h_queries + g->q0[i] * q->size;
-      if (!e) e = upload_queries(&sh, f->steps, devs[i], ctx, n);
+      if (!e) e = upload_queries(&sh, f->steps, devs[i], ctx);
       g->dq[i] = sh.dev;
       return e;
     });

@@ -137,9 +137,7 @@ hipError_t launch_pack(const kfmi_dev_queries* dq, hipStream_t st);
 /* uploads (kfmi_search.hip) */
 int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx, kfmi_dev_index** out = nullptr);
 int32_t upload_sa(const kfmi_fmi_t* f, kfmi_dev_index* di, DevCtx* ctx);
-/* links: the PCIe links the batch's members upload over at once (a device
- * group's member count), whose host workers are shared (host-packed choice) */
-int32_t upload_queries(kfmi_qrys_t* q, uint32_t K, int dev, DevCtx* ctx, int links = 1);
+int32_t upload_queries(kfmi_qrys_t* q, uint32_t K, int dev, DevCtx* ctx);
 void query_geometry(kfmi_dev_queries* dq, uint32_t K);
 void free_dev_index(kfmi_dev_index* di);
 void free_dev_queries(kfmi_dev_queries* dq);

@@ -1140,28 +1140,19 @@ void query_geometry(kfmi_dev_queries* dq, uint32_t K)
   dq->nwords = (dq->steps + spw - 1) / spw;
 }
 
-/* Host-packed upload (DESIGN.md 6a "Pageable uploads"): a pageable batch has
- * to pass through the host once anyway (staged into pinned buffers, h2d), so
- * for K in {1, 2, 4} that pass packs it instead -- the streamed search's packer
- * (qpack.c) over the host workers, chunk by chunk into pinned buffers while the
- * previous chunks' DMAs run -- and a quarter of the bytes cross PCIe.  The
- * device then holds only the code words the LF kernels read when packing is
- * not fused.  KFMI_UPLOAD=ascii keeps the ASCII upload, =packed forces this
- * one; by default it is taken for pageable batches of 64 MB and more when
- * the host workers out-pack the link: ~8 GB/s of reads per worker (qpack's
- * AVX-512 path, 16 workers: 1 GB in 7.5 ms) against ~55 GB/s of ASCII per
- * link (copy_probe), the link shared by KFMI_LINK_SHARERS processes and the
- * workers by the `links` members uploading at once. */
-static bool upload_host_packed(const kfmi_qrys_t* q, uint32_t K, int links)
+/* Host-packed upload (KFMI_UPLOAD=packed, DESIGN.md 6a'): for K in {1, 2, 4}
+ * the reads are packed to their 2-bit code words on the host workers (the
+ * streamed search's packer, qpack.c) chunk by chunk into pinned buffers while
+ * the previous chunks' DMAs run, so a quarter of the bytes cross PCIe, and the
+ * device keeps only the code words the LF kernels read when packing is not
+ * fused.  Opt-in: it wins where the host workers out-pack the link (16 workers
+ * on a fast box: 1 GB in 12.4 ms against 18.3 ms for the ASCII DMA) and loses
+ * where they do not (a slower box of the same pool: 18.8 ms; config #5's
+ * 1.5 GB 72 ms against ~45), so the default upload is the ASCII one. */
+static bool upload_host_packed(const kfmi_qrys_t* q, uint32_t K)
 {
   const char* e = getenv("KFMI_UPLOAD");
-  if (e && !strcmp(e, "ascii")) return false;
-  if ((K != 1 && K != 2 && K != 4) || !q->num || !q->h_queries) return false;
-  if (e && !strcmp(e, "packed")) return true;
-  const char* ls = getenv("KFMI_LINK_SHARERS");
-  const int sharers = ls && atoi(ls) > 1 ? atoi(ls) : 1;
-  if (8 * kfmi_host_threads() * sharers < 55 * (links > 1 ? links : 1)) return false;
-  return q->num * (uint64_t) q->size >= (64ull << 20) && !host_pinned(q->h_queries);
+  return e && !strcmp(e, "packed") && (K == 1 || K == 2 || K == 4) && q->num && q->h_queries;
 }
 
 /* Two pinned chunk buffers per device, kept between uploads: pinning costs
@@ -1221,7 +1212,7 @@ void release_upload_staging()
   }
 }
 
-int32_t upload_queries(kfmi_qrys_t* q, uint32_t K, int dev, DevCtx* ctx, int links)
+int32_t upload_queries(kfmi_qrys_t* q, uint32_t K, int dev, DevCtx* ctx)
 {
   if (q->size == 0 || K == 0) return KFMI_E_BAD_ARGUMENT;
   if (64ull * q->size + 16 > 160ull * 1024) return KFMI_E_BAD_ARGUMENT;   /* pack tile (64 rows + 16 B) must fit LDS */
@@ -1232,7 +1223,7 @@ int32_t upload_queries(kfmi_qrys_t* q, uint32_t K, int dev, DevCtx* ctx, int lin
   dq->size = q->size;
   query_geometry(dq, K);
   const uint64_t abytes = q->num * (uint64_t) q->size;
-  const bool hp = upload_host_packed(q, K, links);
+  const bool hp = upload_host_packed(q, K);
   if ((!hp && hipMalloc((void**) &dq->ascii, abytes + 16) != hipSuccess) ||
       hipMalloc((void**) &dq->packed, 4ull * (dq->nwords + 1) * (q->num ? q->num : 1)) != hipSuccess) {
     free_dev_queries(dq);
