@@ -1161,8 +1161,10 @@ static hipError_t h2d_packed(kfmi_dev_queries* dq, const char* src, DevCtx* ctx)
 {
   /* reads per chunk: 100 MB of 100-bp ASCII in, 28 MB of words out (KFMI_UPLOAD_CHUNK: tests) */
   const char* ce = getenv("KFMI_UPLOAD_CHUNK");
-  const uint64_t CQ = ce && atoll(ce) > 0 ? (uint64_t) atoll(ce) : 1ull << 20;
-  const uint64_t rows = dq->nwords + (dq->rem ? 1 : 0), cq = dq->num < CQ ? dq->num : CQ;
+  const uint64_t rows = dq->nwords + (dq->rem ? 1 : 0);
+  uint64_t CQ = ce && atoll(ce) > 0 ? (uint64_t) atoll(ce) : 1ull << 20;
+  if (!ce && 4 * rows * CQ > (64ull << 20)) CQ = (64ull << 20) / (4 * rows);   /* long reads: 64 MB buffers */
+  const uint64_t cq = dq->num < CQ ? dq->num : CQ;
   const uint64_t need = 4 * rows * cq;
   hipStream_t st = ctx->st;
   std::lock_guard<std::mutex> lk(ctx->up_mu);
