@@ -158,5 +158,6 @@ def test_gpu_entry_points_fail_without_a_device(kfmi_mod):
     with pytest.raises(kfmi_mod.KfmiError):
         kfmi_mod.search(idx, q, r)
     assert not r.array().any()
+    assert kfmi_mod.upload_form(q) == "none"          # nothing went up, in either form
     for h in (q, r, idx):
         h.close()
