@@ -63,6 +63,7 @@ struct StreamPool {
    * device's link (KFMI_LINK_SHARERS, default 1: one GPU per rank; ranks
    * rehearsing on one card set it; profiles/r04/stream_contention_r4*.jsonl). */
   double r_pack = 0, r_stage = 0, r_xa = 0, r_xp = 0;
+  double r_direct = 0;   /* KFMI_STREAM_DIRECT: host time inside the pageable copy call, per byte */
 };
 /* One pool per (device, group member): a single-device search uses member 0;
  * the members of a device group stream from pools of their own, so two
@@ -428,10 +429,11 @@ static int32_t stream_on(kfmi_dev_index* di, int member, const char* ascii, uint
     if (mode == 0 || mode == 1) host_pack = mode == 1;
     else if (mode == 3) host_pack = (i & 1) == 0;
     else if (pool.r_pack <= 0 || pool.r_xp <= 0) host_pack = true;      /* measure packing first */
-    else if (pool.r_xa <= 0 || (!pin_in && pool.r_stage <= 0)) host_pack = false;   /* then ASCII */
+    else if (pool.r_xa <= 0 || (!pin_in && (direct ? pool.r_direct : pool.r_stage) <= 0)) host_pack = false;   /* then ASCII */
     else {
       const double dn = (double) s.n;
-      const double hp_ms = pool.r_pack * abytes * dn, st_ms = pin_in ? 0.0 : pool.r_stage * abytes * dn;
+      const double hp_ms = pool.r_pack * abytes * dn;
+      const double st_ms = pin_in ? 0.0 : (direct ? pool.r_direct : pool.r_stage) * abytes * dn;
       const double xp = pool.r_xp * sharers, xa = pool.r_xa * sharers;
       const double done_p = std::max(t_host + hp_ms, t_link) + xp * pbytes * dn;
       /* direct: r_stage is the time the host spends inside the pageable copy
@@ -480,7 +482,8 @@ static int32_t stream_on(kfmi_dev_index* di, int member, const char* ascii, uint
                        (host_pack || a.maxw || launch_pack(&s.dq, s.st) == hipSuccess);
     if (!host_pack && direct) hms += since(tc);   /* the pageable copy call's own staging */
     host_ms += hms;
-    if (s.n && (host_pack || !pin_in)) ema(host_pack ? pool.r_pack : pool.r_stage, hms / (s.n * abytes));
+    if (s.n && (host_pack || !pin_in))
+      ema(host_pack ? pool.r_pack : direct ? pool.r_direct : pool.r_stage, hms / (s.n * abytes));
     if (!up_ok || dispatch(op, K, di->nb, di->layout, a) != hipSuccess ||
         hipMemcpyAsync(hdst, s.d_res, 8ull * s.n, hipMemcpyDeviceToHost, s.st) != hipSuccess ||
         hipEventRecord(s.done, s.st) != hipSuccess) {

@@ -33,6 +33,8 @@ K.transfer_to_gpu(idx, None, None)
 pin = K.pinned_empty(reads.shape, np.uint8)
 pin[:] = reads
 pout = K.pinned_empty((2 * reads.shape[0],), np.uint32)
+
+
 def set_mode(m):
     os.environ["KFMI_STREAM_HOSTPACK"] = m.rstrip("d")
     os.environ["KFMI_STREAM_DIRECT"] = "1" if m.endswith("d") else "0"
