@@ -135,32 +135,26 @@ __global__ __launch_bounds__(256) void fa_rows(const uint8_t* __restrict__ raw, 
   }
 }
 
-/* The file into device memory at dst (n bytes), through two pinned 64 MB
- * buffers: the read of one piece overlaps the DMA of the other. */
-static int32_t fa_upload(int fd, uint64_t n, uint8_t* dst, hipStream_t st)
+/* The file into device memory at dst (n bytes), through the device's two
+ * pinned 64 MB upload buffers (kept between calls: pinning them per call cost
+ * 42 ms, copy_probe): the read of one piece overlaps the DMA of the other. */
+static int32_t fa_upload(int fd, uint64_t n, uint8_t* dst, DevCtx* ctx)
 {
   constexpr uint64_t CH = 64ull << 20;
-  void* buf[2] = {nullptr, nullptr};
-  hipEvent_t ev[2] = {nullptr, nullptr};
+  const hipStream_t st = ctx->st;
+  std::lock_guard<std::mutex> lk(ctx->up_mu);
+  if (upload_staging(ctx, CH) != hipSuccess) return KFMI_E_ALLOCATING_MFASTA;
   int32_t err = KFMI_SUCCESS;
-  for (int b = 0; b < 2 && !err; ++b)
-    if (hipHostMalloc(&buf[b], CH, hipHostMallocDefault) != hipSuccess ||
-        hipEventCreateWithFlags(&ev[b], hipEventDisableTiming) != hipSuccess)
-      err = KFMI_E_ALLOCATING_MFASTA;
   for (uint64_t off = 0, i = 0; off < n && !err; off += CH, ++i) {
     const int b = (int) (i & 1);
-    if (i >= 2 && hipEventSynchronize(ev[b]) != hipSuccess) { err = KFMI_E_KERNEL; break; }
+    if (i >= 2 && hipEventSynchronize(ctx->up_ev[b]) != hipSuccess) { err = KFMI_E_KERNEL; break; }
     const uint64_t len = n - off < CH ? n - off : CH;
-    if (!par_pread(fd, buf[b], off, len)) { err = KFMI_E_READING_MFASTA_FILE; break; }
-    if (hipMemcpyAsync(dst + off, buf[b], len, hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipEventRecord(ev[b], st) != hipSuccess)
+    if (!par_pread(fd, ctx->up_buf[b], off, len)) { err = KFMI_E_READING_MFASTA_FILE; break; }
+    if (hipMemcpyAsync(dst + off, ctx->up_buf[b], len, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipEventRecord(ctx->up_ev[b], st) != hipSuccess)
       err = KFMI_E_KERNEL;
   }
-  if (hipStreamSynchronize(st) != hipSuccess && !err) err = KFMI_E_KERNEL;
-  for (int b = 0; b < 2; ++b) {
-    if (ev[b]) (void) hipEventDestroy(ev[b]);
-    if (buf[b]) (void) hipHostFree(buf[b]);
-  }
+  if (hipStreamSynchronize(st) != hipSuccess && !err) err = KFMI_E_KERNEL;   /* buffers free again */
   return err;
 }
 
@@ -197,7 +191,7 @@ extern "C" int32_t kfmi_load_queries_gpu(const char* fn, uint32_t sizequery, uin
     close(fd);
     return KFMI_E_DEVICE_ALLOC;
   }
-  err = n ? fa_upload(fd, n, raw.as<uint8_t>(), st) : KFMI_SUCCESS;
+  err = n ? fa_upload(fd, n, raw.as<uint8_t>(), ctx) : KFMI_SUCCESS;
   close(fd);
   if (err) return err;
   /* zero the tail of the last tile and the pad: no line starts there (i < n) */

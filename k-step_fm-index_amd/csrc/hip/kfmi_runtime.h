@@ -108,6 +108,8 @@ struct DevCtx {
   uint64_t up_cap = 0;
 };
 void release_upload_staging();   /* kfmi_stream_release */
+/* ctx's pinned chunk buffers grown to `need` bytes each (caller holds up_mu) */
+hipError_t upload_staging(DevCtx* ctx, uint64_t need);
 int32_t ctx_for(int dev, DevCtx** out);   /* selects `dev`, creates its stream once */
 /* The calling thread's three timing events on device `dev` (current device). */
 hipEvent_t* thread_events(int dev);

@@ -1155,19 +1155,12 @@ static bool upload_host_packed(const kfmi_qrys_t* q, uint32_t K)
   return e && !strcmp(e, "packed") && (K == 1 || K == 2 || K == 4) && q->num && q->h_queries;
 }
 
-/* Two pinned chunk buffers per device, kept between uploads: pinning costs
- * ~0.3 ms per MB (copy_probe), more than packing the chunk. */
-static hipError_t h2d_packed(kfmi_dev_queries* dq, const char* src, DevCtx* ctx)
+/* The device's two pinned chunk buffers, kept between uploads (pinning costs
+ * ~0.3 ms per MB, copy_probe: 42 ms for 2 x 64 MB), grown to `need` bytes
+ * each, and their events.  The caller holds ctx->up_mu while it uses them and
+ * leaves the copies from them complete. */
+hipError_t upload_staging(DevCtx* ctx, uint64_t need)
 {
-  /* reads per chunk: 100 MB of 100-bp ASCII in, 28 MB of words out (KFMI_UPLOAD_CHUNK: tests) */
-  const char* ce = getenv("KFMI_UPLOAD_CHUNK");
-  const uint64_t rows = dq->nwords + (dq->rem ? 1 : 0);
-  uint64_t CQ = ce && atoll(ce) > 0 ? (uint64_t) atoll(ce) : 1ull << 20;
-  if (!ce && 4 * rows * CQ > (64ull << 20)) CQ = (64ull << 20) / (4 * rows);   /* long reads: 64 MB buffers */
-  const uint64_t cq = dq->num < CQ ? dq->num : CQ;
-  const uint64_t need = 4 * rows * cq;
-  hipStream_t st = ctx->st;
-  std::lock_guard<std::mutex> lk(ctx->up_mu);
   hipError_t e = hipSuccess;
   if (ctx->up_cap < need) {
     for (int b = 0; b < 2; ++b)
@@ -1182,6 +1175,21 @@ static hipError_t h2d_packed(kfmi_dev_queries* dq, const char* src, DevCtx* ctx)
   }
   for (int b = 0; b < 2 && e == hipSuccess; ++b)
     if (!ctx->up_ev[b]) e = hipEventCreateWithFlags(&ctx->up_ev[b], hipEventDisableTiming);
+  return e;
+}
+
+static hipError_t h2d_packed(kfmi_dev_queries* dq, const char* src, DevCtx* ctx)
+{
+  /* reads per chunk: 100 MB of 100-bp ASCII in, 28 MB of words out (KFMI_UPLOAD_CHUNK: tests) */
+  const char* ce = getenv("KFMI_UPLOAD_CHUNK");
+  const uint64_t rows = dq->nwords + (dq->rem ? 1 : 0);
+  uint64_t CQ = ce && atoll(ce) > 0 ? (uint64_t) atoll(ce) : 1ull << 20;
+  if (!ce && 4 * rows * CQ > (64ull << 20)) CQ = (64ull << 20) / (4 * rows);   /* long reads: 64 MB buffers */
+  const uint64_t cq = dq->num < CQ ? dq->num : CQ;
+  const uint64_t need = 4 * rows * cq;
+  hipStream_t st = ctx->st;
+  std::lock_guard<std::mutex> lk(ctx->up_mu);
+  hipError_t e = upload_staging(ctx, need);
   for (uint64_t q0 = 0, i = 0; q0 < dq->num && e == hipSuccess; q0 += cq, ++i) {
     const int b = (int) (i & 1);
     if (i >= 2) e = hipEventSynchronize(ctx->up_ev[b]);
