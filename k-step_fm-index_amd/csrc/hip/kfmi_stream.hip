@@ -63,7 +63,6 @@ struct StreamPool {
    * device's link (KFMI_LINK_SHARERS, default 1: one GPU per rank; ranks
    * rehearsing on one card set it; profiles/r04/stream_contention_r4*.jsonl). */
   double r_pack = 0, r_stage = 0, r_xa = 0, r_xp = 0;
-  double r_direct = 0;   /* KFMI_STREAM_DIRECT: host time inside the pageable copy call, per byte */
 };
 /* One pool per (device, group member): a single-device search uses member 0;
  * the members of a device group stream from pools of their own, so two
@@ -364,12 +363,6 @@ static int32_t stream_on(kfmi_dev_index* di, int member, const char* ascii, uint
   const uint32_t steps = (size - rem) / K, spw = 32 / (2 * K), nwords = (steps + spw - 1) / spw;
   const uint32_t rows = nwords + (rem ? 1u : 0u);   /* code-word rows per read */
   const bool pin_in = host_pinned(ascii), pin_out = host_pinned(results);
-  /* KFMI_STREAM_DIRECT=1: pageable ASCII chunks go to hipMemcpyAsync as they
-   * are (the runtime's own staging; the call returns once the bytes are
-   * staged, so its time is host time) instead of through the workers' copy
-   * into a pinned slot buffer */
-  const char* dir = getenv("KFMI_STREAM_DIRECT");
-  const bool direct = !pin_in && dir && atoi(dir);
 
   std::lock_guard<std::mutex> lk(g_pool_mu[di->device][member]);
   StreamPool& pool = g_pool[di->device][member];
@@ -377,7 +370,7 @@ static int32_t stream_on(kfmi_dev_index* di, int member, const char* ascii, uint
   const int nslot = stream_slots();
   for (int k = 0; k < nslot; ++k) {
     StreamSlot& s = pool.slot[k];
-    err = slot_reserve(s, chunk, size, rows, !pin_in && !direct && any_ascii, !pin_out, any_pack);
+    err = slot_reserve(s, chunk, size, rows, !pin_in && any_ascii, !pin_out, any_pack);
     if (err) return err;
     s.busy = false;
   }
@@ -429,30 +422,28 @@ static int32_t stream_on(kfmi_dev_index* di, int member, const char* ascii, uint
     if (mode == 0 || mode == 1) host_pack = mode == 1;
     else if (mode == 3) host_pack = (i & 1) == 0;
     else if (pool.r_pack <= 0 || pool.r_xp <= 0) host_pack = true;      /* measure packing first */
-    else if (pool.r_xa <= 0 || (!pin_in && (direct ? pool.r_direct : pool.r_stage) <= 0)) host_pack = false;   /* then ASCII */
+    else if (pool.r_xa <= 0 || (!pin_in && pool.r_stage <= 0)) host_pack = false;   /* then ASCII */
     else {
       const double dn = (double) s.n;
-      const double hp_ms = pool.r_pack * abytes * dn;
-      const double st_ms = pin_in ? 0.0 : (direct ? pool.r_direct : pool.r_stage) * abytes * dn;
+      const double hp_ms = pool.r_pack * abytes * dn, st_ms = pin_in ? 0.0 : pool.r_stage * abytes * dn;
       const double xp = pool.r_xp * sharers, xa = pool.r_xa * sharers;
       const double done_p = std::max(t_host + hp_ms, t_link) + xp * pbytes * dn;
-      /* direct: r_stage is the time the host spends inside the pageable copy
-       * call, which holds the host and the link together */
-      const double done_a = direct ? std::max(t_host, t_link) + std::max(st_ms, xa * abytes * dn)
-                                   : std::max(t_host + st_ms, t_link) + xa * abytes * dn;
+      const double done_a = std::max(t_host + st_ms, t_link) + xa * abytes * dn;
       host_pack = done_p <= done_a;
-      t_host = host_pack ? t_host + hp_ms : (direct ? done_a : t_host + st_ms);
+      t_host += host_pack ? hp_ms : st_ms;
       t_link = host_pack ? done_p : done_a;
     }
     s.packed_mode = host_pack;
     npacked += host_pack ? s.n : 0;
     const auto th = clk::now();
     if (host_pack) par_pack(src, s.n, size, rem, s.h_pk);
-    else if (!pin_in && !direct) {
+    else if (!pin_in) {
       par_copy(s.h_in, src, bytes);
       hsrc = s.h_in;
     }
-    double hms = since(th);
+    const double hms = since(th);
+    host_ms += hms;
+    if (s.n && (host_pack || !pin_in)) ema(host_pack ? pool.r_pack : pool.r_stage, hms / (s.n * abytes));
     s.dq.device = di->device;
     s.dq.num = s.n;
     s.dq.size = size;
@@ -473,17 +464,12 @@ static int32_t stream_on(kfmi_dev_index* di, int member, const char* ascii, uint
     a.nwords = nwords;
     a.res = s.d_res;
     void* hdst = pin_out ? (void*) (results + 2 * s.q0) : (void*) s.h_out;
-    const auto tc = clk::now();
     const bool up_ok = hipEventRecord(s.x0, s.st) == hipSuccess &&
                        (host_pack ? hipMemcpyAsync(s.dq.packed, s.h_pk, 4ull * rows * s.n, hipMemcpyHostToDevice,
                                                    s.st) == hipSuccess
                                   : hipMemcpyAsync(s.dq.ascii, hsrc, bytes, hipMemcpyHostToDevice, s.st) == hipSuccess) &&
                        hipEventRecord(s.x1, s.st) == hipSuccess &&
                        (host_pack || a.maxw || launch_pack(&s.dq, s.st) == hipSuccess);
-    if (!host_pack && direct) hms += since(tc);   /* the pageable copy call's own staging */
-    host_ms += hms;
-    if (s.n && (host_pack || !pin_in))
-      ema(host_pack ? pool.r_pack : direct ? pool.r_direct : pool.r_stage, hms / (s.n * abytes));
     if (!up_ok || dispatch(op, K, di->nb, di->layout, a) != hipSuccess ||
         hipMemcpyAsync(hdst, s.d_res, 8ull * s.n, hipMemcpyDeviceToHost, s.st) != hipSuccess ||
         hipEventRecord(s.done, s.st) != hipSuccess) {
