@@ -1507,6 +1507,10 @@ def main():
                          # that can only be fetched whole, not a re-read
                          "traffic_GB_per_s": round(traffic / (lf_avg_ms / 1e3) / 1e9, 1) if traffic else None,
                          "traffic_over_algorithmic": round(traffic / bytes_alg, 3) if traffic else None,
+                         # BASELINE's "achieved HBM GB/s %": those bytes against the HBM peak (an
+                         # upper bound on the HBM share: Infinity-Cache hits are in the count)
+                         "traffic_frac_of_peak": round(traffic / (lf_avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
+                         if traffic else None,
                          # every LF is a random 128-B line: the binding limit is the rate of random line
                          # requests at the L2/fabric boundary, calibrated by gather_probe on the same 3 GB
                          # table size.  Requests x 128 B includes Infinity-Cache hits: an upper bound on HBM
