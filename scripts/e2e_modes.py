@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Streamed (host -> host) search: per-chunk transfer mode (KFMI_STREAM_HOSTPACK
-0 = ASCII, 1 = host-packed, 2 = adaptive)
+0 = ASCII, 1 = host-packed, 2 = adaptive; an "r" suffix sets KFMI_STREAM_RAMP=1,
+else 0 -- growing first and halving last chunks)
 x stream slots (E2E_SLOTS, E2E_MODES comma lists) x host packing ISA, pinned and
 pageable input, 3 Gbase / 10M x 100 bp (dev tool; not the bench contract).
 One JSON line per measurement on stdout."""
@@ -32,7 +33,12 @@ K.transfer_to_gpu(idx, None, None)
 pin = K.pinned_empty(reads.shape, np.uint8)
 pin[:] = reads
 pout = K.pinned_empty((2 * reads.shape[0],), np.uint32)
-for isa in ("avx2", "avx512"):
+def set_mode(m):
+    os.environ["KFMI_STREAM_HOSTPACK"] = m.rstrip("r")
+    os.environ["KFMI_STREAM_RAMP"] = "1" if m.endswith("r") else "0"
+
+
+for isa in os.environ.get("E2E_ISA", "avx2,avx512").split(","):
     os.environ["KFMI_QPACK_ISA"] = isa
     t = time.perf_counter()
     K.pack_queries(reads[:2_000_000])
@@ -45,11 +51,11 @@ for isa in ("avx2", "avx512"):
         frac = {}
         ok = {}
         for m in modes:                       # warm-up (and the adaptive model's first measurements)
-            os.environ["KFMI_STREAM_HOSTPACK"] = m
+            set_mode(m)
             K.search_stream(idx, src, out=dst)
-        for _ in range(5):                    # interleaved rounds: drift hits every mode alike
+        for _ in range(int(os.environ.get("E2E_ROUNDS", "5"))):   # interleaved rounds: drift hits every mode alike
             for m in modes:
-                os.environ["KFMI_STREAM_HOSTPACK"] = m
+                set_mode(m)
                 t = time.perf_counter()
                 out = K.search_stream(idx, src, out=dst)
                 ms[m].append((time.perf_counter() - t) * 1e3)
