@@ -408,29 +408,13 @@ static int32_t stream_on(kfmi_dev_index* di, int member, const char* ascii, uint
     }
     s.busy = false;
   };
-  /* KFMI_STREAM_RAMP (default 1): the first chunks grow (chunk/8, /4, /2) so
-   * the GPU starts after a small first pack and copy, and the last ones
-   * shrink (half of what is left, down to chunk/8) so little LF and D2H is
-   * left once the host is done; 0 = equal chunks */
-  const char* rp = getenv("KFMI_STREAM_RAMP");
-  const bool ramp = !(rp && !atoi(rp));
-  const uint64_t cmin = std::max<uint64_t>(4096, (chunk / 8) & ~63ull);
-  auto next_n = [&](uint64_t i, uint64_t left) -> uint64_t {
-    uint64_t n = chunk;
-    if (ramp && chunk > cmin) {
-      if (i < 3) n = std::max<uint64_t>(cmin, (chunk >> (3 - i)) & ~63ull);
-      if (left <= chunk + chunk / 2) n = std::max<uint64_t>(cmin, (left / 2 + 63) & ~63ull);
-    }
-    return n < left ? n : left;
-  };
-  uint64_t q0 = 0;
-  for (uint64_t i = 0; q0 < num && status == KFMI_SUCCESS; ++i) {
+  const uint64_t nchunks = (num + chunk - 1) / chunk;
+  for (uint64_t i = 0; i < nchunks && status == KFMI_SUCCESS; ++i) {
     StreamSlot& s = pool.slot[i % nslot];
     retire(s);
     if (status) break;
-    s.q0 = q0;
-    s.n = next_n(i, num - q0);
-    q0 += s.n;
+    s.q0 = i * chunk;
+    s.n = num - s.q0 < chunk ? num - s.q0 : chunk;
     const char* src = ascii + s.q0 * size;
     const uint64_t bytes = s.n * size;
     const void* hsrc = src;

@@ -49,24 +49,6 @@ def test_stream_equals_batch_and_oracle(setup, oracle_mod, backend, chunk, hostp
         assert np.array_equal(got, ores)
 
 
-@pytest.mark.parametrize("hostpack", ["1", "0", "2"])
-@pytest.mark.parametrize("ramp", ["1", "0"])
-def test_stream_chunk_ramp(setup, oracle_mod, hostpack, ramp, monkeypatch):
-    """KFMI_STREAM_RAMP (default on): growing first chunks (chunk/8, /4, /2)
-    and halving last ones, every size a multiple of 64 but the very last;
-    with 32K-read chunks over 200,003 reads both the head and the tail ramp
-    run.  Same results as equal chunks and as the oracle."""
-    K, idx, reads = setup
-    big = np.concatenate([reads] * 20)[:200_003]
-    monkeypatch.setenv("KFMI_STREAM_HOSTPACK", hostpack)
-    monkeypatch.setenv("KFMI_STREAM_RAMP", ramp)
-    got = K.search_stream(idx, big, chunk=32_768)
-    want = np.tile(K.search_array(idx, reads, "task-mid").reshape(-1, 2), (20, 1))[:200_003].ravel()
-    assert np.array_equal(got, want)
-    w10, _ = oracle_mod.search(idx.image(), reads[:2000])
-    assert np.array_equal(got[:4000], w10)
-
-
 @pytest.mark.parametrize("slots", ["2", "3", "8"])
 @pytest.mark.parametrize("hostpack", ["3", "2"])
 def test_stream_slot_counts(setup, hostpack, slots, monkeypatch):
