@@ -1,7 +1,6 @@
 #!/usr/bin/env python3
 """Streamed (host -> host) search: per-chunk transfer mode (KFMI_STREAM_HOSTPACK
-0 = ASCII, 1 = host-packed, 2 = adaptive; an "r" suffix sets KFMI_STREAM_RAMP=1,
-else 0 -- growing first and halving last chunks)
+0 = ASCII, 1 = host-packed, 2 = adaptive; E2E_ISA, E2E_ROUNDS)
 x stream slots (E2E_SLOTS, E2E_MODES comma lists) x host packing ISA, pinned and
 pageable input, 3 Gbase / 10M x 100 bp (dev tool; not the bench contract).
 One JSON line per measurement on stdout."""
@@ -34,8 +33,7 @@ pin = K.pinned_empty(reads.shape, np.uint8)
 pin[:] = reads
 pout = K.pinned_empty((2 * reads.shape[0],), np.uint32)
 def set_mode(m):
-    os.environ["KFMI_STREAM_HOSTPACK"] = m.rstrip("r")
-    os.environ["KFMI_STREAM_RAMP"] = "1" if m.endswith("r") else "0"
+    os.environ["KFMI_STREAM_HOSTPACK"] = m
 
 
 for isa in os.environ.get("E2E_ISA", "avx2,avx512").split(","):
