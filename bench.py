@@ -691,7 +691,13 @@ def variant_roofline(blocks: int, b_lf: int, lf_ms: float, a, backend: str, pmc:
         out.update({"fabric_read_requests_per_launch": req, "line_requests_per_query": round(req / a.queries, 2),
                     "line_requests_G_per_s": round(req / (lf_ms / 1e3) / 1e9, 2),
                     "l2_requests_per_launch": row.get("tcc_req_per_launch"),
-                    "pmc_kernel_ms": row.get("kernel_ms_under_pmc"), "pmc_source": pmc.get("source")})
+                    "pmc_kernel_ms": row.get("kernel_ms_under_pmc"), "pmc_source": pmc.get("source"),
+                    # every random L2 miss on gfx950 is one 128-B request, whatever the line
+                    # width the layout reads (TCC_EA0_RDREQ_128B, profiles/r04/pmc_r4k_*_sizes):
+                    # the guide's FETCH_SIZE x 2, Infinity-Cache hits included
+                    "traffic": req * 128, "traffic_GB_per_s": round(req * 128 / (lf_ms / 1e3) / 1e9, 1),
+                    "traffic_frac_of_peak": round(req * 128 / (lf_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                    "traffic_over_algorithmic": round(req * 128 / bytes_alg, 3) if bytes_alg else None})
     return out
 
 

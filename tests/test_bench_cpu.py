@@ -54,6 +54,8 @@ def test_variant_roofline_and_pmc_file(tmp_path, monkeypatch):
     assert r["bytes_per_launch"] == 578_600_000 * 36
     assert abs(r["frac"] - 578_600_000 * 36 / 10.9e-3 / 8e12) < 1e-4
     assert r["line_requests_per_query"] == 58.2 and "line_request_frac" not in r
+    assert r["traffic"] == 582_000_000 * 128                 # one 128-B request per random L2 miss
+    assert abs(r["traffic_frac_of_peak"] - 582e6 * 128 / 10.9e-3 / 8e12) < 1e-4
     assert "fabric_read_requests_per_launch" not in bench.variant_roofline(1, 36, 1.0, a, "task", got, 56.0)
     a.queries = 1_000_000                                # another config: the file does not apply
     assert bench.load_variants_pmc(a) is None
