@@ -16,7 +16,7 @@ timeout -s KILL 300 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_REQ_sum --kernel-inclu
 CSV=$(ls $OUT/pmc_r4c/*/*counter_collection.csv 2>/dev/null | head -1)
 [ -z "$CSV" ] && CSV=$(find $OUT/pmc_r4c -name "*counter_collection.csv" | head -1)
 mkdir -p $R/profiles/r04
-python3 $R/scripts/traffic_variants.py $CSV $OUT/pmc_r4c_order.json --source "profiles/r04/pmc_r4c_variants.csv (rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_REQ_sum over scripts/pmc_variants.py, scripts/gpu_r4c.sh)" > $OUT/traffic_variants_r4c.json || exit 34
+python3 $R/scripts/traffic_variants.py $CSV $OUT/pmc_r4c_order.json --source "profiles/r04/pmc_r4c_variants.csv (rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_REQ_sum over scripts/pmc_variants.py, scripts/sessions/gpu_r4c.sh)" > $OUT/traffic_variants_r4c.json || exit 34
 cp $OUT/traffic_variants_r4c.json $R/profiles/r04/traffic_variants.json
 cp $CSV $OUT/pmc_r4c_variants.csv
 CMD="python3 $R/bench.py --gpus 1 --steps 20 --warmup 5"

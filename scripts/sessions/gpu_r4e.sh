@@ -12,4 +12,4 @@ tail -2 $OUT/gpu_tests_r4e.log
 cd /tmp
 timeout -k 10 600 python3 $R/bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench_r4e.json 2> $OUT/bench_r4e.log || { tail -20 $OUT/bench_r4e.log; exit 32; }
 cut -c1-300 $OUT/bench_r4e.json
-bash $R/scripts/gpu_r4d.sh
+bash $R/scripts/sessions/gpu_r4d.sh

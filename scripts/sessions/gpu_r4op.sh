@@ -4,4 +4,4 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}
 cd $R
-bash scripts/gpu_r4p.sh && bash scripts/gpu_r4o.sh
+bash scripts/sessions/gpu_r4p.sh && bash scripts/sessions/gpu_r4o.sh

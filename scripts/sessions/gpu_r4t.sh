@@ -7,7 +7,7 @@ OUT=$R/gpurun_out
 mkdir -p $OUT
 export TMPDIR=/tmp
 cd $R
-bash scripts/gpu_r4s.sh || exit 30
+bash scripts/sessions/gpu_r4s.sh || exit 30
 timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/gpu_tests_r4t.log 2>&1 || { tail -60 $OUT/gpu_tests_r4t.log; exit 31; }
 tail -2 $OUT/gpu_tests_r4t.log
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke_r4t.log 2>&1 || { tail -30 $OUT/smoke_r4t.log; exit 32; }
