@@ -736,17 +736,17 @@ extern "C" int32_t kfmi_host_entries(kfmi_fmi_t* f)
   if (__atomic_load_n(&f->h_index, __ATOMIC_ACQUIRE)) return KFMI_SUCCESS;
   if (!f->d_entries) return KFMI_E_BAD_ARGUMENT;
   const uint64_t body = 4ull * f->entry_words * f->nentries;
-  uint8_t* img = (uint8_t*) malloc(f->header_bytes + body + 64);
+  uint8_t* img = (uint8_t*) kfmi_big_alloc(f->header_bytes + body + 64);
   if (!img) return KFMI_E_ALLOCATING_FMI;
   memcpy(img, f->image, f->header_bytes);
   memset(img + f->header_bytes + body, 0, 64);
   kfmi::DeviceGuard dg;
   if (hipSetDevice(f->d_entries_dev) != hipSuccess ||
       hipMemcpy(img + f->header_bytes, f->d_entries, body, hipMemcpyDeviceToHost) != hipSuccess) {
-    free(img);
+    kfmi_big_free(img);
     return KFMI_E_KERNEL;
   }
-  free(f->image_retired);   /* never set twice: h_index is published once */
+  kfmi_big_free(f->image_retired);   /* never set twice: h_index is published once */
   f->image_retired = f->image;
   f->image = img;
   __atomic_store_n(&f->h_index, (uint32_t*) (img + f->header_bytes), __ATOMIC_RELEASE);

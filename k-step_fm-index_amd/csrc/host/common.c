@@ -253,6 +253,63 @@ int32_t kfmi_process_cpus(void)
   return (int32_t) (cpus < 1 ? 1 : cpus);
 }
 
+/* Big-buffer registry: the mappings kfmi_big_alloc made (pointer, length), so
+ * kfmi_big_free can tell them from calloc'd buffers. */
+static pthread_mutex_t big_mu = PTHREAD_MUTEX_INITIALIZER;
+static struct { void *p; uint64_t len; } *big_tab;
+static size_t big_n, big_cap;
+
+#define KFMI_HUGE (2ull << 20)
+
+void *kfmi_big_alloc(uint64_t bytes)
+{
+  uint64_t len;
+  uint8_t *raw, *p;
+  const char *e = getenv("KFMI_HUGEPAGES");   /* 0: plain calloc (measurements) */
+  if (bytes < (64ull << 20) || (e && !atoi(e))) return calloc(1, bytes ? bytes : 1);
+  len = (bytes + KFMI_HUGE - 1) & ~(KFMI_HUGE - 1);
+  raw = (uint8_t *) mmap(NULL, len + KFMI_HUGE, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (raw == MAP_FAILED) return calloc(1, bytes);
+  p = (uint8_t *) (((uintptr_t) raw + KFMI_HUGE - 1) & ~(uintptr_t) (KFMI_HUGE - 1));
+  if (p > raw) munmap(raw, (size_t) (p - raw));
+  if (raw + len + KFMI_HUGE > p + len) munmap(p + len, (size_t) (raw + len + KFMI_HUGE - (p + len)));
+  (void) madvise(p, len, MADV_HUGEPAGE);   /* a hint: without THP the pages stay 4 KB */
+  pthread_mutex_lock(&big_mu);
+  if (big_n == big_cap) {
+    size_t nc = big_cap ? 2 * big_cap : 16;
+    void *t = realloc(big_tab, nc * sizeof(*big_tab));
+    if (!t) {
+      pthread_mutex_unlock(&big_mu);
+      munmap(p, len);
+      return calloc(1, bytes);
+    }
+    big_tab = t;
+    big_cap = nc;
+  }
+  big_tab[big_n].p = p;
+  big_tab[big_n].len = len;
+  ++big_n;
+  pthread_mutex_unlock(&big_mu);
+  return p;
+}
+
+void kfmi_big_free(void *p)
+{
+  size_t i;
+  if (!p) return;
+  pthread_mutex_lock(&big_mu);
+  for (i = 0; i < big_n; ++i)
+    if (big_tab[i].p == p) {
+      const uint64_t len = big_tab[i].len;
+      big_tab[i] = big_tab[--big_n];
+      pthread_mutex_unlock(&big_mu);
+      munmap(p, len);
+      return;
+    }
+  pthread_mutex_unlock(&big_mu);
+  free(p);
+}
+
 int32_t kfmi_host_threads(void)
 {
   const char *e = getenv("KFMI_HOST_THREADS");

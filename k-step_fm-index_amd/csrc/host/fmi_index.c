@@ -74,7 +74,7 @@ int32_t kfmi_index_alloc_ex(uint32_t tag, uint32_t steps, uint32_t bwtsize, uint
   f->entry_words = kfmi_entry_words(tag, steps, chunk);
   f->header_bytes = 24 + 8 * steps;
   f->image_bytes = f->header_bytes + 4ull * f->entry_words * nentries;
-  f->image = (uint8_t *) calloc(1, (with_entries ? f->image_bytes : f->header_bytes) + 64);
+  f->image = (uint8_t *) kfmi_big_alloc((with_entries ? f->image_bytes : f->header_bytes) + 64);
   if (!f->image) { pthread_rwlock_destroy(&f->rw); free(f); return KFMI_E_ALLOCATING_FMI; }
   h = (uint32_t *) f->image;
   h[0] = tag; h[1] = steps; h[2] = bwtsize; h[3] = ncounters; h[4] = nentries; h[5] = chunk;
@@ -149,7 +149,7 @@ static int32_t load_file(const char *fn, uint32_t required_tag, void **index)
   body = 4ull * ew * f->nentries;
   (void) hb;
   if (fread(f->h_index, 1, body, fp) != body) {
-    fclose(fp); free(f->image); free(f); return KFMI_E_READING_FMI;
+    fclose(fp); kfmi_big_free(f->image); pthread_rwlock_destroy(&f->rw); free(f); return KFMI_E_READING_FMI;
   }
   fclose(fp);
   snprintf(f->src_name, sizeof(f->src_name), "%s", fn);
@@ -227,8 +227,8 @@ int32_t freeIndex(void **index)
   if (f->dev || f->grp) freeIndexGPU(index);
   if (f->d_entries) kfmi_free_dev_entries(f);
   free(f->h_sa);
-  free(f->image);
-  free(f->image_retired);
+  kfmi_big_free(f->image);
+  kfmi_big_free(f->image_retired);
   pthread_rwlock_destroy(&f->rw);
   free(f);
   *index = NULL;
