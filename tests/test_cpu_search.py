@@ -187,3 +187,32 @@ def test_cpu_search_on_a_device_resident_index(kfmi_mod):
     want = K.search_array(idx, q, "task-mid")
     assert np.array_equal(K.search_cpu_array(idx, q, nthreads=4), want)
     idx.close()
+
+
+def test_large_image_on_2mb_pages(kfmi_mod, oracle_mod, monkeypatch, tmp_path):
+    """An index image of 64 MB or more is a 2 MB-aligned mapping advised to
+    huge pages (kfmi_big_alloc; the host search's random LFs then walk 2 MB
+    pages), KFMI_HUGEPAGES=0 a plain allocation; both search alike, survive a
+    save / load round trip and are released by freeIndex."""
+    import ctypes
+    t, text, rng = _random_case(46_000_001, 13)          # 46M bases: a 69 MB tag-100 image
+    q = t[rng.integers(0, len(text) - 100, size=3000)[:, None] + np.arange(100)]
+    res = {}
+    for hp in ("1", "0"):
+        monkeypatch.setenv("KFMI_HUGEPAGES", hp)
+        I = kfmi_mod.Index.build(text, k=2, d=64)
+        img = I.image()
+        assert img.nbytes >= 64 << 20
+        addr = img.__array_interface__["data"][0]
+        assert (addr % (2 << 20) == 0) == (hp == "1"), (hp, hex(addr))
+        res[hp] = kfmi_mod.search_cpu_array(I, q, nthreads=4)
+        I.save(tmp_path / f"i{hp}")                                   # the reference's file naming
+        J = kfmi_mod.Index.load(next(tmp_path.glob(f"i{hp}.*fmi")))  # loadIndex allocates the same way
+        assert np.array_equal(kfmi_mod.search_cpu_array(J, q, nthreads=2), res[hp])
+        J.close()
+        if hp == "1":
+            want, _ = oracle_mod.search(img, q)
+            assert np.array_equal(res[hp], want)
+        del img
+        I.close()
+    assert np.array_equal(res["1"], res["0"])
