@@ -490,11 +490,18 @@ int32_t kfmi_build_index_cpu_sa(const char *text, uint64_t n, uint32_t k, uint32
   if (n == 0 || n + 1 < k || n + 1 > 0xFFFFFFFEull) return KFMI_E_BAD_ARGUMENT;
   if (k < 1 || k > KFMI_MAX_STEPS || d == 0 || d % 32) return KFMI_E_BAD_ARGUMENT;
   if (sa_rate && !kfmi_sa_rate_ok(sa_rate)) return KFMI_E_BAD_ARGUMENT;
-  codes = (uint8_t *) malloc(n);
-  sym = (uint8_t *) malloc(n + 1);
-  sa = (uint32_t *) malloc(sizeof(uint32_t) * (n + 1));
-  if (!codes || !sym || !sa) { free(codes); free(sym); free(sa); return KFMI_E_ALLOCATING_BWT; }
-  if (text_to_codes(text, n, codes, mode, &acgt_only)) { free(codes); free(sym); free(sa); return KFMI_E_BUILDING_BWT; }
+  /* on 2 MB pages (kfmi_big_alloc): SA-IS scatters over the whole of sa */
+  codes = (uint8_t *) kfmi_big_alloc(n);
+  sym = (uint8_t *) kfmi_big_alloc(n + 1);
+  sa = (uint32_t *) kfmi_big_alloc(sizeof(uint32_t) * (n + 1));
+  if (!codes || !sym || !sa) {
+    kfmi_big_free(codes); kfmi_big_free(sym); kfmi_big_free(sa);
+    return KFMI_E_ALLOCATING_BWT;
+  }
+  if (text_to_codes(text, n, codes, mode, &acgt_only)) {
+    kfmi_big_free(codes); kfmi_big_free(sym); kfmi_big_free(sa);
+    return KFMI_E_BUILDING_BWT;
+  }
   if (mode == KFMI_ALPHA_REF && !acgt_only) {
     for (i = 0; i < n; i++) sym[i] = (uint8_t) text[i];        /* raw bytes, as divbwt64 sorts them */
     sym[n] = 0;
@@ -504,7 +511,7 @@ int32_t kfmi_build_index_cpu_sa(const char *text, uint64_t n, uint32_t k, uint32
     sym[n] = 0;
     err = kfmi_sais(sym, sa, (uint32_t) (n + 1), 5);
   }
-  free(sym);
+  kfmi_big_free(sym);
   if (!err) {
     if (mode == KFMI_ALPHA_REF && !acgt_only && k > 1)
       err = kfmi_index_ref_walk(text, sa, n, k, d, kfmi_ref_fill(), (kfmi_fmi_t **) index);
@@ -518,8 +525,8 @@ int32_t kfmi_build_index_cpu_sa(const char *text, uint64_t n, uint32_t k, uint32
     else
       for (i = 0; i < f->sa_count; i++) f->h_sa[i] = sa[i * sa_rate];
   }
-  free(codes);
-  free(sa);
+  kfmi_big_free(codes);
+  kfmi_big_free(sa);
   return err;
 }
 
