@@ -209,6 +209,28 @@ int main(int argc, char **argv)
     freeResults(&rs); freeQueries(&qs); freeIndex(&x);
   }
 
+  /* 8. big host buffers: below 64 MB calloc, from 64 MB a 2 MB-aligned mapping
+   *    (unless KFMI_HUGEPAGES=0); zeroed, writable to the last byte, freed by
+   *    kfmi_big_free either way (and NULL is a no-op) */
+  {
+    const uint64_t sizes[3] = {1000, (64ull << 20) + 12345, (80ull << 20)};
+    int t;
+    for (t = 0; t < 3; ++t) {
+      unsigned char *bp = (unsigned char *) kfmi_big_alloc(sizes[t]);
+      uint64_t j, nz = 0;
+      CHECK(bp != NULL, "big alloc %llu", (unsigned long long) sizes[t]);
+      if (!bp) continue;
+      if (sizes[t] >= (64ull << 20))
+        CHECK(((uintptr_t) bp & ((2u << 20) - 1)) == 0, "big alloc 2 MB aligned");
+      for (j = 0; j < sizes[t]; j += 4093) nz += bp[j] != 0;
+      nz += bp[sizes[t] - 1] != 0;
+      CHECK(nz == 0, "big alloc zeroed");
+      memset(bp, 0x5a, sizes[t]);
+      kfmi_big_free(bp);
+    }
+    kfmi_big_free(NULL);
+  }
+
   freeIndex(&idx); freeIndex(&t101); freeIndex(&t200); freeIndex(&t201);
   printf("%s %d checks, %d failures\n", failures ? "FAILED" : "OK", checks, failures);
   return failures ? 1 : 0;
