@@ -295,90 +295,6 @@ __global__ __launch_bounds__(256) void task_kernel(IdxArgs ix, const uint32_t* _
   }
 }
 
-/* ------------------------------------------------------------------------ */
-/* in-call batch reorder (KFMI_REORDER=1): reads sharing their */
-/* last 2t bases share [L, R) for the first t K-steps, so searching them in  */
-/* the order of their reversed 16-base suffix makes steps 4-7 (which miss a  */
-/* 4 MB L2 in random order) wave-local.  reorder_keys_kernel packs each read  */
-/* (as the fused task kernel does) into row-major code words and emits its  */
-/* sort key; rocPRIM radix-sorts (key, read); task_sorted_kernel searches in */
-/* key order and scatters (L, R) back to the read's own slot.               */
-/* ------------------------------------------------------------------------ */
-
-/* word 0 of the code stream holds bases m-1 .. m-16 at bits 0-1 .. 30-31;
- * the key puts base m-1 in the top two bits, then m-2, ... (K-independent) */
-__device__ __forceinline__ uint32_t suffix_key(uint32_t w0)
-{
-  const uint32_t r = __builtin_bitreverse32(w0);
-  return ((r >> 1) & 0x55555555u) | ((r & 0x55555555u) << 1);
-}
-
-template <int MAXW>
-__global__ __launch_bounds__(256) void reorder_keys_kernel(const uint8_t* __restrict__ ascii, uint32_t m,
-                                                           uint64_t num, uint32_t* __restrict__ keys,
-                                                           uint32_t* __restrict__ vals, uint32_t* __restrict__ pk)
-{
-  extern __shared__ __attribute__((aligned(16))) uint8_t stage[];
-  uint32_t cw[MAXW], rc;
-  stage_query_codes<MAXW>(ascii, num, m, stage, cw, 0u, rc);   /* whole block, before any exit */
-  const uint64_t q = (uint64_t) blockIdx.x * 256 + threadIdx.x;
-  if (q >= num) return;
-  keys[q] = suffix_key(cw[0]);
-  vals[q] = (uint32_t) q;
-  uint4* d = reinterpret_cast<uint4*>(pk + q * MAXW);
-#pragma unroll
-  for (int i = 0; i < MAXW / 4; ++i) d[i] = make_uint4(cw[4 * i], cw[4 * i + 1], cw[4 * i + 2], cw[4 * i + 3]);
-}
-
-template <class G, int MAXW>
-__global__ __launch_bounds__(256) void task_sorted_kernel(IdxArgs ix, const uint32_t* __restrict__ perm,
-                                                          const uint32_t* __restrict__ pk, uint64_t num,
-                                                          uint32_t steps, uint32_t nwords, uint32_t* __restrict__ res)
-{
-  constexpr int SPW = G::SPW;
-  const uint64_t i = (uint64_t) blockIdx.x * 256 + threadIdx.x;
-  if (i >= num) return;
-  const uint64_t q = perm[i];
-  uint32_t cw[MAXW];
-  const uint4* s = reinterpret_cast<const uint4*>(pk + q * MAXW);
-#pragma unroll
-  for (int k = 0; k < MAXW / 4; ++k) {
-    const uint4 v = s[k];
-    cw[4 * k] = v.x; cw[4 * k + 1] = v.y; cw[4 * k + 2] = v.z; cw[4 * k + 3] = v.w;
-  }
-  uint32_t L = 0, R = ix.bwtsize;
-  for (uint32_t w = 0; w < nwords; ++w) {
-    const uint32_t word = cw[0];
-#pragma unroll
-    for (int k = 0; k + 1 < MAXW; ++k) cw[k] = cw[k + 1];
-    const uint32_t left = steps - w * SPW;
-#pragma unroll
-    for (int j = 0; j < SPW; ++j) {
-      if ((uint32_t) j >= left) continue;
-      const uint32_t c = (word >> (2 * G::K * j)) & (uint32_t) (G::NC - 1);
-      uint32_t sx[2 * G::K];
-      plane_xor<G::K>(c, sx);
-      if constexpr (G::SMALL) {
-        Blk<G> kl, kr;
-        if constexpr (X4<G>::OK) {
-          fetch_ends_x4<G, 8>(ix, L, R, c, kl, kr);
-        } else {
-          fetch_block<G>(ix, L / (uint32_t) G::D, c, kl);
-          const uint32_t br = R / (uint32_t) G::D;
-          if (br != kl.b) fetch_block<G>(ix, br, c, kr);
-          else kr = kl;
-        }
-        L = lf_from_block<G>(ix, kl, L, c, sx);
-        R = lf_from_block<G>(ix, kr, R, c, sx);
-      } else {
-        L = lf_stream<G>(ix, L, c, sx);
-        R = lf_stream<G>(ix, R, c, sx);
-      }
-    }
-  }
-  *reinterpret_cast<uint2*>(res + 2 * q) = make_uint2(L, R);
-}
-
 /* ftab construction: [L, R) of every code stream v of ftab_steps K-steps
  * (the search's own first steps, from [0, n+1)). */
 template <class G>
@@ -482,9 +398,6 @@ struct SearchLaunch {
   uint32_t* pos;
   unsigned long long* slot_ctr;   /* walk slot queue, zeroed before the launch */
   uint32_t slot_chunk;            /* slots per queue take (64 .. 4096) */
-  /* in-call reorder: search order and row-major code words (MAXW = 8) */
-  const uint32_t* perm;
-  const uint32_t* pk;
   /* ftab build */
   uint2* ftab_out;
   uint32_t ftab_steps;
@@ -498,9 +411,7 @@ static void launch_task_split(const SearchLaunch& a)
 {
   if (a.maxw) {
     const uint64_t blocks = (a.num + 255) / 256;
-    /* KFMI_LDS_PAD (experiment): extra LDS per workgroup to cap resident waves */
-    const char* pe = getenv("KFMI_LDS_PAD");
-    const size_t lds = 4 * (size_t) stage_slot_bytes(a.m) + (pe ? (size_t) atoi(pe) : 0);
+    const size_t lds = 4 * (size_t) stage_slot_bytes(a.m);
     if (a.maxw == 8)
       hipLaunchKernelGGL((task_kernel<G, 1, 8, SPLIT>), dim3((uint32_t) blocks), dim3(256), lds, a.st, a.ix, a.qp,
                          a.ascii, a.m, a.num, a.steps, a.nwords, a.res);
@@ -601,16 +512,7 @@ static hipError_t launch_rem_tab(const SearchLaunch& a)
   return hipGetLastError();
 }
 
-template <class G>
-static hipError_t launch_task_sorted(const SearchLaunch& a)
-{
-  const uint64_t blocks = (a.num + 255) / 256;
-  hipLaunchKernelGGL((task_sorted_kernel<G, 8>), dim3((uint32_t) blocks), dim3(256), 0, a.st, a.ix, a.perm, a.pk,
-                     a.num, a.steps, a.nwords, a.res);
-  return hipGetLastError();
-}
-
-enum class Op { Task, Coop, Count, Locate, Ftab, TaskSorted, RemTab };
+enum class Op { Task, Coop, Count, Locate, Ftab, RemTab };
 
 /* Defined here, instantiated once per (K, NB, LAY) in kfmi_inst_*.hip. */
 template <int K, int NB, int LAY>
@@ -622,7 +524,6 @@ hipError_t dispatch_one(Op op, const SearchLaunch& a, unsigned long long* d_tota
     case Op::Coop: return launch_coop<G>(a);
     case Op::Locate: return launch_locate<G>(a);
     case Op::Ftab: return launch_ftab<G>(a);
-    case Op::TaskSorted: return launch_task_sorted<G>(a);
     case Op::RemTab: return launch_rem_tab<G>(a);
     default: return launch_count<G>(a, d_total);
   }

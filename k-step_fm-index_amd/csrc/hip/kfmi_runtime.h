@@ -62,11 +62,6 @@ struct kfmi_dev_queries {
   uint8_t* ascii = nullptr;    /* num*size bytes, plain layout; null when the host packed the
                                   reads on upload (`packed` is then already valid) */
   uint32_t* packed = nullptr;  /* (nwords + 1) x num u32 codes; row nwords: remainder codes */
-  /* in-call reorder (KFMI_REORDER=1): keys/reads double buffers, row-major
-   * code words, rocPRIM temporary storage; allocated on first use */
-  uint32_t* ro_buf = nullptr;
-  void* ro_tmp = nullptr;
-  size_t ro_tmp_bytes = 0;
   uint64_t num = 0;
   /* m = size = rem + K * steps: the last rem (< K) bases of a read are resolved
    * by one remainder-table lookup before its K-steps (query_geometry) */
@@ -100,8 +95,12 @@ RwLock& index_lock(const void* f);
 struct DevCtx {
   bool init = false;
   hipStream_t st = nullptr;
-  /* pinned chunk buffers of host-packed query uploads (upload_queries), kept
-   * between calls; one upload at a time per device uses them */
+  /* pinned chunk buffers of host-packed query uploads (upload_queries) and of
+   * device-parsed FASTA loads (fa_upload), kept between calls.  One user at a
+   * time per device holds up_mu for its whole pass -- a FASTA load holds it
+   * through its file reads too, so a host-packed upload on the same device
+   * waits for that load to finish (both are bulk host -> device streams that
+   * would share the one link anyway) */
   std::mutex up_mu;
   void* up_buf[2] = {nullptr, nullptr};
   hipEvent_t up_ev[2] = {nullptr, nullptr};

@@ -26,7 +26,6 @@
 #include "kfmi_coop.h"
 #include "kfmi_locate.h"
 #include "kfmi_runtime.h"
-#include <rocprim/device/device_radix_sort.hpp>
 
 namespace kfmi {
 
@@ -1012,8 +1011,25 @@ int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx, kfmi_dev_
  * KFMI_SPLIT=1|2|4 (a test knob) answers in place of the table size, so that
  * a small test index runs the fetch form a table of that size class gets
  * (launch_task: one form per geometry and class). */
+/* Knobs of earlier rounds' experiments that no longer exist, and KFMI_SPLIT
+ * values of the old fetch-form meaning (4/6/7/8 picked a form; it now names a
+ * table-size class 1/2/4): one message per process, so a rerun of an old
+ * sweep does not quietly time the default path under another label. */
+static void warn_stale_knobs_once()
+{
+  static std::once_flag once;
+  std::call_once(once, [] {
+    for (const char* k : {"KFMI_REORDER", "KFMI_LDS_PAD", "KFMI_COOP_ISSUE", "KFMI_QPT", "KFMI_NT_FROM"})
+      if (getenv(k)) fprintf(stderr, "kstepfmi: %s is no longer read (removed experiment knob); ignored\n", k);
+    const char* e = getenv("KFMI_SPLIT");
+    if (e && *e && strcmp(e, "1") && strcmp(e, "2") && strcmp(e, "4"))
+      fprintf(stderr, "kstepfmi: KFMI_SPLIT=%s: only 1, 2 or 4 (table-size class) are read; using 1\n", e);
+  });
+}
+
 static uint32_t split_for(uint64_t table_bytes, int layout)
 {
+  warn_stale_knobs_once();
   const char* e = getenv("KFMI_SPLIT");
   if (e && *e) {
     const int v = atoi(e);
@@ -1126,8 +1142,6 @@ void free_dev_queries(kfmi_dev_queries* dq)
   if (dq->device >= 0) (void) hipSetDevice(dq->device);
   if (dq->ascii) (void) hipFree(dq->ascii);
   if (dq->packed) (void) hipFree(dq->packed);
-  if (dq->ro_buf) (void) hipFree(dq->ro_buf);
-  if (dq->ro_tmp) (void) hipFree(dq->ro_tmp);
   delete dq;
 }
 
@@ -1184,7 +1198,10 @@ static hipError_t h2d_packed(kfmi_dev_queries* dq, const char* src, DevCtx* ctx)
   const char* ce = getenv("KFMI_UPLOAD_CHUNK");
   const uint64_t rows = dq->nwords + (dq->rem ? 1 : 0);
   uint64_t CQ = ce && atoll(ce) > 0 ? (uint64_t) atoll(ce) : 1ull << 20;
-  if (!ce && 4 * rows * CQ > (64ull << 20)) CQ = (64ull << 20) / (4 * rows);   /* long reads: 64 MB buffers */
+  /* long reads: 64 MB buffers; a requested chunk is held to 1 GB of words */
+  const uint64_t cap = (ce ? 1ull << 30 : 64ull << 20) / (4 * rows);
+  if (CQ > cap) CQ = cap;
+  if (CQ < 1) CQ = 1;   /* one read per chunk at least: the loop below always advances */
   const uint64_t cq = dq->num < CQ ? dq->num : CQ;
   const uint64_t need = 4 * rows * cq;
   hipStream_t st = ctx->st;
@@ -1217,6 +1234,8 @@ void release_upload_staging()
     for (int b = 0; b < 2; ++b) {
       if (c.up_buf[b]) (void) hipHostFree(c.up_buf[b]);
       c.up_buf[b] = nullptr;
+      if (c.up_ev[b]) (void) hipEventDestroy(c.up_ev[b]);
+      c.up_ev[b] = nullptr;
     }
     c.up_cap = 0;
   }
@@ -1355,51 +1374,8 @@ extern "C" int32_t transferCPUtoGPU(void* index, void* queries, void* results)
   return KFMI_SUCCESS;
 }
 
-/* KFMI_REORDER=1: search a task backend's batch in suffix order (DESIGN.md
- * 5c).  Needs fused packing with 8 code words (m <= 128), no ftab, < 2^32 reads. */
-static bool reorder_wanted(const kfmi_dev_index* di, const kfmi_dev_queries* dq, int maxw, bool ftab)
-{
-  const char* e = getenv("KFMI_REORDER");
-  return e && atoi(e) && !is_coop(di->backend) && maxw == 8 && !ftab && di->K != 3 && dq->num > 0 &&
-         dq->num < 0xFFFFFFFFull;
-}
-
-/* keys, reads (2 buffers each of num u32) and 8 code words per read */
-static int32_t reorder_queue(kfmi_dev_queries* dq, hipStream_t st, const uint32_t** perm, const uint32_t** pk)
-{
-  const uint64_t n = dq->num;
-  if (!dq->ro_buf) {
-    if (hipMalloc((void**) &dq->ro_buf, 4ull * n * (4 + 8)) != hipSuccess) {
-      dq->ro_buf = nullptr;
-      return KFMI_E_DEVICE_ALLOC;
-    }
-    size_t tb = 0;
-    uint32_t* b = dq->ro_buf;
-    if (rocprim::radix_sort_pairs(nullptr, tb, b, b + n, b + 2 * n, b + 3 * n, (size_t) n, 0, 32, st) != hipSuccess ||
-        hipMalloc(&dq->ro_tmp, tb ? tb : 1) != hipSuccess)
-      return KFMI_E_DEVICE_ALLOC;
-    dq->ro_tmp_bytes = tb;
-  }
-  uint32_t* keys = dq->ro_buf;
-  uint32_t* keys2 = keys + n;
-  uint32_t* vals = keys + 2 * n;
-  uint32_t* vals2 = keys + 3 * n;
-  uint32_t* words = keys + 4 * n;
-  const size_t lds = 4 * (size_t) stage_slot_bytes(dq->size);
-  hipLaunchKernelGGL(reorder_keys_kernel<8>, dim3((uint32_t) ((n + 255) / 256)), dim3(256), lds, st, dq->ascii,
-                     dq->size, n, keys, vals, words);
-  HIP_OK(hipGetLastError());
-  const unsigned bits = dq->size >= 16 ? 32u : 2u * dq->size;
-  size_t tb = dq->ro_tmp_bytes;
-  HIP_OK(rocprim::radix_sort_pairs(dq->ro_tmp, tb, keys, keys2, vals, vals2, (size_t) n, 0, bits, st));
-  *perm = vals2;
-  *pk = words;
-  return KFMI_SUCCESS;
-}
-
 /* Queues pack (if not fused) + LF of one device batch on `st`, bracketed by
- * ev[0..2]; search_finish waits and reads the timings.  With the reorder,
- * the key/sort launches sit between ev[0] and ev[1] (reported as pack). */
+ * ev[0..2]; search_finish waits and reads the timings. */
 int32_t search_enqueue(kfmi_dev_index* di, kfmi_dev_queries* dq, uint32_t* d_res, hipStream_t st,
                               hipEvent_t* ev, uint32_t ftab)
 {
@@ -1418,16 +1394,11 @@ int32_t search_enqueue(kfmi_dev_index* di, kfmi_dev_queries* dq, uint32_t* d_res
   a.steps = dq->steps;
   a.nwords = dq->nwords;
   a.res = d_res;
-  const bool reorder = reorder_wanted(di, dq, a.maxw, a.ix.ftab != nullptr || dq->rem);
   HIP_OK(hipEventRecord(ev[0], st));
   if (!a.maxw) HIP_OK(launch_pack(dq, st));
-  if (reorder) {
-    err = reorder_queue(dq, st, &a.perm, &a.pk);
-    if (err) return err;
-  }
   HIP_OK(hipEventRecord(ev[1], st));
   if (dq->num) {
-    const Op op = reorder ? Op::TaskSorted : (is_coop(di->backend) ? Op::Coop : Op::Task);
+    const Op op = is_coop(di->backend) ? Op::Coop : Op::Task;
     HIP_OK(dispatch(op, di->K, di->nb, di->layout, a));
   }
   HIP_OK(hipEventRecord(ev[2], st));

@@ -253,6 +253,88 @@ def test_cpu_search_on_duplicate_dollar_rows(ref_mode, oracle_mod):
             x.close()
 
 
+def dup_dollar_last_block_indexes(K):
+    """'ref'-mode indexes with (n+1) % 64 == 0 and a '$' row two D_s share in
+    the last block: the R end of the first K-step lands one block past the
+    end (B5), where every searcher of this build takes the end counters.
+    Texts replayed from a recorded seeded search (rng 77: draws 1613 and 3512,
+    n = 127 and 575; K = 4 and K = 2, 3, 4)."""
+    rng = np.random.default_rng(77)
+    alpha = np.frombuffer(b"ACGTN", np.uint8)
+    out = []
+    for it in range(3513):
+        n = 64 * int(rng.integers(2, 40)) - 1
+        t = alpha[rng.choice(5, size=n, p=rng.dirichlet(np.ones(5)))].tobytes()
+        for k in {1613: (4,), 3512: (2, 3, 4)}.get(it, ()):
+            idx = K.Index.build(t, k=k, d=64)
+            dp = idx.header()["dollar_pos"]
+            assert (n + 1) % 64 == 0 and any(dp.count(p) > 1 and p // 64 == (n + 1) // 64 - 1 for p in dp), (it, k, dp)
+            out.append((t, k, idx))
+    return out
+
+
+def _end_counters(idx):
+    """What a padding entry past the last block holds (the GPU layouts store
+    one): per code, the last entry's counter plus the code's rows in the last
+    block, less each distinct '$' row of that block with that dollarBase once.
+    Read from the tag-100 image: 24 + 8K header bytes, then entries of
+    2 * NB * K plane words (plane s*2NB + t*NB + w, row p at bit 31 - p of
+    word w) and NC counters."""
+    h = idx.header()
+    k, nb, nc, ne = h["steps"], h["chunk"] // 32, h["ncounters"], h["nentries"]
+    ew = 2 * nb * k + nc
+    ent = np.frombuffer(bytes(idx.image()[24 + 8 * k:]), np.uint32)[:ne * ew].reshape(ne, ew)
+    last = ent[-1]
+    rows = np.arange(32 * nb)
+    codes = np.zeros(rows.size, np.int64)
+    for s in range(k):
+        b0 = (last[s * 2 * nb + rows // 32] >> (31 - rows % 32).astype(np.uint32)) & 1
+        b1 = (last[s * 2 * nb + nb + rows // 32] >> (31 - rows % 32).astype(np.uint32)) & 1
+        codes |= (b0.astype(np.int64) | (b1.astype(np.int64) << 1)) << (2 * s)
+    end = last[2 * nb * k:].astype(np.int64) + np.bincount(codes, minlength=nc)
+    lastblk = ne - 1
+    for p in set(h["dollar_pos"]):
+        if p // (32 * nb) == lastblk:
+            end[codes[p % (32 * nb)]] -= 1
+    return ent[0, 2 * nb * k:].astype(np.int64), end
+
+
+def test_cpu_search_end_counters_discount_each_dollar_row_once(ref_mode):
+    """past the last block (B5) the host search uses the end
+    counters, which exclude a '$' row once however many D_s share it.  One
+    K-step of every K-mer from [0, n+1) must give [C0[c], end[c]) -- end[c]
+    as a padding entry holds it; discounting the shared row once per s left
+    R one short for its dollarBase code."""
+    import itertools
+    K = ref_mode
+    for t, k, idx in dup_dollar_last_block_indexes(K):
+        c0, end = _end_counters(idx)
+        q = np.stack([np.frombuffer(bytes(p), np.uint8) for p in itertools.product(b"ACGT", repeat=k)])
+        # itertools order = code order: first base in the high digit, last base at bits 0-1
+        for tagged in (idx, idx.interleave()):
+            iv = K.search_cpu_array(tagged, q, 1).reshape(-1, 2).astype(np.int64)
+            assert np.array_equal(iv[:, 0], c0) and np.array_equal(iv[:, 1], end), (k, idx.header()["dollar_pos"])
+        idx.close()
+
+
+@pytest.mark.gpu
+def test_gpu_end_counters_equal_cpu_search_on_duplicate_dollar_rows(ref_mode):
+    """The same last-block indexes: every plain GPU backend equals
+    searchIndexCPU (the reference reads past its file there, B5, so the
+    product's host search is the check), on all K-mers and text substrings."""
+    K = ref_mode
+    K.set_device(0)
+    rng = np.random.default_rng(8)
+    for t, k, idx in dup_dollar_last_block_indexes(K):
+        for m, q in _all_reads(t, k, rng).items():
+            want = K.search_cpu_array(idx, q, 1)
+            for be in (PLAIN if k == 2 else ("coop-grp", "task-grp")):
+                if not coop_supported(be, k, 64):
+                    continue
+                assert np.array_equal(K.search_array(idx, q, be), want), (k, m, be, idx.header()["dollar_pos"])
+        idx.close()
+
+
 @pytest.mark.gpu
 def test_gpu_search_on_duplicate_dollar_rows(ref_mode, oracle_mod):
     """Every backend on indexes with a repeated '$' row equals the reference

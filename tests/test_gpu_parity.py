@@ -263,23 +263,6 @@ def test_long_reads_fused_limit_and_pack_fallback(gpu, oracle_mod, random_index,
             gpu.search_array(idx, _reads(text, 64, 2560, seed=7), backend)
 
 
-@pytest.mark.parametrize("backend", ["task-mid", "task", "task-ac", "task-packed", "task-ac128"])
-def test_reorder_equals_oracle(gpu, oracle_mod, random_index, backend, monkeypatch):
-    """KFMI_REORDER=1 (in-call suffix-order search): same results,
-    written back to each read's own slot; reads over 128 bases (K=2) keep the
-    plain path."""
-    text, idxs = random_index
-    monkeypatch.setenv("KFMI_REORDER", "1")
-    for k, d in ((2, 64), (1, 64), (2, 192)):
-        idx = idxs[(k, d)]
-        ref_img = idx.alt_counters()[0].image() if backend in ALT else idx.image()
-        for m, n in ((100, 30000), (128, 3000), (150, 2000), (2 * k, 1000), (14, 700)):
-            q = _reads(text, n, m, seed=m + 5 * k)
-            want, _ = oracle_mod.search(ref_img, q)
-            got = gpu.search_array(idx, q, backend)
-            assert np.array_equal(got, want), (backend, k, d, m)
-
-
 @pytest.mark.parametrize("n", [63, 127, 191, 255, 1023, 4095, 100, 129, 5000, 62, 125])
 @pytest.mark.parametrize("tail", ["random", "T-run"])
 def test_ac_tail_blocks(gpu, oracle_mod, n, tail):
