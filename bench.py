@@ -36,8 +36,47 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 PROBE_CEILING_GLINES = 56.0   # gather_probe, 200 MB table (Infinity-Cache resident), profiles/r03/gather_probe_r3g.jsonl
 
 
-def log(*a):
-    print(f"[bench {time.strftime('%H:%M:%S')}]", *a, file=sys.stderr, flush=True)
+_LOG = {"file": None, "echo": True}
+
+
+def setup_logging(rank: int) -> Path | None:
+    """Every rank logs to its own file (KFMI_BENCH_LOGDIR, else TMPDIR): rank
+    0 also echoes the brief progress lines to stderr; ranks > 0 send their fds
+    1 and 2 to the file, so nothing of theirs (gloo's connect lines, library
+    messages) reaches the stream rank 0's JSON line is printed on."""
+    d = Path(os.environ.get("KFMI_BENCH_LOGDIR") or os.environ.get("TMPDIR") or "/tmp")
+    fn = d / f"kfmi_bench_rank{rank}_{os.environ.get('MASTER_PORT', '0')}_{os.getpid()}.log"
+    try:
+        d.mkdir(parents=True, exist_ok=True)
+        f = open(fn, "a", buffering=1)
+    except OSError:
+        f, fn = None, None
+    _LOG["file"] = f
+    if rank != 0:
+        _LOG["echo"] = False
+        if f is not None:
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os.dup2(f.fileno(), 1)
+            os.dup2(f.fileno(), 2)
+    return fn
+
+
+def log(*a, brief: bool = False):
+    """A line in this rank's log file; on rank 0 the `brief` ones (a dozen
+    progress lines per run) also go to stderr, cut to 160 characters
+    (KFMI_BENCH_VERBOSE=1: every line, whole)."""
+    msg = " ".join(str(x) for x in a)
+    line = f"[bench {time.strftime('%H:%M:%S')}] {msg}"
+    f = _LOG["file"]
+    if f is not None:
+        try:
+            f.write(line + "\n")
+        except (OSError, ValueError):
+            pass
+    verbose = os.environ.get("KFMI_BENCH_VERBOSE") == "1"
+    if _LOG["echo"] and (brief or verbose or f is None):
+        print(line if verbose else line[:160], file=sys.stderr, flush=True)
 
 
 def parse():
@@ -82,6 +121,9 @@ def parse():
     p.add_argument("--locate-steps", type=int, default=3)
     p.add_argument("--no-config1", dest="config1", action="store_false",
                    help="skip the 64 Mbase / 2^20-read leg (BASELINE config #1)")
+    p.add_argument("--detail", default=None,
+                   help="where the full record goes (default gpurun_out/bench_detail_n<N>.json, else TMPDIR); "
+                        "the JSON line carries its path")
     return p.parse_args()
 
 
@@ -325,7 +367,7 @@ def bench_text(D, n: int):
         mm = _node_shared(D, f"text_{n}", n, lambda f: [f.write(ch) for ch in synth.text_chunks(n)])
         if mm is not None:
             return mm
-        log(f"rank {D.rank}: no room for the node-shared text: generating it in this process")
+        log(f"rank {D.rank}: no room for the node-shared text: generating it in this process", brief=True)
     buf = bytearray(n)
     off = 0
     for ch in synth.text_chunks(n):
@@ -360,7 +402,7 @@ def _node_shared(D, name: str, nbytes: int, write):
             tmp.unlink(missing_ok=True)
     if not D.all_ok(err is None):
         if err:
-            log(f"node-shared {name}: {err}")
+            log(f"node-shared {name}: {err}", brief=True)
         return None
     with open(fn, "rb") as f:
         mm = mmap.mmap(f.fileno(), 0, access=mmap.ACCESS_READ)
@@ -546,7 +588,7 @@ def cpu_reference_baseline(idx, reads, ns, k, d, thr, res_gpu):
             p = subprocess.run([str(binp), str(ip), str(qp), str(m), str(ns)], env=env, capture_output=True,
                                text=True, timeout=900)
             if p.returncode != 0 or "TIME:" not in p.stdout:
-                log(f"reference cpu baseline failed: rc={p.returncode} {p.stdout[-300:]} {p.stderr[-300:]}")
+                log(f"reference cpu baseline failed: rc={p.returncode} {p.stdout[-300:]} {p.stderr[-300:]}", brief=True)
                 return None
             t_iter = float(p.stdout.split("TIME:")[1].split()[0])
             vals = np.array((Path(str(ip) + ".res.cpu")).read_bytes().split(), dtype=np.uint64)
@@ -651,27 +693,53 @@ def replay_requests(replay: list | None, pmc: dict | None) -> dict | None:
     return {"requests": req, "G_requests_per_s": rate, "best_G_requests_per_s": rate[best], "best_mode": best}
 
 
-VARIANTS_PMC = ROOT / "profiles" / "r04" / "traffic_variants.json"
+# the newest committed pass (this round's, else round 4's)
+VARIANTS_PMC = next((p for p in (ROOT / "profiles" / r / "traffic_variants.json" for r in ("r05", "r04"))
+                     if p.exists()), ROOT / "profiles" / "r05" / "traffic_variants.json")
+VARIANTS_PMC_Q150 = ROOT / "profiles" / "r05" / "traffic_variants_q150.json"
+
+# backend -> layout id of its kernels' Geo<K, NB, LAY> (kfmi_device.h Layout)
+LAYOUT = {"task": 0, "coop": 0, "task-ac": 1, "coop-ac": 1, "task-packed": 2, "coop-packed": 2, "task-mid": 3,
+          "coop-mid": 3, "task-ac128": 4, "coop-ac128": 4, "task-ac-mid": 5, "coop-ac-mid": 5, "task-grp": 6,
+          "coop-grp": 6}
 
 
-def load_variants_pmc(a) -> dict | None:
+def kernel_prefix(backend: str, k: int, d: int, qlen: int) -> str:
+    """The demangled-name prefix of `backend`'s LF kernel for reads of qlen
+    bases (fused packing: 8 code words up to 128 bases of K-steps, else 16;
+    kfmi_search.hip fused_maxw), as rocprofv3 prints it."""
+    name = backend.partition("+")[0]
+    maxw = 8 if k * (qlen // k) <= 128 else 16
+    geo = f"kfmi::Geo<{k}, {d // 32}, {LAYOUT[name]}>"
+    return f"kfmi::coop_kernel<{geo}, {maxw}>" if name.startswith("coop") else f"kfmi::task_kernel<{geo}, 1, {maxw},"
+
+
+def launch_spec(backend: str, k: int, d: int, qlen: int, num: int, first: int, count: int) -> dict:
+    """Where a row's timed LF launches sit in a rocprofv3 kernel trace of this
+    run: the launches of kernel `kernel` whose grid covers `num` reads, in
+    dispatch order, [first, first + count) (scripts/rows_from_trace.py)."""
+    return {"kernel": kernel_prefix(backend, k, d, qlen), "num": int(num), "first": int(first), "count": int(count)}
+
+
+def load_variants_pmc(queries: int, ref_size: int, qlen: int, d: int, path: Path | None = None) -> dict | None:
     """Per-backend fabric read requests per launch (TCC_EA0_RDREQ) of the 3 Gbase
-    / 10M x 100 bp LF kernels, from the committed PMC pass
-    (scripts/traffic_variants.py over scripts/pmc_variants.py under rocprofv3);
-    None unless it was taken on this bench's config."""
+    LF kernels, from a committed PMC pass (scripts/traffic_variants.py over
+    scripts/pmc_variants.py under rocprofv3): the 10M x 100 bp batch, or with
+    `path` = VARIANTS_PMC_Q150 config #5's 10M x 150 bp shard; None unless it
+    was taken on that config."""
     try:
-        tv = json.loads(VARIANTS_PMC.read_text())
+        tv = json.loads((path or VARIANTS_PMC).read_text())
     except (OSError, ValueError):
         return None
     cfg = tv.get("config", {})
-    if (cfg.get("queries") != a.queries or cfg.get("ref_size") != a.ref_size or cfg.get("qlen") != a.qlen
-            or cfg.get("d") != a.d):
+    if (cfg.get("queries") != queries or cfg.get("ref_size") != ref_size or cfg.get("qlen") != qlen
+            or cfg.get("d") != d):
         return None
     return tv
 
 
 def variant_roofline(blocks: int, b_lf: int, lf_ms: float, a, backend: str, pmc: dict | None,
-                     ceiling: float, k: int | None = None) -> dict:
+                     ceiling: float, k: int | None = None, queries: int | None = None) -> dict:
     """Roofline of one backend's LF launch on the bench batch: SURVEY 8(d)
     algorithmic bytes (K*d/4 + 4 B per distinct block) over its HIP-event time,
     against the HBM peak; and, when the committed PMC pass holds this backend,
@@ -688,7 +756,8 @@ def variant_roofline(blocks: int, b_lf: int, lf_ms: float, a, backend: str, pmc:
         # random 64/128-B lines, and other layouts' request mixes (64-B lines,
         # an L2-resident superblock table, 96 GB tables) sit on either side of
         # it -- coop-packed issues 58.6 G/s, coop-grp 49.9
-        out.update({"fabric_read_requests_per_launch": req, "line_requests_per_query": round(req / a.queries, 2),
+        out.update({"fabric_read_requests_per_launch": req,
+                    "line_requests_per_query": round(req / (queries or a.queries), 2),
                     "line_requests_G_per_s": round(req / (lf_ms / 1e3) / 1e9, 2),
                     "l2_requests_per_launch": row.get("tcc_req_per_launch"),
                     "pmc_kernel_ms": row.get("kernel_ms_under_pmc"), "pmc_source": pmc.get("source"),
@@ -696,7 +765,10 @@ def variant_roofline(blocks: int, b_lf: int, lf_ms: float, a, backend: str, pmc:
                     # width the layout reads (TCC_EA0_RDREQ_128B, profiles/r04/pmc_r4k_*_sizes):
                     # the guide's FETCH_SIZE x 2, Infinity-Cache hits included
                     "traffic": req * 128, "traffic_GB_per_s": round(req * 128 / (lf_ms / 1e3) / 1e9, 1),
-                    "traffic_frac_of_peak": round(req * 128 / (lf_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                    # whole-line bytes at the L2/fabric boundary (Infinity-Cache hits included)
+                    # against 8 TB/s: NOT an HBM fraction -- that is `frac` above
+                    "l2_fabric_line_bytes_vs_8TBs_incl_ic_hits": round(req * 128 / (lf_ms / 1e3) / 1e9
+                                                                       / HBM_PEAK_GBS, 4),
                     "traffic_over_algorithmic": round(req * 128 / bytes_alg, 3) if bytes_alg else None})
     return out
 
@@ -725,8 +797,15 @@ def config1_leg(backend: str, thr: int, steps: int = 5) -> dict:
     r = K.Results.alloc(reads.shape[0])
     wall, lf, tot = time_backend(idx, q, r, backend, steps, 20)
     res = r.array().copy()
+    blocks = K.count_blocks(idx, q)
+    b_lf = 2 * 64 // 4 + 4
     out = {"backend": backend, "mqps": round(reads.shape[0] / float(np.median(wall)) / 1e6, 2), "lf_ms": round(lf, 3),
-           "results_md5_pinned": synth.results_md5(res) == synth.MD5["res64"]}
+           "results_md5_pinned": synth.results_md5(res) == synth.MD5["res64"],
+           # 36 B x distinct blocks over the HIP-event LF time against 8 TB/s; the
+           # 64 MB MID128 table sits in the 256 MB Infinity Cache, so this row is
+           # not HBM-bound and may exceed the 3 Gbase rows' fraction
+           "bytes_per_launch": int(blocks * b_lf), "frac": round(blocks * b_lf / (lf / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+           "launches": launch_spec(backend, 2, 64, reads.shape[1], reads.shape[0], 20, steps)}
     ref = cpu_reference_baseline(idx, reads, reads.shape[0], 2, 64, thr, res)
     if ref:
         out["cpu_reference"] = {k: ref[k] for k in ("value", "unit", "cores", "parity_with_gpu")}
@@ -739,7 +818,7 @@ def config1_leg(backend: str, thr: int, steps: int = 5) -> dict:
 
 
 def config5_leg(D, idx, text: bytes, backend: str, qlen: int, nq: int, steps: int, warmup: int, ac: bool,
-                oracle_img=None, ingest: bool = False) -> dict:
+                oracle_img=None, ingest: bool = False, k: int = 2, d: int = 64, pmc: dict | None = None) -> dict:
     """BASELINE config #5's read shape on every rank: this rank's shard of nq
     reads of qlen bases (seed 20 + rank; 10M x 150 bp = one eighth of the
     80M x 150 bp batch at N = 8), searched on the resident index; timed like
@@ -789,6 +868,16 @@ def config5_leg(D, idx, text: bytes, backend: str, qlen: int, nq: int, steps: in
         total = D.sum(float(nq))
         out.update({"mqps": round(total * steps / el / 1e6, 2), "ms_per_step": round(el / steps * 1e3, 4),
                     "lf_ms_per_rank": D.gather(round(float(np.mean(lf)), 4) if lf else None)})
+        # this rank's roofline: SURVEY 8(d) bytes (K*d/4 + 4 per distinct block,
+        # counted on the device over the same shard) over its HIP-event LF time
+        blocks = S.run(K.count_blocks, idx, h["q"]) if lf else None
+        if blocks is not None:
+            b_lf = k * d // 4 + 4
+            lfm = float(np.mean(lf))
+            out["roofline"] = variant_roofline(blocks, b_lf, lfm, argparse.Namespace(queries=nq, k=k), backend, pmc,
+                                               PROBE_CEILING_GLINES, k=k, queries=nq)
+            out["roofline"]["lf_ms"] = round(lfm, 4)
+            out["launches"] = launch_spec(backend, k, d, qlen, nq, warmup, steps)
     # host memory to host memory on every rank (config #5's wall
     # time across the GPUs): this rank's reads H2D, search, results D2H on the
     # resident index, bracketed by barriers, max over ranks
@@ -861,7 +950,8 @@ def config5_leg(D, idx, text: bytes, backend: str, qlen: int, nq: int, steps: in
 
 
 def kstep4_leg(D, text: bytes, reads: np.ndarray, res: np.ndarray, img2, steps: int, pinned_md5: str | None,
-               c5_qlen: int, c5_queries: int, a=None, pmc: dict | None = None, ceiling: float | None = None) -> dict:
+               c5_qlen: int, c5_queries: int, a=None, pmc: dict | None = None, ceiling: float | None = None,
+               pmc150: dict | None = None) -> dict:
     """Every rank's reads on a K = 4 index (the reference's K_STEPS parameter;
     its GPU files stop at K = 2): built on the device with no host image (the
     51 GB of tag-100 entries stay in HBM), laid out as LAY_GRP -- one 128-B line
@@ -926,6 +1016,7 @@ def kstep4_leg(D, text: bytes, reads: np.ndarray, res: np.ndarray, img2, steps: 
             # K*d/4 + 4 = 68 B per distinct block at K = 4
             out["roofline"] = dict(variant_roofline(blocks, 4 * 64 // 4 + 4, lfm, a, "coop-grp", pmc,
                                                     ceiling or PROBE_CEILING_GLINES, k=4), note="rank 0's launch")
+            out["launches"] = launch_spec("coop-grp", 4, 64, reads.shape[1], reads.shape[0], 60, steps)
         if D.world == 1 and S.ok:
             i4, q, r = h["i4"], h["q"], h["r"]
             # opt-in jump start on the K = 4 index: the first 16 bases
@@ -945,7 +1036,7 @@ def kstep4_leg(D, text: bytes, reads: np.ndarray, res: np.ndarray, img2, steps: 
     if c5_queries > 0:
         if D.all_ok(S.ok):
             out["config5"] = config5_leg(D, h["i4"], text, "coop-grp", c5_qlen, c5_queries, steps, 5, False,
-                                         oracle_img=img2)
+                                         oracle_img=img2, k=4, pmc=pmc150)
     if "i4" in h:
         try:
             h["i4"].free_gpu()
@@ -1001,6 +1092,167 @@ def time_backend(idx, q, r, backend, steps, warmup):
     return walls, float(np.mean(lf)), float(np.mean(tot))
 
 
+def _compact_row(v: dict | None, extra: tuple = ()) -> dict | None:
+    """One backend's row for the line: Mq/s, HIP-event LF ms, algorithmic HBM
+    fraction, fabric line requests per read (committed PMC pass), equality
+    with the headline's md5-pinned results."""
+    if not v:
+        return None
+    if "error" in v:
+        return {"error": str(v["error"])[:120]}
+    rf = v.get("roofline") or {}
+    out = {"mqps": v.get("mqps"), "lf_ms": v.get("lf_ms", rf.get("lf_ms")), "frac": rf.get("frac", v.get("frac")),
+           "lrpq": rf.get("line_requests_per_query")}
+    if "results_equal" in v:
+        out["eq"] = v["results_equal"]
+    for k in extra:
+        if k in v:
+            out[k] = v[k]
+    return {k: x for k, x in out.items() if x is not None}
+
+
+def _all_true(xs) -> bool | None:
+    xs = list(xs or [])
+    return None if not xs or any(x is None for x in xs) else bool(all(xs))
+
+
+def _max(xs):
+    xs = [x for x in (xs or []) if x is not None]
+    return max(xs) if xs else None
+
+
+def config_rows(detail: dict, a=None) -> dict:
+    """One short row per BASELINE.json config, from the full
+    record: #1 the 64 Mbase plumbing case (GPU and the reference's CPU
+    searcher), #2-#4 the reference's Task/Coop/AltCounters kernels -- each
+    with its layout-matched MID form beside the reference layout -- #5 the
+    per-GPU 150 bp shard, and K = 4 (coop-grp) on the same reads."""
+    V = detail.get("variants") or {}
+    rf = detail.get("roofline") or {}
+    backend = (detail.get("config") or {}).get("backend")
+    head = {"mqps": detail.get("value"), "lf_ms": rf.get("lf_ms"), "frac": rf.get("frac"),
+            "lrpq": rf.get("line_requests_per_query"), "md5": (detail.get("parity") or {}).get("results_md5_pinned")}
+    head = {k: x for k, x in head.items() if x is not None}
+
+    def pick(b):
+        return head if b == backend else _compact_row(V.get(b))
+
+    rows = {}
+    c1 = V.get("config1_64mbase")
+    if c1:
+        if "error" in c1:
+            rows["1"] = {"error": str(c1["error"])[:120]}
+        else:
+            ref = c1.get("cpu_reference") or {}
+            rows["1"] = {"what": "64 Mbase, 1M x 100 bp",
+                         "gpu": {k: x for k, x in (("mqps", c1.get("mqps")), ("lf_ms", c1.get("lf_ms")),
+                                                   ("frac", c1.get("frac")), ("md5", c1.get("results_md5_pinned")))
+                                 if x is not None},
+                         "cpu_ref": {k: x for k, x in (("mqps", ref.get("value")), ("cores", ref.get("cores")),
+                                                       ("eq", ref.get("parity_with_gpu"))) if x is not None}}
+    for key, what, pair in (("2", "Task-2Step, 3 Gbase, 10M x 100 bp", ("task-mid", "task")),
+                            ("3", "Coop-2Step, same index and reads", ("coop-mid", "coop")),
+                            ("4", "Task-2Step-AltCounters, same", ("task-ac", "task-ac-mid"))):
+        r = {b: pick(b) for b in pair}
+        if any(r.values()):
+            rows[key] = dict(what=what, **{b: x for b, x in r.items() if x})
+
+    def c5_row(c5):
+        if not c5:
+            return None
+        if "mqps" not in c5:
+            return {"error": str(c5.get("error_per_rank") or "no timing")[:120]}
+        crf = c5.get("roofline") or {}
+        h2h = c5.get("host_to_host") or {}
+        out = {"mqps": c5.get("mqps"), "ms_per_step": c5.get("ms_per_step"),
+               "lf_ms_max": _max(c5.get("lf_ms_per_rank")), "frac": crf.get("frac"),
+               "lrpq": crf.get("line_requests_per_query"), "oracle_ok": _all_true(c5.get("oracle_sample_ok_per_rank")),
+               "h2h_mqps": h2h.get("mqps"), "stream_mqps": (h2h.get("streamed") or {}).get("mqps")}
+        return {k: x for k, x in out.items() if x is not None}
+
+    c5 = c5_row(V.get("config5"))
+    if c5:
+        qlen = getattr(a, "config5_qlen", 150)
+        nq = getattr(a, "config5_queries", 10_000_000)
+        rows["5"] = dict(what=f"{nq // 1_000_000}M x {qlen} bp per GPU, index replicated", **c5)
+    k4 = V.get("kstep4")
+    if k4:
+        r = _compact_row(k4) or {}
+        if "results_md5_pinned" in k4:
+            r["md5"] = k4["results_md5_pinned"]
+        if k4.get("results_equal_k2_per_rank") is not None:
+            r["eq_k2"] = _all_true(k4.get("results_equal_k2_per_rank"))
+        k4c5 = c5_row(k4.get("config5"))
+        rows["k4"] = dict(what="K=4 index, coop-grp, same reads", **r, **({"c5": k4c5} if k4c5 else {}))
+    return rows
+
+
+LINE_MAX = 6000   # bytes of the JSON line: the driver keeps an 8 KB stdout tail (VERDICT r4 #1)
+
+
+def compact_line(detail: dict, detail_path: str | None) -> dict:
+    """The one JSON line rank 0 prints: the contract's keys, a compact
+    roofline and cpu_baseline, parity, launcher, whole-job rank summary and
+    the per-config rows; everything else stays in the detail file whose path
+    the line carries.  Held to LINE_MAX bytes: past it the rows' labels go,
+    then the rows themselves (still in the detail file)."""
+    line = {k: detail.get(k) for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                                       "higher_is_better", "scaling", "vs_baseline", "dtype", "data")}
+    cfg = detail.get("config") or {}
+    line["config"] = {k: cfg[k] for k in ("workload", "backend", "k", "d", "ref_size", "queries_per_gpu", "qlen",
+                                          "query_upload", "parallelism") if k in cfg}
+    rf = detail.get("roofline") or {}
+    line["roofline"] = {k: rf.get(k) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic",
+                                                "bytes_per_launch", "traffic_over_algorithmic",
+                                                "line_requests_per_query", "line_request_frac",
+                                                "line_request_ceiling_G_per_s", "lf_ms", "kernel")}
+    line["roofline"]["frac_is"] = "achieved HBM fraction: SURVEY 8(d) algorithmic bytes / LF time / 8 TB/s"
+    cpu = detail.get("cpu_baseline")
+    if cpu:
+        line["cpu_baseline"] = {k: cpu.get(k) for k in ("value", "unit", "cores", "kind", "cpu_model",
+                                                        "cgroup_cpu_quota", "parity_with_gpu")}
+        line["cpu_baseline"]["sample"] = str(cpu.get("sample", ""))[:200]
+    else:
+        line["cpu_baseline"] = None
+    line["parity"] = detail.get("parity")
+    line["ranks_launched"] = detail.get("ranks_launched")
+    line["launcher"] = detail.get("launcher")
+    rk = detail.get("ranks") or {}
+    dv = detail.get("devices") or {}
+    line["ranks"] = {k: x for k, x in (("n", rk.get("n_ranks")), ("lf_ms_min", rk.get("lf_ms_min")),
+                                       ("lf_ms_max", rk.get("lf_ms_max")), ("step_ms_max", rk.get("step_ms_max")),
+                                       ("parity_ok_all", rk.get("parity_ok_all")),
+                                       ("distinct_gpus", dv.get("distinct_devices")),
+                                       ("shared_gpus", dv.get("shared_devices"))) if x is not None}
+    line["configs"] = detail.get("configs") or {}
+    line["detail"] = detail_path
+    if len(json.dumps(line, separators=(",", ":"))) > LINE_MAX:
+        line["configs"] = {k: {kk: vv for kk, vv in v.items() if kk != "what"} for k, v in line["configs"].items()}
+    if len(json.dumps(line, separators=(",", ":"))) > LINE_MAX:
+        line["configs"] = {"in_detail_file": True}
+    if len(json.dumps(line, separators=(",", ":"))) > LINE_MAX:
+        line["roofline"].pop("frac_is", None)
+        line["cpu_baseline"] and line["cpu_baseline"].pop("sample", None)
+    return line
+
+
+def write_detail(detail: dict, path: str | None, world: int) -> str | None:
+    """The full record (every leg, per-rank rows, probes, variants) as JSON:
+    `path`, else gpurun_out/bench_detail_n<N>.json, else TMPDIR; its path, or
+    None when nothing could be written."""
+    tmp = Path(os.environ.get("TMPDIR") or "/tmp")
+    cands = [Path(path)] if path else [ROOT / "gpurun_out" / f"bench_detail_n{world}.json",
+                                       tmp / f"kfmi_bench_detail_n{world}_{os.getpid()}.json"]
+    for p in cands:
+        try:
+            p.parent.mkdir(parents=True, exist_ok=True)
+            p.write_text(json.dumps(detail, indent=1, default=str))
+            return str(p)
+        except OSError:
+            continue
+    return None
+
+
 def main():
     a = parse()
     ws = os.environ.get("WORLD_SIZE")
@@ -1013,6 +1265,7 @@ def main():
     if ws is not None and int(ws) != a.gpus:
         raise SystemExit(f"bench.py: --gpus {a.gpus} but the launcher started WORLD_SIZE={ws} ranks; "
                          "refusing to report a run of a different size")
+    setup_logging(int(os.environ.get("RANK", "0")))
     D = Dist(a.gpus)
     ph = Phases()
     K.load()
@@ -1034,7 +1287,7 @@ def main():
     dev_agg = aggregate_devices(dev_rows)
     if dev_agg["shared_devices"] and D.rank == 0:
         log(f"WARNING: {D.world} ranks on {dev_agg['distinct_devices']} distinct GPU(s) -- a rehearsal, "
-            "not a multi-GPU measurement (n_gpus reports distinct devices, no scaling claim)")
+            "not a multi-GPU measurement (n_gpus reports distinct devices, no scaling claim)", brief=True)
     if dev_agg["shared_devices"]:
         # ranks rehearsing on one card share its PCIe link: the streamed
         # search's transfer-mode model charges its link by that many
@@ -1051,7 +1304,7 @@ def main():
     # ---- inputs: reference text, index replica, this rank's reads ----------
     t = time.perf_counter()
     text = bench_text(D, a.ref_size)
-    log(f"rank {D.rank}: text {len(text)} bases in {time.perf_counter() - t:.1f}s")
+    log(f"rank {D.rank}: text {len(text)} bases in {time.perf_counter() - t:.1f}s", brief=True)
     ph.mark("text")
     t = time.perf_counter()
     # N = 1: host image + SA samples (locate runs at N = 1 only).  N > 1: no
@@ -1075,7 +1328,7 @@ def main():
         if not D.all_ok(err is None):
             raise SystemExit(f"bench.py: rank {D.rank}: index build failed: {err}")
     build_s = time.perf_counter() - t
-    log(f"rank {D.rank}: GPU index build {build_s:.1f}s")
+    log(f"rank {D.rank}: GPU index build {build_s:.1f}s", brief=True)
     img = shared_image(D, idx)
     ph.mark("index_build")
     pinned = (a.ref_size == 3_000_000_000 and a.k == 2 and a.d == 64)
@@ -1083,7 +1336,7 @@ def main():
     if pinned and D.rank == 0 and not a.no_md5:
         h = hashlib.md5(idx.image()).hexdigest()
         index_md5_ok = h == synth.MD5["ref3g.k2d64.fmi"]
-        log(f"index md5 {h} pinned-ok={index_md5_ok}")
+        log(f"index md5 {h} pinned-ok={index_md5_ok}", brief=True)
     t = time.perf_counter()
     starts = synth.read_starts(len(text), a.queries, a.qlen, seed=10 + D.rank)
     reads = synth.gather_reads(text, starts, a.qlen)
@@ -1129,7 +1382,7 @@ def main():
     results_md5_ok = None
     if pinned and a.qlen == 100 and a.queries == 10_000_000 and D.rank == 0 and not a.no_md5:
         results_md5_ok = synth.results_md5(res) == synth.MD5["res3g.q10M"]
-        log(f"results md5 pinned-ok={results_md5_ok}")
+        log(f"timed: {value:.1f} Mq/s, LF {np.mean(lf_ms):.3f} ms; results md5 pinned-ok={results_md5_ok}", brief=True)
     # every rank: an evenly spread sample of its own results against the CPU
     # oracle (oracle/fmi_oracle.c, test infrastructure; never on the timed path),
     # with the semantics of the backend (AltCounters for the *-ac backends)
@@ -1145,7 +1398,7 @@ def main():
         parity_ok = bool(np.array_equal(want.reshape(-1, 2), res.reshape(-1, 2)[sel]))
         if ac:
             img_idx.close()
-        log(f"rank {D.rank}: oracle sample {ns_par} reads parity_ok={parity_ok} ({time.perf_counter() - t:.1f}s)")
+        log(f"rank {D.rank}: oracle sample {ns_par} reads parity_ok={parity_ok} ({time.perf_counter() - t:.1f}s)", brief=True)
     ph.mark("parity")
 
     # ---- roofline: algorithmic bytes of the LF kernel ------------------------
@@ -1193,12 +1446,17 @@ def main():
     ph.mark("count_blocks")
     # ---- auxiliary legs: each makes the same collective calls on every rank
     # whatever fails locally (Steps), so one failing rank never hangs the rest
+    # the committed PMC passes (one GPU; not applied to N > 1 runs)
+    pmc100 = load_variants_pmc(a.queries, a.ref_size, a.qlen, a.d) if D.world == 1 else None
+    pmc150 = (load_variants_pmc(a.config5_queries, a.ref_size, a.config5_qlen, a.d, VARIANTS_PMC_Q150)
+              if D.world == 1 else None)
     c5 = None
     if a.config5_queries > 0:
         c5 = config5_leg(D, idx, text, a.backend, a.config5_qlen, a.config5_queries, a.steps, 5,
                          a.backend in ("task-ac", "coop-ac", "task-ac128", "coop-ac128", "task-ac-mid",
-                                       "coop-ac-mid"), oracle_img=img, ingest=ingest_on)
+                                       "coop-ac-mid"), oracle_img=img, ingest=ingest_on, k=a.k, d=a.d, pmc=pmc150)
         log(f"rank {D.rank}: config #5 leg {c5}")
+        log(f"config #5 leg: {c5.get('mqps')} Mq/s", brief=True)
         ph.mark("config5")
     ingest = None
     if ingest_on:
@@ -1213,8 +1471,9 @@ def main():
         k4 = kstep4_leg(D, text, reads, res, img, a.steps,
                         synth.MD5["res3g.q10M"] if (pinned and a.qlen == 100 and a.queries == 10_000_000)
                         else None, a.config5_qlen, a.config5_queries, a=a,
-                        pmc=load_variants_pmc(a) if D.world == 1 else None)
+                        pmc=pmc100, pmc150=pmc150)
         log(f"rank {D.rank}: K=4 leg {k4}")
+        log(f"K=4 leg: {k4.get('mqps')} Mq/s", brief=True)
         ph.mark("kstep4")
     rank_rows = D.gather({"ingest": ingest, "rank": D.rank, "device": dev,
                           "pci_bus_id": dev_rows[D.rank]["pci_bus_id"], "queries": int(reads.shape[0]),
@@ -1284,7 +1543,7 @@ def main():
                                    "to a sampled row (kernel_ms = walk kernel, call_ms = incl. D2H of positions)"}
         log(f"locate {extra['locate']}")
         loc.close()
-    variants_pmc = load_variants_pmc(a) if D.world == 1 else None
+    variants_pmc = pmc100
     if D.rank == 0 and D.world == 1:
         # ---- other backends (same index, same reads) ------------------------
         for b in [x for x in a.variants.split(",") if x and x != a.backend]:
@@ -1305,10 +1564,13 @@ def main():
                     # its fabric read requests from the committed PMC pass
                     extra[b]["roofline"] = variant_roofline(K.count_blocks(idx, q), b_lf, lf, a, b, variants_pmc,
                                                             ceiling)
+                    extra[b]["launches"] = launch_spec(b, a.k, a.d, a.qlen, reads.shape[0], 10, a.variant_steps)
                 log(f"variant {b}: {extra[b]}")
             except K.KfmiError as e:
                 extra[b] = {"error": str(e)}
             idx.free_gpu()
+        log("variants: " + ", ".join(f"{b} {extra[b].get('mqps')}" for b in a.variants.split(",")
+                                     if b in extra and b != a.backend), brief=True)
         # ---- device-group replication (kfmi_set_devices): the layout is built
         # once and fanned out device-to-device; here one card listed n times ----
         try:
@@ -1457,6 +1719,7 @@ def main():
         extra["cpu_product"] = cpu_product_rows(idx, reads[:ns], res[:2 * ns], thrs)
         log(f"cpu product {extra['cpu_product']}")
         log(f"cpu baseline {cpu}")
+        log(f"cpu baseline: {cpu.get('value')} Mq/s on {cpu.get('cores')} threads ({cpu.get('kind')})", brief=True)
     ph.mark("rank0_n1_legs_and_cpu_baseline")
     # per-rank phase wall times and peak host RSS (the N = 8 budget: DESIGN.md 7)
     ph_rows = D.gather({"rank": D.rank, "phases_s": ph.rows, "peak_rss_gb": Phases.peak_rss_gb(),
@@ -1473,7 +1736,7 @@ def main():
               "ingest_legs": ingest_on}
 
     if D.rank == 0:
-        line = {
+        detail = {
             "metric": f"Mqueries/s ({a.qlen} bp reads, {a.ref_size / 1e9:g} Gbase index)",
             "value": round(value, 3),
             "unit": "Mqueries/s",
@@ -1500,7 +1763,9 @@ def main():
             "devices": dict(dev_agg, per_rank=dev_rows),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "LF kernel (task/coop search), HIP-event average over the timed steps",
+                         "kernel": kernel_prefix(a.backend, a.k, a.d, a.qlen).split("<", 1)[0].replace("kfmi::", "")
+                                   + f" {a.backend}, HIP-event average over the timed steps",
+                         "launches": launch_spec(a.backend, a.k, a.d, a.qlen, reads.shape[0], a.warmup, a.steps),
                          "bytes_per_launch": bytes_alg, "distinct_blocks": blocks, "bytes_per_block": b_lf,
                          "bytes_per_query_io": q_in + 8,
                          "achieved_incl_query_io": round((bytes_alg + bytes_io) / (lf_avg_ms / 1e3) / 1e9, 1),
@@ -1513,10 +1778,11 @@ def main():
                          # that can only be fetched whole, not a re-read
                          "traffic_GB_per_s": round(traffic / (lf_avg_ms / 1e3) / 1e9, 1) if traffic else None,
                          "traffic_over_algorithmic": round(traffic / bytes_alg, 3) if traffic else None,
-                         # BASELINE's "achieved HBM GB/s %": those bytes against the HBM peak (an
-                         # upper bound on the HBM share: Infinity-Cache hits are in the count)
-                         "traffic_frac_of_peak": round(traffic / (lf_avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
-                         if traffic else None,
+                         # those bytes against 8 TB/s: NOT the HBM fraction (Infinity-Cache hits
+                         # are in the count; it can exceed the 6.29 TB/s achievable HBM rate).
+                         # BASELINE's "achieved HBM GB/s %" is `frac`
+                         "l2_fabric_line_bytes_vs_8TBs_incl_ic_hits":
+                             round(traffic / (lf_avg_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
                          # every LF is a random 128-B line: the binding limit is the rate of random line
                          # requests at the L2/fabric boundary, calibrated by gather_probe on the same 3 GB
                          # table size.  Requests x 128 B includes Infinity-Cache hits: an upper bound on HBM
@@ -1563,7 +1829,13 @@ def main():
             "phases": phases,
             "variants": extra,
         }
-        print(json.dumps(line), flush=True)
+        detail["configs"] = config_rows(detail, a)
+        dpath = write_detail(detail, a.detail, D.world)
+        line = compact_line(detail, dpath)
+        log(f"detail: {dpath}; line {len(json.dumps(line))} B", brief=True)
+        # the line is the last thing on stdout, after everything on stderr
+        sys.stderr.flush()
+        print(json.dumps(line, separators=(",", ":")), flush=True)
     D.barrier()          # every rank leaves together (rank 0 ran the CPU baseline)
     D.close()
 

@@ -7,7 +7,8 @@ profiles/r04/traffic_variants.json).
       -d out -o p --output-format csv -- python3 scripts/pmc_variants.py --order out/order.json
 
 The 3 Gbase recipe text, its K = 2 d = 64 index built on the device, the
-bench's rank-0 reads (10M x 100 bp, seed 10); each backend: upload, `warmup`
+bench's rank-0 reads (10M x 100 bp, seed 10; --qlen 150 --seed 20: config
+#5's shard); each backend: upload, `warmup`
 untimed searches, `steps` searches (one LF launch each); then the same reads on
 the K = 4 index (coop-grp, task-grp).  The order file lists (backend, K,
 launches) in dispatch order, which is how the PMC rows are attributed.
@@ -44,12 +45,14 @@ def main():
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--ref-size", type=int, default=3_000_000_000)
     p.add_argument("--queries", type=int, default=10_000_000)
+    p.add_argument("--qlen", type=int, default=100, help="150: config #5's shard shape")
+    p.add_argument("--seed", type=int, default=10, help="read seed (bench: 10 + rank main leg, 20 + rank config #5)")
     a = p.parse_args()
     K.load()
     K.set_device(0)
     text = synth.text_3g(a.ref_size) if a.ref_size == 3_000_000_000 else \
         b"".join(synth.text_chunks(a.ref_size))
-    reads = synth.gather_reads(text, synth.read_starts(len(text), a.queries, 100, seed=10), 100)
+    reads = synth.gather_reads(text, synth.read_starts(len(text), a.queries, a.qlen, seed=a.seed), a.qlen)
     q = K.Queries.from_array(reads)
     r = K.Results.alloc(a.queries)
     order, first = [], None
@@ -75,7 +78,7 @@ def main():
             log(order[-1])
             idx.free_gpu()
         idx.close()
-    Path(a.order).write_text(json.dumps({"queries": a.queries, "ref_size": a.ref_size, "qlen": 100, "d": 64,
+    Path(a.order).write_text(json.dumps({"queries": a.queries, "ref_size": a.ref_size, "qlen": a.qlen, "d": 64,
                                          "order": order}, indent=1))
 
 

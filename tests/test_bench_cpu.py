@@ -48,17 +48,21 @@ def test_variant_roofline_and_pmc_file(tmp_path, monkeypatch):
     fn = tmp_path / "tv.json"
     fn.write_text(json.dumps(pmc))
     monkeypatch.setattr(bench, "VARIANTS_PMC", fn)
-    got = bench.load_variants_pmc(a)
+    got = bench.load_variants_pmc(a.queries, a.ref_size, a.qlen, a.d)
     assert got == pmc
     r = bench.variant_roofline(578_600_000, 36, 10.9, a, "coop", got, 56.0)
     assert r["bytes_per_launch"] == 578_600_000 * 36
     assert abs(r["frac"] - 578_600_000 * 36 / 10.9e-3 / 8e12) < 1e-4
     assert r["line_requests_per_query"] == 58.2 and "line_request_frac" not in r
     assert r["traffic"] == 582_000_000 * 128                 # one 128-B request per random L2 miss
-    assert abs(r["traffic_frac_of_peak"] - 582e6 * 128 / 10.9e-3 / 8e12) < 1e-4
+    # fabric line bytes are labelled as such, never as an HBM fraction
+    assert abs(r["l2_fabric_line_bytes_vs_8TBs_incl_ic_hits"] - 582e6 * 128 / 10.9e-3 / 8e12) < 1e-4
+    assert not any("hbm" in k.lower() for k in r)
     assert "fabric_read_requests_per_launch" not in bench.variant_roofline(1, 36, 1.0, a, "task", got, 56.0)
     a.queries = 1_000_000                                # another config: the file does not apply
-    assert bench.load_variants_pmc(a) is None
+    assert bench.load_variants_pmc(a.queries, a.ref_size, a.qlen, a.d) is None
+    # config #5's pass (150 bp) is its own file, keyed by its own shape
+    assert bench.load_variants_pmc(10_000_000, 3_000_000_000, 150, 64, fn) is None
 
 
 def test_traffic_variants_parser(tmp_path):
