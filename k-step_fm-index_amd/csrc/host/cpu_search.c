@@ -19,9 +19,11 @@
  *                  the inverted mask, the "X <= D_s" '$' rule).
  * Where the reference reads past its own index (B5: a step with L or R in
  * block nentries when (n+1) % d == 0) the plain step is taken from the last
- * real block at offset d, each distinct '$' row there discounted once -- the
- * integer a padding entry with the end counters gives, which is what the GPU
- * layouts store -- and the AltCounters step
+ * real block at offset d -- the integer a padding entry with the end counters
+ * would give, which is what the GPU layouts store (kfmi_search.hip
+ * end_counters: the reference's in-block rule carried to row n+1, so a '$' row
+ * two D_s share is discounted once per s there too; tests/test_alphabet.py
+ * dup_dollar_last_block_indexes pins host = every GPU layout) -- and the AltCounters step
  * reads zero counters past the sentinel and is capped at n + d rows, as the
  * GPU's AltCounters backends do.  Reads with m % K != 0 take
  * their last m % K bases from a remainder table (the true suffix-array
@@ -51,7 +53,6 @@ typedef struct {
   int      ac;               /* AltCounters semantics (tags 200, 201) */
   uint32_t nent, bwtsize;
   uint32_t dpos[KFMI_MAX_STEPS], dbase[KFMI_MAX_STEPS], dblk[KFMI_MAX_STEPS];
-  uint32_t duniq[KFMI_MAX_STEPS];   /* 1 for the first s of each distinct '$' row */
 } cs_idx_t;
 
 static inline uint32_t cs_code(uint8_t x)   /* base2index, fmIndexCPUBaseline.c:213-222 */
@@ -135,14 +136,10 @@ CS_INLINE uint32_t cs_lf(const cs_idx_t *ix, uint32_t K, uint32_t NB, int inter,
   uint32_t b = X / d, o = X % d, s, pop;
   int corr = 0;
   if (!ac) {
-    /* B5: the end counters.  They exclude each '$' row once, as the padding
-     * entry of the GPU layouts does, so a row two D_s share (a 'ref'-mode
-     * index) is discounted once here, not once per s */
-    const int end = b >= ix->nent;
-    if (end) { b = ix->nent - 1; o = d; }
+    if (b >= ix->nent) { b = ix->nent - 1; o = d; }          /* B5: the end counters */
     pop = cs_count(K, NB, inter, cs_entry(ix, b) + ix->pl_off, o, c, 0);
     for (s = 0; s < K; ++s)
-      corr += (ix->dblk[s] == b && ix->dbase[s] == c && X > ix->dpos[s] && (!end || ix->duniq[s]));
+      corr += (ix->dblk[s] == b && ix->dbase[s] == c && X > ix->dpos[s]);
     return cs_entry(ix, b)[ix->cnt_off + c] + pop - (uint32_t) corr;
   } else {
     const uint32_t e = cs_ac_e(K, b, c), half = (1u << (2u * K)) >> 1;
@@ -222,9 +219,6 @@ static int32_t cs_setup(kfmi_fmi_t *f, const kfmi_qrys_t *q, const kfmi_res_t *r
     ix->dpos[s] = f->dollarPositionBWT[s];
     ix->dbase[s] = f->dollarBaseBWT[s];
     ix->dblk[s] = f->dollarPositionBWT[s] / f->chunk;
-    ix->duniq[s] = 1;
-    for (uint32_t t = 0; t < s; ++t)
-      if (f->dollarPositionBWT[t] == f->dollarPositionBWT[s]) ix->duniq[s] = 0;
   }
   return KFMI_SUCCESS;
 }

@@ -275,8 +275,11 @@ def dup_dollar_last_block_indexes(K):
 
 def _end_counters(idx):
     """What a padding entry past the last block holds (the GPU layouts store
-    one): per code, the last entry's counter plus the code's rows in the last
-    block, less each distinct '$' row of that block with that dollarBase once.
+    one, kfmi_search.hip end_counters): per code, the last entry's counter plus
+    the code's rows in the last block, less one per step s whose '$' row lies in
+    that block with that dollarBase -- the reference's in-block rule
+    (fmIndexCPUBaseline.c:252-256) carried to row n+1, so a row two D_s share
+    is discounted twice, as every searcher of the reference does inside a block.
     Read from the tag-100 image: 24 + 8K header bytes, then entries of
     2 * NB * K plane words (plane s*2NB + t*NB + w, row p at bit 31 - p of
     word w) and NC counters."""
@@ -293,18 +296,19 @@ def _end_counters(idx):
         codes |= (b0.astype(np.int64) | (b1.astype(np.int64) << 1)) << (2 * s)
     end = last[2 * nb * k:].astype(np.int64) + np.bincount(codes, minlength=nc)
     lastblk = ne - 1
-    for p in set(h["dollar_pos"]):
+    for p, c in zip(h["dollar_pos"], h["dollar_base"]):
         if p // (32 * nb) == lastblk:
-            end[codes[p % (32 * nb)]] -= 1
+            end[c] -= 1
     return ent[0, 2 * nb * k:].astype(np.int64), end
 
 
-def test_cpu_search_end_counters_discount_each_dollar_row_once(ref_mode):
-    """past the last block (B5) the host search uses the end
-    counters, which exclude a '$' row once however many D_s share it.  One
-    K-step of every K-mer from [0, n+1) must give [C0[c], end[c]) -- end[c]
-    as a padding entry holds it; discounting the shared row once per s left
-    R one short for its dollarBase code."""
+def test_cpu_search_end_counters_on_shared_dollar_rows(ref_mode):
+    """ADVICE r4 asked whether the host search's past-the-end step (B5) and
+    the GPU layouts' padding entry disagree when two D_s share a row of the
+    last block.  They do not: both discount per s (end_counters); checked here
+    against the counters computed from the image, and on the GPU against every
+    backend (test_gpu_end_counters_equal_cpu_search_on_duplicate_dollar_rows).
+    One K-step of every K-mer from [0, n+1) gives [C0[c], end[c])."""
     import itertools
     K = ref_mode
     for t, k, idx in dup_dollar_last_block_indexes(K):
