@@ -564,9 +564,14 @@ static inline const uint32_t* host_index(const kfmi_fmi_t* f)
 }
 
 /* Counters at row n+1 (one past the last row) from a tag-100/101 index:
- * cnt_{E-1} + rows of each code in the last block, $ rows excluded.  Used for
- * the padding entry that keeps R/d == nentries in bounds when (n+1) % d == 0
- * (reference defect B5: it reads past the end there). */
+ * cnt_{E-1} + rows of each code in the last block, $ rows excluded -- each
+ * distinct row once, as the builder's counters exclude them (a 'ref'-mode index
+ * can put two D_s on one row), so the padding entry is the next
+ * block the builder would have written and every layout agrees past the end:
+ * INTER's line-local step from entry E-1, GRP/PACKED/MID's stored copies and
+ * MID's backward steps (corrected by dollar_dup like every other block).  Used
+ * for the padding entry that keeps R/d == nentries in bounds when
+ * (n+1) % d == 0 (reference defect B5: it reads past the end there). */
 static bool end_counters(const kfmi_fmi_t* f, uint32_t* out)
 {
   const uint32_t nc = 1u << (2 * f->steps), nb = f->nbitmaps;
@@ -598,8 +603,12 @@ static bool end_counters(const kfmi_fmi_t* f, uint32_t* out)
         }
       pop += (uint32_t) __builtin_popcount(m);
     }
-    for (uint32_t s = 0; s < f->steps; ++s)
-      if (f->modposdollarBWT[s] == last && f->dollarBaseBWT[s] == c && f->bwtsize > f->dollarPositionBWT[s]) pop--;
+    for (uint32_t s = 0; s < f->steps; ++s) {
+      bool first = true;   /* the first s of its row */
+      for (uint32_t t = 0; t < s; ++t) first = first && f->dollarPositionBWT[t] != f->dollarPositionBWT[s];
+      if (first && f->modposdollarBWT[s] == last && f->dollarBaseBWT[s] == c && f->bwtsize > f->dollarPositionBWT[s])
+        pop--;
+    }
     out[c] = e[2 * nb * f->steps + c] + pop;
   }
   return true;

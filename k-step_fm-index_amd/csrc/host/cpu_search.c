@@ -18,12 +18,12 @@
  *                  counters: entry b or b+1 by block parity and code half,
  *                  the inverted mask, the "X <= D_s" '$' rule).
  * Where the reference reads past its own index (B5: a step with L or R in
- * block nentries when (n+1) % d == 0) the plain step is taken from the last
- * real block at offset d -- the integer a padding entry with the end counters
- * would give, which is what the GPU layouts store (kfmi_search.hip
- * end_counters: the reference's in-block rule carried to row n+1, so a '$' row
- * two D_s share is discounted once per s there too; tests/test_alphabet.py
- * dup_dollar_last_block_indexes pins host = every GPU layout) -- and the AltCounters step
+ * block nentries when (n+1) % d == 0) the plain step reads a padding entry,
+ * as every GPU layout does: the end counters (kfmi_search.hip end_counters:
+ * the next block the builder would write, a '$' row two D_s share excluded
+ * once) and rows that read as code 0 -- on a 'ref'-mode index
+ * whose walk is not a permutation a step can land past n+1
+ * (tests/test_alphabet.py dup_dollar_last_block_indexes) -- and the AltCounters step
  * reads zero counters past the sentinel and is capped at n + d rows, as the
  * GPU's AltCounters backends do.  Reads with m % K != 0 take
  * their last m % K bases from a remainder table (the true suffix-array
@@ -53,6 +53,7 @@ typedef struct {
   int      ac;               /* AltCounters semantics (tags 200, 201) */
   uint32_t nent, bwtsize;
   uint32_t dpos[KFMI_MAX_STEPS], dbase[KFMI_MAX_STEPS], dblk[KFMI_MAX_STEPS];
+  uint32_t endc[1u << (2 * KFMI_MAX_STEPS)];   /* the padding entry's counters (plain tags) */
 } cs_idx_t;
 
 static inline uint32_t cs_code(uint8_t x)   /* base2index, fmIndexCPUBaseline.c:213-222 */
@@ -136,7 +137,10 @@ CS_INLINE uint32_t cs_lf(const cs_idx_t *ix, uint32_t K, uint32_t NB, int inter,
   uint32_t b = X / d, o = X % d, s, pop;
   int corr = 0;
   if (!ac) {
-    if (b >= ix->nent) { b = ix->nent - 1; o = d; }          /* B5: the end counters */
+    if (b >= ix->nent) {   /* B5: the padding entry -- end counters, its rows read as code 0 */
+      const uint32_t past = X - ix->nent * d;
+      return ix->endc[c] + (c == 0 ? (past < d ? past : d) : 0u);
+    }
     pop = cs_count(K, NB, inter, cs_entry(ix, b) + ix->pl_off, o, c, 0);
     for (s = 0; s < K; ++s)
       corr += (ix->dblk[s] == b && ix->dbase[s] == c && X > ix->dpos[s]);
@@ -219,6 +223,23 @@ static int32_t cs_setup(kfmi_fmi_t *f, const kfmi_qrys_t *q, const kfmi_res_t *r
     ix->dpos[s] = f->dollarPositionBWT[s];
     ix->dbase[s] = f->dollarBaseBWT[s];
     ix->dblk[s] = f->dollarPositionBWT[s] / f->chunk;
+  }
+  if (!ix->ac) {
+    /* counters at row n+1: the last entry's, plus its rows below n+1, less
+     * each distinct '$' row there once, as the builder's counters exclude them
+     * (kfmi_search.hip end_counters: what every GPU layout's padding entry
+     * holds) */
+    const uint32_t last = ix->nent - 1, rows = ix->bwtsize - last * ix->d;
+    for (uint32_t c = 0; c < ix->NC; ++c) {
+      uint32_t v = cs_entry(ix, last)[ix->cnt_off + c] +
+                   cs_count(ix->K, ix->NB, ix->inter, cs_entry(ix, last) + ix->pl_off, rows, c, 0);
+      for (s = 0; s < ix->K; ++s) {
+        int first = 1;
+        for (uint32_t t = 0; t < s; ++t) first = first && ix->dpos[t] != ix->dpos[s];
+        v -= (first && ix->dblk[s] == last && ix->dbase[s] == c && ix->bwtsize > ix->dpos[s]);
+      }
+      ix->endc[c] = v;
+    }
   }
   return KFMI_SUCCESS;
 }

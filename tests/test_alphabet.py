@@ -276,10 +276,9 @@ def dup_dollar_last_block_indexes(K):
 def _end_counters(idx):
     """What a padding entry past the last block holds (the GPU layouts store
     one, kfmi_search.hip end_counters): per code, the last entry's counter plus
-    the code's rows in the last block, less one per step s whose '$' row lies in
-    that block with that dollarBase -- the reference's in-block rule
-    (fmIndexCPUBaseline.c:252-256) carried to row n+1, so a row two D_s share
-    is discounted twice, as every searcher of the reference does inside a block.
+    the code's rows in the last block, less each distinct '$' row of that block
+    with that dollarBase once -- the next entry the builder would write (its
+    counters exclude a row once however many D_s share it).
     Read from the tag-100 image: 24 + 8K header bytes, then entries of
     2 * NB * K plane words (plane s*2NB + t*NB + w, row p at bit 31 - p of
     word w) and NC counters."""
@@ -296,19 +295,23 @@ def _end_counters(idx):
         codes |= (b0.astype(np.int64) | (b1.astype(np.int64) << 1)) << (2 * s)
     end = last[2 * nb * k:].astype(np.int64) + np.bincount(codes, minlength=nc)
     lastblk = ne - 1
+    seen = set()
     for p, c in zip(h["dollar_pos"], h["dollar_base"]):
-        if p // (32 * nb) == lastblk:
+        if p // (32 * nb) == lastblk and p not in seen:
             end[c] -= 1
+        seen.add(p)
     return ent[0, 2 * nb * k:].astype(np.int64), end
 
 
 def test_cpu_search_end_counters_on_shared_dollar_rows(ref_mode):
-    """ADVICE r4 asked whether the host search's past-the-end step (B5) and
-    the GPU layouts' padding entry disagree when two D_s share a row of the
-    last block.  They do not: both discount per s (end_counters); checked here
-    against the counters computed from the image, and on the GPU against every
-    backend (test_gpu_end_counters_equal_cpu_search_on_duplicate_dollar_rows).
-    One K-step of every K-mer from [0, n+1) gives [C0[c], end[c])."""
+    """past the last block (B5) the host search and the GPU layouts
+    disagreed when two D_s share a row of the last block (the host discounted
+    it per s; INTER's line-local step once; the stored padding entries per s,
+    which MID's backward steps then corrected a second time).  Every searcher
+    now reads the same padding entry: the end counters with each '$' row
+    excluded once.  One K-step of every K-mer from [0, n+1) gives
+    [C0[c], end[c]); on the GPU every backend equals the host search
+    (test_gpu_end_counters_equal_cpu_search_on_duplicate_dollar_rows)."""
     import itertools
     K = ref_mode
     for t, k, idx in dup_dollar_last_block_indexes(K):
@@ -318,6 +321,37 @@ def test_cpu_search_end_counters_on_shared_dollar_rows(ref_mode):
         for tagged in (idx, idx.interleave()):
             iv = K.search_cpu_array(tagged, q, 1).reshape(-1, 2).astype(np.int64)
             assert np.array_equal(iv[:, 0], c0) and np.array_equal(iv[:, 1], end), (k, idx.header()["dollar_pos"])
+        idx.close()
+
+
+def padded_image(idx):
+    """The tag-100 image with one more entry: the padding block every GPU
+    layout appends (end counters, zero planes = rows of code 0), so that the
+    oracle -- the reference's searcher restated -- never reads past its index
+    where the reference would (B5)."""
+    h = idx.header()
+    k, nb = h["steps"], h["chunk"] // 32
+    img = np.array(idx.image())
+    pad = np.zeros(2 * nb * k + h["ncounters"], np.uint32)
+    pad[2 * nb * k:] = _end_counters(idx)[1].astype(np.uint32)
+    hdr = img[:24].view(np.uint32).copy()
+    hdr[4] += 1
+    return np.concatenate([hdr.view(np.uint8), img[24:], pad.view(np.uint8)])
+
+
+def test_cpu_search_past_the_end_is_the_padding_entry(ref_mode, oracle_mod):
+    """On 'ref'-mode indexes with (n+1) % 64 == 0 and shared '$' rows in the
+    last block, searchIndexCPU equals the oracle run on the image plus the
+    GPU layouts' padding entry: steps can land past n+1 there (the walk is
+    not a permutation), where the padding block's rows read as code 0."""
+    K = ref_mode
+    rng = np.random.default_rng(8)
+    for t, k, idx in dup_dollar_last_block_indexes(K):
+        img = padded_image(idx)
+        for m, q in _all_reads(t, k, rng).items():
+            want, _ = oracle_mod.search(img, q)
+            for tagged in (idx, idx.interleave()):
+                assert np.array_equal(K.search_cpu_array(tagged, q, 1), want), (k, m, tagged.header()["tag"])
         idx.close()
 
 
