@@ -251,6 +251,13 @@ int32_t kfmi_build_stats(uint64_t *ties, uint32_t *rounds);
 /* Dedup-aware algorithmic traffic of the last search: sum over queries and
  * steps of distinct d-blocks touched (1 if L/d == R/d else 2), SURVEY 8(d). */
 int32_t kfmi_count_blocks(void *index, void *queries, uint64_t *blocks);
+/* The 128-B lines the active backend's task-kernel fetches touch over the
+ * batch (statistics, not timed): out[0] distinct lines per K-step summed over
+ * the batch (lines the two ends share counted once), out[1] LF ends whose
+ * counter lies outside their planes' line, out[2] LF ends fetched, out[3] ends
+ * counted forward from block b-1 (line-local, tags 101/201).  Set the backend
+ * and transfer the index first (as for kfmi_count_blocks). */
+int32_t kfmi_count_lines(void *index, void *queries, uint64_t out[4]);
 
 /* Streamed search from host memory: `num` queries of `size`
  * ASCII bytes at `ascii`, results [L0,R0,L1,R1,...] into `results` (2*num

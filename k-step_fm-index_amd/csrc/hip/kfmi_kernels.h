@@ -375,6 +375,102 @@ __global__ __launch_bounds__(256) void count_blocks_kernel(IdxArgs ix, const uin
   if ((threadIdx.x & 63) == 0) atomicAdd(total, (unsigned long long) cnt);
 }
 
+/* 128-B lines one LF end's task-kernel fetch touches (fetch_block: the
+ * planes, the counter word -- the superblock word for PACKED -- and, when the
+ * step is counted forward from block b-1 (line_local_prev), b-1's planes).
+ * Returns how many ids it appended to ln; *extra = 1 when the counter lies
+ * outside the planes' line(s), *prev = 1 for a line-local step. */
+template <class G>
+__device__ __forceinline__ int lf_lines(const IdxArgs& ix, uint32_t X, uint32_t c, uint64_t* ln, uint32_t* extra,
+                                        uint32_t* prev)
+{
+  const uint32_t b = X / (uint32_t) G::D;
+  Where<G> w = locate<G>(ix, b, c);
+  line_local_prev<G>(ix, b, c, w);
+  int n = 0;
+  const uint64_t p0 = (uint64_t) (uintptr_t) w.planes >> 7, p1 = (uint64_t) (uintptr_t) (w.planes + G::BMW - 1) >> 7;
+  ln[n++] = p0;
+  if (p1 != p0) ln[n++] = p1;
+  uint64_t cl;
+  if constexpr (G::LAY == LAY_PACKED) {
+    constexpr int S = sb_shift_for(G::D);
+    cl = (uint64_t) (uintptr_t) (ix.sb + (uint64_t) (b >> S) * G::NC + c) >> 7;
+  } else {
+    cl = (uint64_t) (uintptr_t) w.cnt >> 7;
+  }
+  *extra = (cl != p0 && cl != p1) ? 1u : 0u;
+  if (*extra) ln[n++] = cl;
+  *prev = w.prev ? 1u : 0u;
+  if (w.prev) {
+    const uint64_t q0 = (uint64_t) (uintptr_t) w.pplanes >> 7, q1 = (uint64_t) (uintptr_t) (w.pplanes + G::BMW - 1) >> 7;
+    if (q0 != p0 && q0 != p1) ln[n++] = q0;
+    if (q1 != q0 && q1 != p0 && q1 != p1) ln[n++] = q1;
+  }
+  return n;
+}
+
+/* Statistics only (not timed): per batch, the distinct 128-B lines each
+ * K-step's fetches touch (L's block, and R's when it is another block, as the
+ * task kernel fetches them; lines shared by the two ends counted once) --
+ * out[0]; the ends whose counter lies outside their planes' line -- out[1];
+ * the ends fetched -- out[2]; the ends counted forward from block b-1
+ * (line-local) -- out[3].  Compared with the PMC's fabric requests per read
+ * this splits a layout's requests into the structural lines its fetches need
+ * and what the caches absorb. */
+template <class G>
+__global__ __launch_bounds__(256) void count_lines_kernel(IdxArgs ix, const uint32_t* __restrict__ qp, uint64_t num,
+                                                          uint32_t steps, uint32_t nwords,
+                                                          unsigned long long* __restrict__ out)
+{
+  const uint64_t q = (uint64_t) blockIdx.x * 256 + threadIdx.x;
+  uint32_t lines = 0, extra = 0, ends = 0, prevs = 0;
+  if (q < num) {
+    uint32_t L = 0, R = ix.bwtsize;
+    if (ix.rem) {
+      const uint2 lr = ix.rtab[qp[(uint64_t) nwords * num + q]];
+      L = lr.x;
+      R = lr.y;
+    }
+    for (uint32_t t = 0; t < steps; ++t) {
+      const uint32_t word = qp[(uint64_t) (t / G::SPW) * num + q];
+      const uint32_t c = (word >> (2 * G::K * (t % G::SPW))) & (uint32_t) (G::NC - 1);
+      uint64_t ln[10];
+      uint32_t ex, pv;
+      int n = lf_lines<G>(ix, L, c, ln, &ex, &pv);
+      extra += ex;
+      prevs += pv;
+      ++ends;
+      if (R / (uint32_t) G::D != L / (uint32_t) G::D) {
+        n += lf_lines<G>(ix, R, c, ln + n, &ex, &pv);
+        extra += ex;
+        prevs += pv;
+        ++ends;
+      }
+      for (int i = 0; i < n; ++i) {
+        bool dup = false;
+        for (int j = 0; j < i; ++j) dup = dup || ln[j] == ln[i];
+        lines += dup ? 0u : 1u;
+      }
+      uint32_t sx[2 * G::K];
+      plane_xor<G::K>(c, sx);
+      L = lf_stream<G>(ix, L, c, sx);
+      R = lf_stream<G>(ix, R, c, sx);
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    lines += __shfl_xor(lines, off);
+    extra += __shfl_xor(extra, off);
+    ends += __shfl_xor(ends, off);
+    prevs += __shfl_xor(prevs, off);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(out + 0, (unsigned long long) lines);
+    atomicAdd(out + 1, (unsigned long long) extra);
+    atomicAdd(out + 2, (unsigned long long) ends);
+    atomicAdd(out + 3, (unsigned long long) prevs);
+  }
+}
+
 /* ------------------------------------------------------------------------ */
 /* dispatch tables                                                          */
 /* ------------------------------------------------------------------------ */
@@ -512,7 +608,16 @@ static hipError_t launch_rem_tab(const SearchLaunch& a)
   return hipGetLastError();
 }
 
-enum class Op { Task, Coop, Count, Locate, Ftab, RemTab };
+template <class G>
+static hipError_t launch_count_lines(const SearchLaunch& a, unsigned long long* d_out)
+{
+  const uint64_t blocks = (a.num + 255) / 256;
+  hipLaunchKernelGGL((count_lines_kernel<G>), dim3((uint32_t) blocks), dim3(256), 0, a.st, a.ix, a.qp, a.num,
+                     a.steps, a.nwords, d_out);
+  return hipGetLastError();
+}
+
+enum class Op { Task, Coop, Count, Locate, Ftab, RemTab, CountLines };
 
 /* Defined here, instantiated once per (K, NB, LAY) in kfmi_inst_*.hip. */
 template <int K, int NB, int LAY>
@@ -525,6 +630,7 @@ hipError_t dispatch_one(Op op, const SearchLaunch& a, unsigned long long* d_tota
     case Op::Locate: return launch_locate<G>(a);
     case Op::Ftab: return launch_ftab<G>(a);
     case Op::RemTab: return launch_rem_tab<G>(a);
+    case Op::CountLines: return launch_count_lines<G>(a, d_total);
     default: return launch_count<G>(a, d_total);
   }
 }

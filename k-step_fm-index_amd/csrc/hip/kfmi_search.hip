@@ -1459,15 +1459,15 @@ extern "C" void searchIndexGPU(void* index, void* queries, void* resIntervals)
   if (e) fprintf(stderr, "kstepfmi: searchIndexGPU failed: %s\n", errorCommon(e));
 }
 
-static int32_t count_on(kfmi_dev_index* di, kfmi_dev_queries* dq, uint64_t* blocks);
+static int32_t count_on(kfmi_dev_index* di, kfmi_dev_queries* dq, Op op, uint64_t* out, int nout);
 
-/* Distinct d-blocks the batch's LF steps touch (SURVEY 8(d) algorithmic bytes);
- * on a device group the sum over the members' slices. */
-extern "C" int32_t kfmi_count_blocks(void* index, void* queries, uint64_t* blocks)
+/* A statistics launch over the batch (Op::Count: one total; Op::CountLines:
+ * four), on a device group summed over the members' slices. */
+static int32_t count_stat(void* index, void* queries, Op op, uint64_t* out, int nout)
 {
   kfmi_fmi_t* f = (kfmi_fmi_t*) index;
   kfmi_qrys_t* q = (kfmi_qrys_t*) queries;
-  if (!f || !q || !blocks) return KFMI_E_BAD_ARGUMENT;
+  if (!f || !q || !out) return KFMI_E_BAD_ARGUMENT;
   DeviceGuard dg;
   std::shared_lock<RwLock> lk(index_lock(f));
   if (f->grp || q->grp) {
@@ -1475,21 +1475,36 @@ extern "C" int32_t kfmi_count_blocks(void* index, void* queries, uint64_t* block
     GroupSlices* gq = (GroupSlices*) q->grp;
     if (!gi || !gq) return KFMI_E_NOT_ON_DEVICE;   /* handles moved to different modes */
     if (gq->n != gi->n) return KFMI_E_BAD_ARGUMENT;
-    uint64_t sum = 0;
+    for (int j = 0; j < nout; ++j) out[j] = 0;
     for (int i = 0; i < gi->n; ++i) {
-      uint64_t b = 0;
-      const int32_t e = count_on(gi->di[i], gq->dq[i], &b);
+      uint64_t part[4] = {0, 0, 0, 0};
+      const int32_t e = count_on(gi->di[i], gq->dq[i], op, part, nout);
       if (e) return e;
-      sum += b;
+      for (int j = 0; j < nout; ++j) out[j] += part[j];
     }
-    *blocks = sum;
     return KFMI_SUCCESS;
   }
   if (!f->dev || !q->dev) return KFMI_E_NOT_ON_DEVICE;
-  return count_on(f->dev, q->dev, blocks);
+  return count_on(f->dev, q->dev, op, out, nout);
 }
 
-static int32_t count_on(kfmi_dev_index* di, kfmi_dev_queries* dq, uint64_t* blocks)
+/* Distinct d-blocks the batch's LF steps touch (SURVEY 8(d) algorithmic bytes);
+ * on a device group the sum over the members' slices. */
+extern "C" int32_t kfmi_count_blocks(void* index, void* queries, uint64_t* blocks)
+{
+  return count_stat(index, queries, Op::Count, blocks, 1);
+}
+
+/* The 128-B lines the backend's task-kernel fetches touch over the batch
+ * (count_lines_kernel): out[0] distinct lines per K-step summed, out[1] ends
+ * whose counter lies outside their planes' line, out[2] ends fetched, out[3]
+ * ends counted forward from block b-1. */
+extern "C" int32_t kfmi_count_lines(void* index, void* queries, uint64_t* out)
+{
+  return count_stat(index, queries, Op::CountLines, out, 4);
+}
+
+static int32_t count_on(kfmi_dev_index* di, kfmi_dev_queries* dq, Op op, uint64_t* out, int nout)
 {
   DevCtx* ctx = nullptr;
   int32_t err = ctx_for(di->device, &ctx);
@@ -1501,7 +1516,7 @@ static int32_t count_on(kfmi_dev_index* di, kfmi_dev_queries* dq, uint64_t* bloc
   err = use_rtab(di, ctx->st, a.ix, dq->rem);
   if (err) return err;
   unsigned long long* d_total = nullptr;
-  HIP_OK(hipMalloc((void**) &d_total, sizeof(unsigned long long)));
+  HIP_OK(hipMalloc((void**) &d_total, 4 * sizeof(unsigned long long)));
   a.qp = dq->packed;
   a.ascii = dq->ascii;
   a.m = dq->size;
@@ -1510,15 +1525,15 @@ static int32_t count_on(kfmi_dev_index* di, kfmi_dev_queries* dq, uint64_t* bloc
   a.steps = dq->steps;
   a.nwords = dq->nwords;
   a.res = nullptr;
-  unsigned long long total = 0;
+  unsigned long long total[4] = {0, 0, 0, 0};
   bool ok = hipMemsetAsync(d_total, 0, sizeof(total), ctx->st) == hipSuccess &&
             launch_pack(dq, ctx->st) == hipSuccess &&
-            (dq->num == 0 || dispatch(Op::Count, di->K, di->nb, di->layout, a, d_total) == hipSuccess) &&
-            hipMemcpyAsync(&total, d_total, sizeof(total), hipMemcpyDeviceToHost, ctx->st) == hipSuccess &&
+            (dq->num == 0 || dispatch(op, di->K, di->nb, di->layout, a, d_total) == hipSuccess) &&
+            hipMemcpyAsync(total, d_total, sizeof(total), hipMemcpyDeviceToHost, ctx->st) == hipSuccess &&
             hipStreamSynchronize(ctx->st) == hipSuccess;
   (void) hipFree(d_total);
   if (!ok) return KFMI_E_KERNEL;
-  *blocks = total;
+  for (int j = 0; j < nout && j < 4; ++j) out[j] = total[j];
   return KFMI_SUCCESS;
 }
 

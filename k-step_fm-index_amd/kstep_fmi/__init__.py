@@ -100,6 +100,7 @@ def load() -> ctypes.CDLL:
         "kfmi_build_index_gpu": (i32, [vp, u64, u32, u32, i32, pvp]),
         "kfmi_build_stats": (i32, [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32)]),
         "kfmi_count_blocks": (i32, [vp, vp, ctypes.POINTER(ctypes.c_uint64)]),
+        "kfmi_count_lines": (i32, [vp, vp, ctypes.POINTER(ctypes.c_uint64)]),
         "kfmi_probe_replay": (i32, [vp, vp, i32, i32, i32, ctypes.POINTER(ctypes.c_double),
                                     ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
         "kfmi_device_index_bytes": (u64, [vp]),
@@ -412,6 +413,14 @@ def count_blocks(index: Index, queries: Queries) -> int:
     n = ctypes.c_uint64()
     _check(load().kfmi_count_blocks(index.ptr, queries.ptr, ctypes.byref(n)), "count_blocks")
     return int(n.value)
+
+
+def count_lines(index: Index, queries: Queries) -> dict:
+    """kfmi_count_lines: the 128-B lines the backend's fetches touch over the batch."""
+    out = (ctypes.c_uint64 * 4)()
+    _check(load().kfmi_count_lines(index.ptr, queries.ptr, out), "count_lines")
+    return {"lines": int(out[0]), "counter_outside_planes_line": int(out[1]), "ends_fetched": int(out[2]),
+            "line_local_ends": int(out[3])}
 
 
 def probe_replay(index: Index, queries: Queries, unroll: int = 1, reps: int = 5, groups: int = 1) -> dict:

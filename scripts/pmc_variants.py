@@ -72,8 +72,12 @@ def main():
             if first is None:
                 first = res
             blocks = K.count_blocks(idx, q)
+            # the lines the backend's fetches need (kfmi_count_lines): the
+            # structural share of the requests the PMC pass counts
+            lines = K.count_lines(idx, q)
             order.append({"backend": b, "k": k, "launches": a.warmup + a.steps, "warmup": a.warmup,
                           "lf_ms_hip_events": round(float(np.mean(lf[a.warmup:])), 4), "distinct_blocks": blocks,
+                          "lines_model": lines,
                           "results_equal_first": bool(np.array_equal(res, first))})
             log(order[-1])
             idx.free_gpu()

@@ -64,6 +64,11 @@ for o in order["order"]:
         "line_requests_per_query": round(req / nq, 2), "tcc_req_per_launch": int(tcc) if tcc else None,
         "kernel_ms_under_pmc": round(ms, 3), "lf_ms_hip_events_same_run": o["lf_ms_hip_events"],
         "distinct_blocks": o["distinct_blocks"], "launches_timed": len(timed),
+        **({"model_lines_per_query": round(o["lines_model"]["lines"] / nq, 2),
+            "model_counter_outside_line_per_end": round(o["lines_model"]["counter_outside_planes_line"]
+                                                         / o["lines_model"]["ends_fetched"], 4),
+            "model_line_local_per_end": round(o["lines_model"]["line_local_ends"] / o["lines_model"]["ends_fetched"], 4),
+            "model_ends_per_query": round(o["lines_model"]["ends_fetched"] / nq, 2)} if "lines_model" in o else {}),
         "request_bytes_upper_bound": int(req * 128)}
 assert i == len(rows), (i, len(rows))
 print(json.dumps(out, indent=1))
