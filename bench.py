@@ -102,7 +102,7 @@ def parse():
     p.add_argument("--cpu-port-only", action="store_true",
                    help="time only our restatement, not the reference's CPU binary (oracle/_ref)")
     p.add_argument("--variants", default="task,coop,task-ac,coop-ac,task-ac128,coop-ac128,task-ac-mid,coop-ac-mid,"
-                                         "task-packed,coop-packed,task-mid,coop-mid,task-mid+ftab14",
+                                         "task-packed,coop-packed,task-mid,coop-mid,task-mid+ftab14,task-mid+ftab16",
                    help="other backends timed on rank 0 at N=1 (empty = none)")
     p.add_argument("--variant-steps", type=int, default=3)
     p.add_argument("--config5-queries", type=int, default=10_000_000,
@@ -1150,7 +1150,7 @@ def config_rows(detail: dict, a=None) -> dict:
                                  if x is not None},
                          "cpu_ref": {k: x for k, x in (("mqps", ref.get("value")), ("cores", ref.get("cores")),
                                                        ("eq", ref.get("parity_with_gpu"))) if x is not None}}
-    for key, what, pair in (("2", "Task-2Step, 3 Gbase, 10M x 100 bp", ("task-mid", "task")),
+    for key, what, pair in (("2", "Task-2Step, 3 Gbase, 10M x 100 bp", ("task-mid", "task", "task-mid+ftab16")),
                             ("3", "Coop-2Step, same index and reads", ("coop-mid", "coop")),
                             ("4", "Task-2Step-AltCounters, same", ("task-ac", "task-ac-mid"))):
         r = {b: pick(b) for b in pair}
@@ -1183,7 +1183,12 @@ def config_rows(detail: dict, a=None) -> dict:
         if k4.get("results_equal_k2_per_rank") is not None:
             r["eq_k2"] = _all_true(k4.get("results_equal_k2_per_rank"))
         k4c5 = c5_row(k4.get("config5"))
-        rows["k4"] = dict(what="K=4 index, coop-grp, same reads", **r, **({"c5": k4c5} if k4c5 else {}))
+        ft = _compact_row(k4.get("coop-grp+ftab16"))
+        if ft:
+            ft.pop("eq", None)
+            ft["eq_k2"] = (k4.get("coop-grp+ftab16") or {}).get("results_equal_k2")
+        rows["k4"] = dict(what="K=4 index, coop-grp, same reads", **r, **({"c5": k4c5} if k4c5 else {}),
+                          **({"ftab16": ft} if ft else {}))
     return rows
 
 
