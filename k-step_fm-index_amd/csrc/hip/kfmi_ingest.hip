@@ -168,7 +168,6 @@ struct DevMem {
 extern "C" int32_t kfmi_load_queries_gpu(const char* fn, uint32_t sizequery, uint64_t numqueries, void** queries)
 {
   if (!fn || !queries || sizequery == 0) return KFMI_E_BAD_ARGUMENT;
-  if (64ull * sizequery + 16 > 160ull * 1024) return KFMI_E_BAD_ARGUMENT;   /* as upload_queries */
   *queries = nullptr;
   DeviceGuard dg;
   const int dev = kfmi_current_device();

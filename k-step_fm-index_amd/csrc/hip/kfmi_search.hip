@@ -229,31 +229,69 @@ hipStream_t thread_stream(int dev)
 /* query packing: ASCII [num][m] -> codes [nwords][num], step t of query q in */
 /* word t/SPW, bits 2K*(t%SPW)..; step t consumes chars m-1-K*t-i (i<K), the  */
 /* order of fmIndexCPUBaseline.c:200-226.                                   */
+/*                                                                          */
+/* Reads of any length: block (x, y) packs the tq rows q0 = x*tq .. and the   */
+/* word chunk y (words [y*wc, (y+1)*wc)), staging only the bytes of those     */
+/* rows that chunk reads -- [m-rem-K*s1, m-rem-K*s0) for its steps [s0, s1),  */
+/* at most K*SPW*wc <= 1 KiB per row -- HBM -> LDS with 16-byte loads where   */
+/* the slice is aligned, then one thread per row builds the chunk's words     */
+/* (writes of a word row: consecutive queries, coalesced).                   */
 /* ------------------------------------------------------------------------ */
+
+/* LDS row pitch of the pack kernel: whole rows stay contiguous (pitch m), a
+ * slice of a longer row takes a 16-B multiple (the launch sizes LDS with the
+ * largest slice, wc words) */
+__host__ __device__ constexpr uint32_t pack_pitch(uint32_t m, uint32_t len)
+{
+  return len == m ? m : ((len + 15u) & ~15u);
+}
 
 template <int K>
 __global__ __launch_bounds__(256) void pack_queries_kernel(const uint8_t* __restrict__ q, uint64_t num,
                                                            uint32_t m, uint32_t steps, uint32_t nwords,
-                                                           uint32_t tq, uint32_t* __restrict__ out, uint32_t rem)
+                                                           uint32_t tq, uint32_t wc, uint32_t* __restrict__ out,
+                                                           uint32_t rem)
 {
   extern __shared__ __attribute__((aligned(16))) uint8_t tile[];
   constexpr int SPW = 32 / (2 * K);
   const uint64_t q0 = (uint64_t) blockIdx.x * tq;
   const uint64_t nq = (num - q0) < tq ? (num - q0) : tq;
-  const uint64_t bytes = nq * m;
-  const uint8_t* src = q + q0 * m;   /* q0*m is a multiple of 64*m: 16-byte aligned when m%... */
-  if ((((uintptr_t) src) & 15u) == 0) {
-    const uint64_t n16 = bytes / 16;
-    for (uint64_t i = threadIdx.x; i < n16; i += blockDim.x)
-      reinterpret_cast<uint4*>(tile)[i] = reinterpret_cast<const uint4*>(src)[i];
-    for (uint64_t i = n16 * 16 + threadIdx.x; i < bytes; i += blockDim.x) tile[i] = src[i];
+  const uint32_t w0 = blockIdx.y * wc;
+  const uint32_t w1 = w0 + wc < nwords ? w0 + wc : nwords;
+  const uint32_t s0 = w0 * SPW, s1 = (w1 * SPW < steps ? w1 * SPW : steps);
+  /* one chunk (reads up to ~1 KiB): whole rows, one contiguous piece of nq
+   * rows; else row r's slice [lo, lo + len) at tile + r * pitch */
+  const bool whole = gridDim.y == 1;
+  const uint32_t lo = whole ? 0u : (m - rem) - K * s1, len = whole ? m : K * (s1 - s0);
+  const uint32_t pitch = pack_pitch(m, len);
+  const bool al = ((m | lo) & 15u) == 0 && ((((uintptr_t) q) & 15u) == 0);
+  if (whole) {
+    const uint64_t bytes = nq * m;
+    const uint8_t* src = q + q0 * m;
+    if ((((uintptr_t) src) & 15u) == 0) {
+      const uint64_t n16 = bytes / 16;
+      for (uint64_t i = threadIdx.x; i < n16; i += blockDim.x)
+        reinterpret_cast<uint4*>(tile)[i] = reinterpret_cast<const uint4*>(src)[i];
+      for (uint64_t i = n16 * 16 + threadIdx.x; i < bytes; i += blockDim.x) tile[i] = src[i];
+    } else {
+      for (uint64_t i = threadIdx.x; i < bytes; i += blockDim.x) tile[i] = src[i];
+    }
+  } else if (al) {
+    const uint32_t n16 = len / 16;
+    for (uint64_t i = threadIdx.x; i < nq * n16; i += blockDim.x) {
+      const uint64_t r = i / n16, k = i % n16;
+      reinterpret_cast<uint4*>(tile + r * pitch)[k] = reinterpret_cast<const uint4*>(q + (q0 + r) * m + lo)[k];
+    }
   } else {
-    for (uint64_t i = threadIdx.x; i < bytes; i += blockDim.x) tile[i] = src[i];
+    for (uint64_t i = threadIdx.x; i < nq * len; i += blockDim.x) {
+      const uint64_t r = i / len, k = i % len;
+      tile[r * pitch + k] = q[(q0 + r) * m + lo + k];
+    }
   }
   __syncthreads();
   for (uint32_t t = threadIdx.x; t < nq; t += blockDim.x) {
-    const uint8_t* p = tile + (uint64_t) t * m;
-    for (uint32_t w = 0; w < nwords; ++w) {
+    const uint8_t* p = tile + (uint64_t) t * pitch;   /* p[pos - lo] for pos in [lo, lo + len) */
+    for (uint32_t w = w0; w < w1; ++w) {
       uint32_t word = 0;
 #pragma unroll
       for (int j = 0; j < SPW; ++j) {
@@ -262,13 +300,14 @@ __global__ __launch_bounds__(256) void pack_queries_kernel(const uint8_t* __rest
           const int pos = (int) (m - rem) - 1 - (int) (K * st);
           uint32_t c = 0;
 #pragma unroll
-          for (int i = 0; i < K; ++i) c |= code_of(p[pos - i]) << (2 * i);
+          for (int i = 0; i < K; ++i) c |= code_of(p[pos - i - (int) lo]) << (2 * i);
           word |= c << (2 * K * j);
         }
       }
       out[(uint64_t) w * num + q0 + t] = word;
     }
-    if (rem) out[(uint64_t) nwords * num + q0 + t] = rem_code(p + m - rem, rem);   /* remainder table index */
+    /* remainder table index: the last rem bases, read from HBM (chunk 0 only) */
+    if (rem && blockIdx.y == 0) out[(uint64_t) nwords * num + q0 + t] = rem_code(q + (q0 + t) * m + m - rem, rem);
   }
 }
 
@@ -1253,7 +1292,6 @@ void release_upload_staging()
 int32_t upload_queries(kfmi_qrys_t* q, uint32_t K, int dev, DevCtx* ctx)
 {
   if (q->size == 0 || K == 0) return KFMI_E_BAD_ARGUMENT;
-  if (64ull * q->size + 16 > 160ull * 1024) return KFMI_E_BAD_ARGUMENT;   /* pack tile (64 rows + 16 B) must fit LDS */
   kfmi_dev_queries* dq = new (std::nothrow) kfmi_dev_queries();
   if (!dq) return KFMI_E_ALLOCATING_MFASTA;
   dq->device = dev;
@@ -1282,22 +1320,32 @@ int32_t upload_queries(kfmi_qrys_t* q, uint32_t K, int dev, DevCtx* ctx)
 hipError_t launch_pack(const kfmi_dev_queries* dq, hipStream_t st)
 {
   if (dq->num == 0 || !dq->ascii) return hipSuccess;   /* no ASCII: packed by the host on upload */
+  /* word chunks of at most 1 KiB of row bytes (K * SPW bases per word), rows
+   * per block so that one block stages <= 64 KiB; m == rem (no K-step) runs
+   * one empty chunk for the remainder codes */
+  const uint32_t bpw = dq->K * (32u / (2u * dq->K));      /* bases per word: 16 (K = 1, 2, 4), 15 (K = 3) */
+  const uint32_t wc = 1024u / bpw;
+  const uint32_t nchunks = dq->nwords ? (dq->nwords + wc - 1) / wc : 1u;
+  /* the largest slice a chunk stages: whole rows when one chunk covers them */
+  const uint32_t pitch = nchunks == 1 ? dq->size : pack_pitch(dq->size, wc * bpw);
   uint32_t tq = 256;
-  while ((uint64_t) tq * dq->size > 64 * 1024 && tq > 64) tq >>= 1;
+  while ((uint64_t) tq * pitch > 64 * 1024 && tq > 64) tq >>= 1;
   const uint64_t blocks = (dq->num + tq - 1) / tq;
-  const size_t lds = (size_t) tq * dq->size + 16;
+  if (blocks > 0xFFFFFFFFull || nchunks > 65535u) return hipErrorInvalidValue;
+  const size_t lds = (size_t) tq * pitch + 16;
+  const dim3 grid((uint32_t) blocks, nchunks);
   if (dq->K == 1)
-    hipLaunchKernelGGL((pack_queries_kernel<1>), dim3((uint32_t) blocks), dim3(256), lds, st, dq->ascii, dq->num,
-                       dq->size, dq->steps, dq->nwords, tq, dq->packed, dq->rem);
+    hipLaunchKernelGGL((pack_queries_kernel<1>), grid, dim3(256), lds, st, dq->ascii, dq->num, dq->size, dq->steps,
+                       dq->nwords, tq, wc, dq->packed, dq->rem);
   else if (dq->K == 4)
-    hipLaunchKernelGGL((pack_queries_kernel<4>), dim3((uint32_t) blocks), dim3(256), lds, st, dq->ascii, dq->num,
-                       dq->size, dq->steps, dq->nwords, tq, dq->packed, dq->rem);
+    hipLaunchKernelGGL((pack_queries_kernel<4>), grid, dim3(256), lds, st, dq->ascii, dq->num, dq->size, dq->steps,
+                       dq->nwords, tq, wc, dq->packed, dq->rem);
   else if (dq->K == 3)
-    hipLaunchKernelGGL((pack_queries_kernel<3>), dim3((uint32_t) blocks), dim3(256), lds, st, dq->ascii, dq->num,
-                       dq->size, dq->steps, dq->nwords, tq, dq->packed, dq->rem);
+    hipLaunchKernelGGL((pack_queries_kernel<3>), grid, dim3(256), lds, st, dq->ascii, dq->num, dq->size, dq->steps,
+                       dq->nwords, tq, wc, dq->packed, dq->rem);
   else
-    hipLaunchKernelGGL((pack_queries_kernel<2>), dim3((uint32_t) blocks), dim3(256), lds, st, dq->ascii, dq->num,
-                       dq->size, dq->steps, dq->nwords, tq, dq->packed, dq->rem);
+    hipLaunchKernelGGL((pack_queries_kernel<2>), grid, dim3(256), lds, st, dq->ascii, dq->num, dq->size, dq->steps,
+                       dq->nwords, tq, wc, dq->packed, dq->rem);
   return hipGetLastError();
 }
 

@@ -505,7 +505,7 @@ extern "C" int32_t kfmi_search_stream(void* index, const char* ascii, uint64_t n
   const uint32_t K = d0->K;
   /* m % K != 0 takes the remainder table, like kfmi_search: not on the
    * AltCounters layouts (their semantics differ there) */
-  if (size == 0 || 64ull * size + 16 > 160ull * 1024) return KFMI_E_BAD_ARGUMENT;
+  if (size == 0) return KFMI_E_BAD_ARGUMENT;
   if (size % K && !rem_supported(d0->layout)) return KFMI_E_BAD_ARGUMENT;
   double ms[KFMI_MAX_GROUP][3] = {};
   uint64_t np[KFMI_MAX_GROUP] = {};

@@ -148,6 +148,14 @@ def test_gpu_parse_golden_and_large(kfmi_mod, gpu_idx, tmp_path):
     q = K.Queries.load_gpu(path, 150, 12_345)
     assert np.array_equal(search_loaded(K, idx, q), want[:2 * 12_345])
     q.close()
+    # long reads (several pack-kernel word chunks; odd length -> remainder table)
+    long = np.concatenate([t[rng.integers(0, len(t) - 5001, size=300)[:, None] + np.arange(5001)],
+                           rng.choice(np.frombuffer(b"ACGT", np.uint8), size=(20, 5001))])
+    path = tmp_path / "long.fa"
+    path.write_bytes(b"".join(b">l%d\n%s\n" % (j, long[j].tobytes()) for j in range(long.shape[0])))
+    q = K.Queries.load_gpu(path, 5001)
+    assert np.array_equal(search_loaded(K, idx, q), K.search_array(idx, long, "task-mid"))
+    q.close()
 
 
 @pytest.mark.gpu

@@ -117,10 +117,11 @@ def test_stream_errors(setup):
 
 
 @pytest.mark.parametrize("hostpack", ["1", "0", "2", "3"])
-@pytest.mark.parametrize("m", [2, 4, 16, 32, 34, 254, 256, 300, 1000])
+@pytest.mark.parametrize("m", [2, 4, 16, 32, 34, 254, 256, 300, 1000, 1030, 3000, 6000])
 def test_stream_read_lengths(kfmi_mod, hostpack, m, monkeypatch):
     """Every word-count class of the host packer (ceil(m/16) words, partial
-    last word) and of the fused/unfused device paths."""
+    last word) and of the fused/unfused device paths, up to reads the pack
+    kernel takes in several word chunks."""
     K = kfmi_mod
     monkeypatch.setenv("KFMI_STREAM_HOSTPACK", hostpack)
     K.set_device(0)
