@@ -104,7 +104,7 @@ def parse():
     p.add_argument("--variants", default="task,coop,task-ac,coop-ac,task-ac128,coop-ac128,task-ac-mid,coop-ac-mid,"
                                          "task-packed,coop-packed,task-mid,coop-mid,task-mid+ftab14,task-mid+ftab16",
                    help="other backends timed on rank 0 at N=1 (empty = none)")
-    p.add_argument("--variant-steps", type=int, default=3)
+    p.add_argument("--variant-steps", type=int, default=5)
     p.add_argument("--config5-queries", type=int, default=10_000_000,
                    help="reads per GPU of the config #5 leg (0 = skip)")
     p.add_argument("--config5-qlen", type=int, default=150)
