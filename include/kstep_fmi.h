@@ -231,6 +231,14 @@ uint64_t  kfmi_results_num(void *results);
 int32_t kfmi_build_index_cpu(const char *text, uint64_t n, uint32_t k, uint32_t d, void **index);
 int32_t kfmi_build_index_gpu(const char *text, uint64_t n, uint32_t k, uint32_t d,
                              int32_t want_host_image, void **index);
+/* A 2K-step index derived on the current device from a K-step one (K = 1 or
+ * 2, tag 100 or 101; k_out = 2K), without the text: row i's 2K-mer is its
+ * K-mer plus the K-mer of row LF_K(i) (DESIGN.md 5d').  The result is the
+ * tag-100 index the builders write for that text at k_out, byte for byte
+ * (ACGT texts; 'ref'-mode walks that are not a permutation return
+ * KFMI_E_BUILDING_FMI); its entries stay in HBM unless want_host_image.  The
+ * reference's K = 2 files thus search on the K = 4 layout (coop-grp). */
+int32_t kfmi_derive_index_gpu(void *index, uint32_t k_out, int32_t want_host_image, void **out);
 /* Alphabet of the builders (process-wide; NULL = KFMI_ALPHABET, else "acgt"):
  *   "acgt" only A/C/G/T (anything else: KFMI_E_BUILDING_BWT);
  *   "map"  every byte through base2index (N -> G, lowercase -> uppercase), a

@@ -223,9 +223,9 @@ __global__ __launch_bounds__(256) void k_dollar(const uint32_t* __restrict__ sa,
 /* One wave per d-block; lane = row inside a 64-row chunk. */
 template <int K>
 __global__ __launch_bounds__(256) void k_blocks(const uint32_t* __restrict__ sa, const uint32_t* __restrict__ packed,
-                                                uint64_t n, uint32_t d, uint32_t nentries, uint32_t d0, uint32_t d1,
-                                                uint32_t d2, uint32_t d3, uint32_t* __restrict__ entries,
-                                                uint32_t* __restrict__ counts)
+                                                const uint8_t* __restrict__ codes, uint64_t n, uint32_t d,
+                                                uint32_t nentries, uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3,
+                                                uint32_t* __restrict__ entries, uint32_t* __restrict__ counts)
 {
   constexpr int NC = 1 << (2 * K);
   const uint32_t lane = threadIdx.x & 63;
@@ -245,7 +245,9 @@ __global__ __launch_bounds__(256) void k_blocks(const uint32_t* __restrict__ sa,
     const bool valid = (base + lane < d) && (r < rows);
     uint32_t code = 0;
     bool isd = false;
-    if (valid) {
+    if (valid && codes) {   /* a derived index: the row's K-mer code is given */
+      code = codes[r];
+    } else if (valid) {
       const uint64_t s_a = r == 0 ? n : (uint64_t) sa[r - 1];
 #pragma unroll
       for (int s = 0; s < K; ++s) {
@@ -254,6 +256,8 @@ __global__ __launch_bounds__(256) void k_blocks(const uint32_t* __restrict__ sa,
         const uint32_t cs = ((uint64_t) pos == n) ? 0u : base_at(packed, (uint64_t) pos);
         code |= cs << (2 * s);
       }
+    }
+    if (valid) {
 #pragma unroll
       for (int s = 0; s < K; ++s) isd |= (drows[s] == (uint32_t) r);
     }
@@ -424,6 +428,122 @@ int32_t resolve_ties(const uint64_t* keys, uint32_t* sa, uint64_t n, uint64_t h0
   return KFMI_SUCCESS;
 }
 
+/* Steps 5-7: the entries of the K-step index whose row r has the K-mer code
+ * codes[r] (derived indexes) or, without codes, the one read from SA and the
+ * packed text; drow = the '$' rows D_s, dbase = their stored codes ('$' as A).
+ * The suffix array (sa_buf, when given) is released once its samples are
+ * taken, before the scans; on success *out owns the index (entries on the
+ * device when !host_image). */
+static int32_t entries_from_rows(hipStream_t st, DevBuf* sa_buf, const uint32_t* packed, const uint8_t* codes,
+                                 uint64_t n, uint32_t k, uint32_t d, const uint32_t* drow, const uint32_t* dbase,
+                                 uint32_t sa_rate, int dev, bool host_image, kfmi_fmi_t** out)
+{
+  const uint64_t rows = n + 1;
+  const uint32_t nentries = (uint32_t) ((rows + d - 1) / d);
+  const uint32_t nc = 1u << (2 * k), nb = d / 32;
+  const uint32_t* sa = sa_buf ? sa_buf->as<uint32_t>() : nullptr;
+  kfmi_fmi_t* f = nullptr;
+  int32_t err = kfmi_index_alloc_ex(100, k, (uint32_t) rows, nentries, d, nullptr, nullptr, host_image ? 1 : 0, &f);
+  if (err) return err;
+  const uint32_t ew = f->entry_words;
+  DevBuf ent, counts, occ, cp;
+  auto fail = [&](int32_t e) { freeIndex((void**) &f); return e; };
+  if (ent.alloc((uint64_t) ew * 4 * nentries) != hipSuccess || counts.alloc((uint64_t) nc * 4 * nentries) != hipSuccess ||
+      occ.alloc((uint64_t) nc * 4 * nentries) != hipSuccess || cp.alloc(4 * nc) != hipSuccess)
+    return fail(KFMI_E_ALLOCATING_FMI);
+  if (hipMemsetAsync(ent.p, 0, (uint64_t) ew * 4 * nentries, st) != hipSuccess) return fail(KFMI_E_BUILDING_FMI);
+  {
+    const dim3 grid((nentries + 3) / 4);
+    hipError_t le;
+    switch (k) {
+      case 1: hipLaunchKernelGGL((k_blocks<1>), grid, dim3(256), 0, st, sa, packed, codes, n, d,
+                                 nentries, drow[0], drow[1], drow[2], drow[3], ent.as<uint32_t>(), counts.as<uint32_t>()); break;
+      case 2: hipLaunchKernelGGL((k_blocks<2>), grid, dim3(256), 0, st, sa, packed, codes, n, d,
+                                 nentries, drow[0], drow[1], drow[2], drow[3], ent.as<uint32_t>(), counts.as<uint32_t>()); break;
+      case 3: hipLaunchKernelGGL((k_blocks<3>), grid, dim3(256), 0, st, sa, packed, codes, n, d,
+                                 nentries, drow[0], drow[1], drow[2], drow[3], ent.as<uint32_t>(), counts.as<uint32_t>()); break;
+      default: hipLaunchKernelGGL((k_blocks<4>), grid, dim3(256), 0, st, sa, packed, codes, n, d,
+                                  nentries, drow[0], drow[1], drow[2], drow[3], ent.as<uint32_t>(), counts.as<uint32_t>()); break;
+    }
+    le = hipGetLastError();
+    if (le != hipSuccess) return fail(KFMI_E_BUILDING_FMI);
+  }
+  if (sa_rate && sa) {   /* locate samples, before the SA is released */
+    err = kfmi_sa_alloc(f, sa_rate);
+    if (err) return fail(err);
+    DevBuf smp;
+    if (smp.alloc(4 * f->sa_count) != hipSuccess) return fail(KFMI_E_ALLOCATING_FMI);
+    hipLaunchKernelGGL(k_sample, dim3((uint32_t) ((f->sa_count + 255) / 256)), dim3(256), 0, st, sa, n,
+                       sa_rate, f->sa_count, smp.as<uint32_t>());
+    if (hipGetLastError() != hipSuccess ||
+        hipMemcpyAsync(f->h_sa, smp.p, 4 * f->sa_count, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+      return fail(KFMI_E_BUILDING_FMI);
+  }
+  if (sa_buf) sa_buf->release();
+  /* 6. per-code exclusive scans over blocks */
+  {
+    size_t tb = 0;
+    if (rocprim::exclusive_scan(nullptr, tb, counts.as<uint32_t>(), occ.as<uint32_t>(), 0u, (size_t) nentries,
+                                rocprim::plus<uint32_t>(), st) != hipSuccess)
+      return fail(KFMI_E_BUILDING_FMI);
+    DevBuf tmp;
+    if (tmp.alloc(tb) != hipSuccess) return fail(KFMI_E_ALLOCATING_FMI);
+    for (uint32_t c = 0; c < nc; ++c)
+      if (rocprim::exclusive_scan(tmp.p, tb, counts.as<uint32_t>() + (uint64_t) c * nentries,
+                                  occ.as<uint32_t>() + (uint64_t) c * nentries, 0u, (size_t) nentries,
+                                  rocprim::plus<uint32_t>(), st) != hipSuccess)
+        return fail(KFMI_E_BUILDING_FMI);
+  }
+  /* 7. C' and counters */
+  std::vector<uint32_t> lastocc(nc), lastcnt(nc), cprime(nc);
+  for (uint32_t c = 0; c < nc; ++c) {
+    if (hipMemcpyAsync(&lastocc[c], occ.as<uint32_t>() + (uint64_t) c * nentries + nentries - 1, 4,
+                       hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(&lastcnt[c], counts.as<uint32_t>() + (uint64_t) c * nentries + nentries - 1, 4,
+                       hipMemcpyDeviceToHost, st) != hipSuccess)
+      return fail(KFMI_E_BUILDING_FMI);
+  }
+  if (hipStreamSynchronize(st) != hipSuccess) return fail(KFMI_E_BUILDING_FMI);
+  {
+    uint64_t acc = 0;
+    for (uint32_t c = 0; c < nc; ++c) {
+      cprime[c] = (uint32_t) acc;
+      acc += (uint64_t) lastocc[c] + lastcnt[c];
+    }
+    for (uint32_t s = 0; s < k; ++s) {
+      const uint32_t masked = dbase[s] & (0xFFFFFFFFu << (2 * s));
+      for (uint32_t c = masked; c < nc; ++c) cprime[c]++;
+    }
+  }
+  if (hipMemcpyAsync(cp.p, cprime.data(), 4 * nc, hipMemcpyHostToDevice, st) != hipSuccess) return fail(KFMI_E_BUILDING_FMI);
+  hipLaunchKernelGGL(k_fill, dim3((nentries + 255) / 256), dim3(256), 0, st, occ.as<uint32_t>(), nentries, nc,
+                     2 * nb * k, ew, cp.as<uint32_t>(), ent.as<uint32_t>());
+  if (hipGetLastError() != hipSuccess ||
+      (host_image &&
+       hipMemcpyAsync(f->h_index, ent.p, (uint64_t) ew * 4 * nentries, hipMemcpyDeviceToHost, st) != hipSuccess) ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return fail(KFMI_E_BUILDING_FMI);
+  if (!host_image) {   /* the entries stay in HBM, owned by the handle */
+    f->d_entries = ent.as<uint32_t>();
+    f->d_entries_dev = dev;
+    ent.p = nullptr;
+  }
+  for (uint32_t s = 0; s < k; ++s) {
+    f->dollarPositionBWT[s] = drow[s];
+    f->dollarBaseBWT[s] = dbase[s];
+    f->modposdollarBWT[s] = drow[s] / d;
+  }
+  uint32_t* hdr = reinterpret_cast<uint32_t*>(f->image);   /* the header words of the image */
+  for (uint32_t s = 0; s < k; ++s) {
+    hdr[6 + s] = drow[s];
+    hdr[6 + k + s] = dbase[s];
+  }
+  *out = f;
+  return KFMI_SUCCESS;
+}
+
+
 int32_t build_gpu(const char* text, uint64_t n, uint32_t k, uint32_t d, uint32_t sa_rate, int dev, bool host_image,
                   kfmi_fmi_t** out)
 {
@@ -439,8 +559,6 @@ int32_t build_gpu(const char* text, uint64_t n, uint32_t k, uint32_t d, uint32_t
   struct StreamGuard { hipStream_t s; ~StreamGuard() { (void) hipStreamDestroy(s); } } sg{st};
 
   const uint64_t rows = n + 1;
-  const uint32_t nentries = (uint32_t) ((rows + d - 1) / d);
-  const uint32_t nc = 1u << (2 * k), nb = d / 32;
   const uint64_t nwords = (n + 15) / 16 + 4;
 
   /* 0. alphabet (fmi_build.c): "ref" on a text with bytes other than A/C/G/T
@@ -573,69 +691,6 @@ int32_t build_gpu(const char* text, uint64_t n, uint32_t k, uint32_t d, uint32_t
     *out = f;
     return KFMI_SUCCESS;
   }
-  kfmi_fmi_t* f = nullptr;
-  int32_t err = kfmi_index_alloc_ex(100, k, (uint32_t) rows, nentries, d, nullptr, nullptr, host_image ? 1 : 0, &f);
-  if (err) return err;
-  const uint32_t ew = f->entry_words;
-  DevBuf ent, counts, occ, cp;
-  auto fail = [&](int32_t e) { freeIndex((void**) &f); return e; };
-  if (ent.alloc((uint64_t) ew * 4 * nentries) != hipSuccess || counts.alloc((uint64_t) nc * 4 * nentries) != hipSuccess ||
-      occ.alloc((uint64_t) nc * 4 * nentries) != hipSuccess || cp.alloc(4 * nc) != hipSuccess)
-    return fail(KFMI_E_ALLOCATING_FMI);
-  if (hipMemsetAsync(ent.p, 0, (uint64_t) ew * 4 * nentries, st) != hipSuccess) return fail(KFMI_E_BUILDING_FMI);
-  {
-    const dim3 grid((nentries + 3) / 4);
-    hipError_t le;
-    switch (k) {
-      case 1: hipLaunchKernelGGL((k_blocks<1>), grid, dim3(256), 0, st, sa.as<uint32_t>(), packed.as<uint32_t>(), n, d,
-                                 nentries, drow[0], drow[1], drow[2], drow[3], ent.as<uint32_t>(), counts.as<uint32_t>()); break;
-      case 2: hipLaunchKernelGGL((k_blocks<2>), grid, dim3(256), 0, st, sa.as<uint32_t>(), packed.as<uint32_t>(), n, d,
-                                 nentries, drow[0], drow[1], drow[2], drow[3], ent.as<uint32_t>(), counts.as<uint32_t>()); break;
-      case 3: hipLaunchKernelGGL((k_blocks<3>), grid, dim3(256), 0, st, sa.as<uint32_t>(), packed.as<uint32_t>(), n, d,
-                                 nentries, drow[0], drow[1], drow[2], drow[3], ent.as<uint32_t>(), counts.as<uint32_t>()); break;
-      default: hipLaunchKernelGGL((k_blocks<4>), grid, dim3(256), 0, st, sa.as<uint32_t>(), packed.as<uint32_t>(), n, d,
-                                  nentries, drow[0], drow[1], drow[2], drow[3], ent.as<uint32_t>(), counts.as<uint32_t>()); break;
-    }
-    le = hipGetLastError();
-    if (le != hipSuccess) return fail(KFMI_E_BUILDING_FMI);
-  }
-  if (sa_rate) {   /* locate samples, before the SA is released */
-    err = kfmi_sa_alloc(f, sa_rate);
-    if (err) return fail(err);
-    DevBuf smp;
-    if (smp.alloc(4 * f->sa_count) != hipSuccess) return fail(KFMI_E_ALLOCATING_FMI);
-    hipLaunchKernelGGL(k_sample, dim3((uint32_t) ((f->sa_count + 255) / 256)), dim3(256), 0, st, sa.as<uint32_t>(), n,
-                       sa_rate, f->sa_count, smp.as<uint32_t>());
-    if (hipGetLastError() != hipSuccess ||
-        hipMemcpyAsync(f->h_sa, smp.p, 4 * f->sa_count, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess)
-      return fail(KFMI_E_BUILDING_FMI);
-  }
-  sa.release();
-  /* 6. per-code exclusive scans over blocks */
-  {
-    size_t tb = 0;
-    if (rocprim::exclusive_scan(nullptr, tb, counts.as<uint32_t>(), occ.as<uint32_t>(), 0u, (size_t) nentries,
-                                rocprim::plus<uint32_t>(), st) != hipSuccess)
-      return fail(KFMI_E_BUILDING_FMI);
-    DevBuf tmp;
-    if (tmp.alloc(tb) != hipSuccess) return fail(KFMI_E_ALLOCATING_FMI);
-    for (uint32_t c = 0; c < nc; ++c)
-      if (rocprim::exclusive_scan(tmp.p, tb, counts.as<uint32_t>() + (uint64_t) c * nentries,
-                                  occ.as<uint32_t>() + (uint64_t) c * nentries, 0u, (size_t) nentries,
-                                  rocprim::plus<uint32_t>(), st) != hipSuccess)
-        return fail(KFMI_E_BUILDING_FMI);
-  }
-  /* 7. C' and counters */
-  std::vector<uint32_t> lastocc(nc), lastcnt(nc), cprime(nc);
-  for (uint32_t c = 0; c < nc; ++c) {
-    if (hipMemcpyAsync(&lastocc[c], occ.as<uint32_t>() + (uint64_t) c * nentries + nentries - 1, 4,
-                       hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipMemcpyAsync(&lastcnt[c], counts.as<uint32_t>() + (uint64_t) c * nentries + nentries - 1, 4,
-                       hipMemcpyDeviceToHost, st) != hipSuccess)
-      return fail(KFMI_E_BUILDING_FMI);
-  }
-  if (hipStreamSynchronize(st) != hipSuccess) return fail(KFMI_E_BUILDING_FMI);
   /* dollarBaseBWT[s] = c(D_s): SA[D_s] = s, so BWT_s'[D_s] = T$[(s-1-s') mod (n+1)] */
   uint32_t dbase[4] = {0, 0, 0, 0};
   for (uint32_t s = 0; s < k; ++s) {
@@ -649,45 +704,28 @@ int32_t build_gpu(const char* text, uint64_t n, uint32_t k, uint32_t d, uint32_t
     }
     dbase[s] = code;
   }
-  {
-    uint64_t acc = 0;
-    for (uint32_t c = 0; c < nc; ++c) {
-      cprime[c] = (uint32_t) acc;
-      acc += (uint64_t) lastocc[c] + lastcnt[c];
-    }
-    for (uint32_t s = 0; s < k; ++s) {
-      const uint32_t masked = dbase[s] & (0xFFFFFFFFu << (2 * s));
-      for (uint32_t c = masked; c < nc; ++c) cprime[c]++;
-    }
-  }
-  if (hipMemcpyAsync(cp.p, cprime.data(), 4 * nc, hipMemcpyHostToDevice, st) != hipSuccess) return fail(KFMI_E_BUILDING_FMI);
-  hipLaunchKernelGGL(k_fill, dim3((nentries + 255) / 256), dim3(256), 0, st, occ.as<uint32_t>(), nentries, nc,
-                     2 * nb * k, ew, cp.as<uint32_t>(), ent.as<uint32_t>());
-  if (hipGetLastError() != hipSuccess ||
-      (host_image &&
-       hipMemcpyAsync(f->h_index, ent.p, (uint64_t) ew * 4 * nentries, hipMemcpyDeviceToHost, st) != hipSuccess) ||
-      hipStreamSynchronize(st) != hipSuccess)
-    return fail(KFMI_E_BUILDING_FMI);
-  if (!host_image) {   /* the entries stay in HBM, owned by the handle */
-    f->d_entries = ent.as<uint32_t>();
-    f->d_entries_dev = dev;
-    ent.p = nullptr;
-  }
-  for (uint32_t s = 0; s < k; ++s) {
-    f->dollarPositionBWT[s] = drow[s];
-    f->dollarBaseBWT[s] = dbase[s];
-    f->modposdollarBWT[s] = drow[s] / d;
-  }
-  uint32_t* hdr = reinterpret_cast<uint32_t*>(f->image);   /* the header words of the image */
-  for (uint32_t s = 0; s < k; ++s) {
-    hdr[6 + s] = drow[s];
-    hdr[6 + k + s] = dbase[s];
-  }
-  *out = f;
-  return KFMI_SUCCESS;
+  return entries_from_rows(st, &sa, packed.as<uint32_t>(), nullptr, n, k, d, drow, dbase, sa_rate, dev, host_image,
+                           out);
 }
 
 }  // namespace
+
+namespace kfmi {
+
+/* Steps 5-7 for a 2K-step index derived from a K-step one (kfmi_derive.hip):
+ * the rows' K-mer codes are given on the device (d_codes, n + 1 bytes). */
+int32_t build_from_codes(const uint8_t* d_codes, uint64_t n, uint32_t k, uint32_t d, const uint32_t* drow,
+                         const uint32_t* dbase, int dev, bool host_image, kfmi_fmi_t** out)
+{
+  if (n == 0 || n + 1 > 0xFFFFFFFEull || k < 1 || k > 4 || d == 0 || d % 32) return KFMI_E_BAD_ARGUMENT;
+  BHIP(hipSetDevice(dev));
+  hipStream_t st;
+  BHIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  struct StreamGuard { hipStream_t s; ~StreamGuard() { (void) hipStreamDestroy(s); } } sg{st};
+  return entries_from_rows(st, nullptr, nullptr, d_codes, n, k, d, drow, dbase, 0, dev, host_image, out);
+}
+
+}  // namespace kfmi
 
 extern "C" int32_t kfmi_build_index_gpu_sa(const char* text, uint64_t n, uint32_t k, uint32_t d, uint32_t sa_rate,
                                            void** index)

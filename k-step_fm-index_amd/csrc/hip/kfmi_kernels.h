@@ -375,6 +375,38 @@ __global__ __launch_bounds__(256) void count_blocks_kernel(IdxArgs ix, const uin
   if ((threadIdx.x & 63) == 0) atomicAdd(total, (unsigned long long) cnt);
 }
 
+/* Derivation of a 2K-step index from a K-step one (kfmi_derive_index_gpu):
+ * row i's 2K-mer code is its own K-mer code (T[p-1-s], s < K, p = SA[i]) and,
+ * above it, the K-mer code of row LF_K(i) -- the row of suffix p - K, whose
+ * K-mer is T[p-1-K-s].  One thread per row (grid-stride).  The K rows whose
+ * K-mer holds the '$' (D_s, s < K) have no valid LF: their upper half is
+ * written by the host from the text's tail (row 0's code, see the caller);
+ * a row whose LF lands on D_s is the row of suffix K + s, the new D_{K+s}
+ * (isa[s]). */
+template <class G>
+__global__ __launch_bounds__(256) void derive_codes_kernel(IdxArgs ix, uint64_t rows, uint8_t* __restrict__ codes,
+                                                           uint32_t* __restrict__ isa)
+{
+  for (uint64_t i = (uint64_t) blockIdx.x * 256 + threadIdx.x; i < rows; i += (uint64_t) gridDim.x * 256) {
+    const uint32_t X = (uint32_t) i;
+    const uint32_t c = row_code<G>(ix, X);
+    bool dollar = false;
+#pragma unroll
+    for (int s = 0; s < G::K; ++s) dollar = dollar || ix.dl.dpos[s] == X;
+    uint32_t up = 0;
+    if (!dollar) {
+      uint32_t sx[2 * G::K];
+      plane_xor<G::K>(c, sx);
+      const uint32_t j = lf_stream<G>(ix, X, c, sx);
+      up = row_code<G>(ix, j);
+#pragma unroll
+      for (int s = 0; s < G::K; ++s)
+        if (ix.dl.dpos[s] == j) isa[s] = X;
+    }
+    codes[i] = (uint8_t) (c | (up << (2 * G::K)));
+  }
+}
+
 /* 128-B lines one LF end's task-kernel fetch touches (fetch_block: the
  * planes, the counter word -- the superblock word for PACKED -- and, when the
  * step is counted forward from block b-1 (line_local_prev), b-1's planes).
@@ -500,6 +532,9 @@ struct SearchLaunch {
   uint64_t ftab_n;
   /* remainder table build: rem bases -> ftab_out */
   uint32_t rem;
+  /* index derivation: 2K-mer code per row (num rows), the rows of suffixes K..2K-1 */
+  uint8_t* derive_codes;
+  uint32_t* derive_isa;
 };
 
 template <class G, int SPLIT>
@@ -617,7 +652,18 @@ static hipError_t launch_count_lines(const SearchLaunch& a, unsigned long long* 
   return hipGetLastError();
 }
 
-enum class Op { Task, Coop, Count, Locate, Ftab, RemTab, CountLines };
+template <class G>
+static hipError_t launch_derive(const SearchLaunch& a)
+{
+  if constexpr (G::LAY == LAY_INTER && G::K <= 2) {
+    hipLaunchKernelGGL((derive_codes_kernel<G>), dim3(grid_blocks((a.num + 255) / 256, 65536)), dim3(256), 0, a.st,
+                       a.ix, a.num, a.derive_codes, a.derive_isa);
+    return hipGetLastError();
+  }
+  return hipErrorInvalidValue;
+}
+
+enum class Op { Task, Coop, Count, Locate, Ftab, RemTab, CountLines, Derive };
 
 /* Defined here, instantiated once per (K, NB, LAY) in kfmi_inst_*.hip. */
 template <int K, int NB, int LAY>
@@ -631,6 +677,7 @@ hipError_t dispatch_one(Op op, const SearchLaunch& a, unsigned long long* d_tota
     case Op::Ftab: return launch_ftab<G>(a);
     case Op::RemTab: return launch_rem_tab<G>(a);
     case Op::CountLines: return launch_count_lines<G>(a, d_total);
+    case Op::Derive: return launch_derive<G>(a);
     default: return launch_count<G>(a, d_total);
   }
 }

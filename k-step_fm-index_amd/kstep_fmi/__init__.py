@@ -98,6 +98,7 @@ def load() -> ctypes.CDLL:
         "kfmi_results_num": (u64, [vp]),
         "kfmi_build_index_cpu": (i32, [vp, u64, u32, u32, pvp]),
         "kfmi_build_index_gpu": (i32, [vp, u64, u32, u32, i32, pvp]),
+        "kfmi_derive_index_gpu": (i32, [vp, u32, i32, pvp]),
         "kfmi_build_stats": (i32, [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32)]),
         "kfmi_count_blocks": (i32, [vp, vp, ctypes.POINTER(ctypes.c_uint64)]),
         "kfmi_count_lines": (i32, [vp, vp, ctypes.POINTER(ctypes.c_uint64)]),
@@ -304,6 +305,13 @@ class Index(_Handle):
 
     def save(self, fn) -> None:
         _check(load().saveIndex(str(fn).encode(), self._p), f"saveIndex {fn}")
+
+    def derive(self, k: int, host_image: bool = False) -> "Index":
+        """kfmi_derive_index_gpu: the 2K-step index of the same text, derived on
+        the current device from this K-step one (K = 1 or 2, k = 2K)."""
+        p = ctypes.c_void_p()
+        _check(load().kfmi_derive_index_gpu(self._p, int(k), int(bool(host_image)), ctypes.byref(p)), "derive_index")
+        return Index(p.value)
 
     def interleave(self) -> "Index":
         p = ctypes.c_void_p()

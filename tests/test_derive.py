@@ -1,0 +1,95 @@
+"""kfmi_derive_index_gpu (DESIGN.md 5d'): a 2K-step index derived on the
+device from a K-step one, without the text, equals the index the builders
+write from the text at 2K -- the whole tag-100 image, byte for byte (header,
+'$' rows and their codes, planes, counters) -- for K = 1 -> 2 and 2 -> 4,
+several d, texts whose tails put '$' rows in the last block and (n+1) % d == 0;
+the reference's own tag-101 file derives the same; searches on the derived
+K = 4 index equal the K = 2 ones."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def K(kfmi_mod):
+    if kfmi_mod.device_count() < 1:
+        pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
+    kfmi_mod.set_device(0)
+    return kfmi_mod
+
+
+def _text(n, tail, seed):
+    rng = np.random.default_rng(seed)
+    t = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=n)
+    if tail == "T-run":
+        t[-min(n, 70):] = ord("T")
+    elif tail == "A-run":
+        t[-min(n, 70):] = ord("A")
+    elif tail == "periodic":
+        t[:] = np.resize(np.frombuffer(b"ACGTTGCA", np.uint8), n)
+    return t.tobytes()
+
+
+@pytest.mark.parametrize("kin", [1, 2])
+@pytest.mark.parametrize("d", [32, 64, 128])
+@pytest.mark.parametrize("n,tail", [(9, "random"), (100, "random"), (127, "T-run"), (191, "A-run"), (255, "random"),
+                                    (1000, "periodic"), (5_000, "T-run"), (200_001, "random")])
+def test_derived_image_equals_built(K, kin, d, n, tail):
+    text = _text(n, tail, n + d + kin)
+    src = K.Index.build(text, k=kin, d=d)
+    want = K.Index.build(text, k=2 * kin, d=d)
+    got = src.derive(2 * kin, host_image=True)
+    assert got.header() == want.header()
+    assert np.array_equal(np.asarray(got.image()), np.asarray(want.image())), (kin, d, n, tail)
+    for x in (src, want, got):
+        x.close()
+
+
+def test_derived_from_tag101_and_device_resident(K):
+    """The reference's interleaved file derives the same index, and a
+    device-resident result (no host image) fetches the same bytes."""
+    text = _text(50_001, "random", 3)
+    src = K.Index.build(text, k=2, d=64)
+    want = K.Index.build(text, k=4, d=64)
+    for s in (src.interleave(), K.Index.build(text, k=2, d=64, gpu=True, host_image=False)):
+        got = s.derive(4)
+        assert np.array_equal(np.asarray(got.image()), np.asarray(want.image()))
+        got.close()
+        s.close()
+
+
+def test_derived_k4_searches_equal_k2(K):
+    rng = np.random.default_rng(5)
+    text = _text(300_001, "random", 11)
+    t = np.frombuffer(text, np.uint8)
+    i2 = K.Index.build(text, k=2, d=64, gpu=True)
+    i4 = i2.derive(4)
+    for m in (100, 150, 102, 8):
+        reads = np.ascontiguousarray(np.concatenate([
+            t[rng.integers(0, len(t) - m, size=4000)[:, None] + np.arange(m)],
+            rng.choice(np.frombuffer(b"ACGTNacgt", np.uint8), size=(500, m))]))
+        want = K.search_array(i2, reads, "task-mid")
+        for be in ("coop-grp", "task-grp"):
+            assert np.array_equal(K.search_array(i4, reads, be), want), (m, be)
+    i4.close()
+    i2.close()
+
+
+def test_derive_rejects(K):
+    text = _text(1000, "random", 1)
+    i2 = K.Index.build(text, k=2, d=64)
+    for kout in (2, 3, 8):
+        with pytest.raises(K.KfmiError):
+            i2.derive(kout)
+    i4 = K.Index.build(text, k=4, d=64)
+    with pytest.raises(K.KfmiError):
+        i4.derive(8)
+    ac = i2.alt_counters()[0]
+    with pytest.raises(K.KfmiError):
+        ac.derive(4)
+    tiny = K.Index.build(b"ACGTACG", k=2, d=64)   # n = 7 < 2 * 4: row 0's LF would be a '$' row
+    with pytest.raises(K.KfmiError):
+        tiny.derive(4)
+    for x in (i2, i4, ac, tiny):
+        x.close()
