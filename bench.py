@@ -1074,6 +1074,32 @@ def kstep3_leg(text: bytes, reads: np.ndarray, res: np.ndarray, steps: int) -> d
     return out
 
 
+def derived_leg(idx, reads: np.ndarray, res: np.ndarray, steps: int) -> dict:
+    """The bench's K = 2 index, without its text, derived on the device into
+    the K = 4 index (kfmi_derive_index_gpu, DESIGN.md 5d') and searched on the
+    K = 4 grouped-counter layout: the reference's K = 2 file at K = 4 speed.
+    The results must equal the K = 2 (md5-pinned) ones."""
+    t = time.perf_counter()
+    i4 = idx.derive(4)
+    out = {"what": "K=4 index derived on the device from the K=2 index (no text), coop-grp",
+           "derive_s": round(time.perf_counter() - t, 2)}
+    q = K.Queries.from_array(reads)
+    r = K.Results.alloc(reads.shape[0])
+    try:
+        wall, lf, tot = time_backend(i4, q, r, "coop-grp", steps, 60)
+        out.update({"mqps": round(q.num() / float(np.median(wall)) / 1e6, 2), "lf_ms": round(lf, 3),
+                    "results_equal": bool(np.array_equal(r.array(), res)), "device_index_bytes": i4.device_bytes()})
+        wall, lf, tot = time_backend(i4, q, r, "coop-grp+ftab16", steps, 5)
+        out["ftab16"] = {"mqps": round(q.num() / float(np.median(wall)) / 1e6, 2), "lf_ms": round(lf, 3),
+                         "results_equal": bool(np.array_equal(r.array(), res))}
+    finally:
+        q.close()
+        r.close()
+        i4.free_gpu()
+        i4.close()
+    return out
+
+
 def time_backend(idx, q, r, backend, steps, warmup):
     """`backend` may carry "+ftabN": the Bowtie-style jump-start table of N bases."""
     name, _, opt = backend.partition("+")
@@ -1138,7 +1164,12 @@ def config_rows(detail: dict, a=None) -> dict:
     head = {k: x for k, x in head.items() if x is not None}
 
     def pick(b):
-        return head if b == backend else _compact_row(V.get(b))
+        if b == backend:
+            return head
+        r = _compact_row(V.get(b), extra=("derive_s",))
+        if r and b == "derived_k4" and (V.get(b) or {}).get("ftab16"):
+            r["ftab16"] = (V[b]["ftab16"] or {}).get("mqps")
+        return r
 
     rows = {}
     c1 = V.get("config1_64mbase")
@@ -1156,7 +1187,8 @@ def config_rows(detail: dict, a=None) -> dict:
                                                        ("eq", ref.get("parity_with_gpu"))) if x is not None},
                          "cpu_product": {k: x for k, x in (("mqps", prod.get("value")), ("cores", prod.get("cores")),
                                                            ("eq", prod.get("equal_gpu"))) if x is not None}}
-    for key, what, pair in (("2", "Task-2Step, 3 Gbase, 10M x 100 bp", ("task-mid", "task", "task-mid+ftab16")),
+    for key, what, pair in (("2", "Task-2Step, 3 Gbase, 10M x 100 bp",
+                             ("task-mid", "task", "task-mid+ftab16", "derived_k4")),
                             ("3", "Coop-2Step, same index and reads", ("coop-mid", "coop")),
                             ("4", "Task-2Step-AltCounters, same", ("task-ac", "task-ac-mid"))):
         r = {b: pick(b) for b in pair}
@@ -1523,6 +1555,14 @@ def main():
             log(f"K=3 leg {extra['kstep3']}")
         except K.KfmiError as e:
             extra["kstep3"] = {"error": str(e)}
+    if a.kstep4 and a.k == 2 and a.d == 64 and D.world == 1:
+        try:
+            extra["derived_k4"] = derived_leg(idx, reads, res, a.steps)
+            log(f"derived K=4 leg {extra['derived_k4']}")
+            log(f"derived K=4 leg: {extra['derived_k4'].get('mqps')} Mq/s", brief=True)
+        except K.KfmiError as e:
+            extra["derived_k4"] = {"error": str(e)}
+        K.set_backend(a.backend)
     if ingest is not None:
         extra["ingest_file"] = ingest          # rank 0's; every rank's is under "ranks"
     cpu = None
