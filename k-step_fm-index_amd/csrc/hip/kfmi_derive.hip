@@ -26,29 +26,23 @@ int32_t build_from_codes(const uint8_t* d_codes, uint64_t n, uint32_t k, uint32_
                          const uint32_t* dbase, int dev, bool host_image, kfmi_fmi_t** out);
 }
 
-using namespace kfmi;
+namespace kfmi {
 
-extern "C" int32_t kfmi_derive_index_gpu(void* index, uint32_t k_out, int32_t want_host_image, void** out)
+/* The derivation on device `dev` (current); the caller holds f's index lock
+ * (shared is enough: f's own device copy is not touched). */
+int32_t derive_index(kfmi_fmi_t* f, uint32_t k_out, int dev, bool host_image, kfmi_fmi_t** out)
 {
-  kfmi_fmi_t* f = (kfmi_fmi_t*) index;
-  if (!f || !out) return KFMI_E_BAD_ARGUMENT;
   *out = nullptr;
   const uint32_t K = f->steps;
   if ((K != 1 && K != 2) || k_out != 2 * K) return KFMI_E_BAD_ARGUMENT;
   if (f->tag != KFMI_INDEX_VER_BASELINE && f->tag != KFMI_INDEX_VER_INTERLEAVE) return KFMI_E_BAD_ARGUMENT;
   const uint64_t rows = f->bwtsize, n = rows - 1;
   if (n < 2ull * k_out) return KFMI_E_BAD_ARGUMENT;   /* row 0's LF must not land on a '$' row */
-  if (kfmi_device_count() < 1) return KFMI_E_NO_DEVICE;
-  DeviceGuard dg;
-  const int dev = kfmi_current_device();
   DevCtx* ctx = nullptr;
   int32_t err = ctx_for(dev, &ctx);
   if (err) return err;
   kfmi_dev_index* di = nullptr;
-  {
-    std::shared_lock<RwLock> lk(index_lock(f));
-    err = upload_index(f, KFMI_BK_TASK, dev, ctx, &di);   /* the tag-101 layout, a copy of our own */
-  }
+  err = upload_index(f, KFMI_BK_TASK, dev, ctx, &di);   /* the tag-101 layout, a copy of our own */
   if (err) return err;
   uint8_t* codes = nullptr;
   uint32_t* isa = nullptr;
@@ -120,9 +114,24 @@ extern "C" int32_t kfmi_derive_index_gpu(void* index, uint32_t k_out, int32_t wa
     dbase[s] = c8;
   }
   kfmi_fmi_t* g = nullptr;
-  err = build_from_codes(codes, n, k_out, f->chunk, drow, dbase, dev, want_host_image != 0, &g);
+  err = build_from_codes(codes, n, k_out, f->chunk, drow, dbase, dev, host_image, &g);
   cleanup();
   if (err) return err;
   *out = g;
   return KFMI_SUCCESS;
+}
+
+}  // namespace kfmi
+
+using namespace kfmi;
+
+extern "C" int32_t kfmi_derive_index_gpu(void* index, uint32_t k_out, int32_t want_host_image, void** out)
+{
+  kfmi_fmi_t* f = (kfmi_fmi_t*) index;
+  if (!f || !out) return KFMI_E_BAD_ARGUMENT;
+  *out = nullptr;
+  if (kfmi_device_count() < 1) return KFMI_E_NO_DEVICE;
+  DeviceGuard dg;
+  std::shared_lock<RwLock> lk(index_lock(f));
+  return derive_index(f, k_out, kfmi_current_device(), want_host_image != 0, (kfmi_fmi_t**) out);
 }

@@ -277,14 +277,14 @@ int32_t group_transfer(kfmi_fmi_t* f, kfmi_qrys_t* q, kfmi_res_t* r, const int* 
       DevCtx* ctx = nullptr;
       int32_t e = ctx_for(devs[i], &ctx);
       if (!e && parsed) {
-        e = slice_device_queries(q->dev, g->q0[i], g->num[i], f->steps, devs[i], ctx, &g->dq[i]);
+        e = slice_device_queries(q->dev, g->q0[i], g->num[i], device_steps(f), devs[i], ctx, &g->dq[i]);
         return e;
       }
       kfmi_qrys_t sh{};
       sh.num = g->num[i];
       sh.size = q->size;
       sh.h_queries = q->h_queries + g->q0[i] * q->size;
-      if (!e) e = upload_queries(&sh, f->steps, devs[i], ctx);
+      if (!e) e = upload_queries(&sh, device_steps(f), devs[i], ctx);
       g->dq[i] = sh.dev;
       return e;
     });

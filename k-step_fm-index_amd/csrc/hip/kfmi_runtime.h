@@ -137,6 +137,11 @@ hipError_t launch_pack(const kfmi_dev_queries* dq, hipStream_t st);
 
 /* uploads (kfmi_search.hip) */
 int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx, kfmi_dev_index** out = nullptr);
+/* the 2K-step index of a K-step one, derived on `dev` (kfmi_derive.hip) */
+int32_t derive_index(kfmi_fmi_t* f, uint32_t k_out, int dev, bool host_image, kfmi_fmi_t** out);
+/* K of the handle's device copy (a K = 2 file on the grouped layout searches
+ * a derived K = 4 index), else of the file: the K queries are packed for */
+uint32_t device_steps(const kfmi_fmi_t* f);
 int32_t upload_sa(const kfmi_fmi_t* f, kfmi_dev_index* di, DevCtx* ctx);
 int32_t upload_queries(kfmi_qrys_t* q, uint32_t K, int dev, DevCtx* ctx);
 void query_geometry(kfmi_dev_queries* dq, uint32_t K);

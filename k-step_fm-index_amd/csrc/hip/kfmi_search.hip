@@ -840,6 +840,25 @@ int32_t upload_sa(const kfmi_fmi_t* f, kfmi_dev_index* di, DevCtx* ctx)
 /* Uploads f for `backend` to `dev`: into f->dev, or into *out (group replicas). */
 int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx, kfmi_dev_index** out)
 {
+  if (f->steps == 2 && layout_of(backend) == LAY_GRP) {
+    /* a K = 2 file (the reference's GPU index) on the grouped-counter layout:
+     * its K = 4 index derived on the device, laid out, and dropped again
+     * (DESIGN.md 5d'); the handle keeps the K = 4 device copy */
+    kfmi_fmi_t* g = nullptr;
+    int32_t e = derive_index(f, 4, dev, false, &g);
+    if (e) return e;
+    kfmi_dev_index* di = nullptr;
+    e = upload_index(g, backend, dev, ctx, &di);
+    freeIndex((void**) &g);
+    if (e) return e;
+    if (out) {
+      *out = di;
+      return KFMI_SUCCESS;
+    }
+    if (f->dev) free_dev_index(f->dev);
+    f->dev = di;
+    return KFMI_SUCCESS;
+  }
   if (f->steps < 1 || f->steps > 4) return KFMI_E_BAD_ARGUMENT;   /* GPU kernels: K in {1,2}; 4 on LAY_GRP */
   if (!nb_supported(f->nbitmaps)) return KFMI_E_BAD_ARGUMENT;
   const int lay = layout_of(backend);
@@ -1356,6 +1375,13 @@ hipError_t launch_pack(const kfmi_dev_queries* dq, hipStream_t st)
 /* interface.h:40, e.g. fmIndexGPU-Coop-2Step.cu:250-285 (index, $ arrays,
  * queries and zeroed results to the device; the index is re-laid-out for the
  * selected backend). */
+uint32_t device_steps(const kfmi_fmi_t* f)
+{
+  if (f->dev) return f->dev->K;
+  if (f->grp && ((const GroupIndex*) f->grp)->di[0]) return ((const GroupIndex*) f->grp)->di[0]->K;
+  return f->steps;
+}
+
 extern "C" int32_t transferCPUtoGPU(void* index, void* queries, void* results)
 {
   kfmi_fmi_t* f = (kfmi_fmi_t*) index;
@@ -1400,7 +1426,7 @@ extern "C" int32_t transferCPUtoGPU(void* index, void* queries, void* results)
     if (!q->h_queries && q->num) {   /* parsed on the device (kfmi_load_queries_gpu): already there */
       if (!q->dev) return KFMI_E_NOT_ON_DEVICE;
       if (q->dev->device != dev) return KFMI_E_BAD_ARGUMENT;
-      query_geometry(q->dev, f->steps);
+      query_geometry(q->dev, device_steps(f));
       kfmi_dev_queries* dq = q->dev;
       if (dq->nwords + 1 > dq->packed_rows) {   /* K = 3 packs 15 bases per word: a few more rows */
         (void) hipFree(dq->packed);
@@ -1411,7 +1437,7 @@ extern "C" int32_t transferCPUtoGPU(void* index, void* queries, void* results)
         dq->packed_rows = dq->nwords + 1;
       }
     } else {
-      err = upload_queries(q, f->steps, dev, ctx);
+      err = upload_queries(q, device_steps(f), dev, ctx);
       if (err) return err;
     }
   }

@@ -93,3 +93,39 @@ def test_derive_rejects(K):
         tiny.derive(4)
     for x in (i2, i4, ac, tiny):
         x.close()
+
+
+def test_grouped_backends_derive_on_upload(K):
+    """transferCPUtoGPU of a K = 2 index for coop-grp / task-grp derives its
+    K = 4 index on the device and searches it (the queries are packed for
+    K = 4); streamed search, block counts and locate through the row-sampled
+    SA of the K = 2 handle (the suffix array is the same) follow."""
+    rng = np.random.default_rng(9)
+    text = _text(100_001, "random", 21)
+    t = np.frombuffer(text, np.uint8)
+    i2 = K.Index.build(text, k=2, d=64, gpu=True, sa_rate=8)
+    reads = np.ascontiguousarray(t[rng.integers(0, len(t) - 100, size=3000)[:, None] + np.arange(100)])
+    want = K.search_array(i2, reads, "task-mid")
+    q = K.Queries.from_array(reads)
+    r = K.Results.alloc(reads.shape[0])
+    K.set_backend("task-mid")
+    K.transfer_to_gpu(i2, q, r)
+    K.search(i2, q, r)
+    loc_want = K.locate(i2, r)
+    off_w, pos_w = loc_want.offsets().copy(), loc_want.positions().copy()
+    loc_want.close()
+    for be in ("coop-grp", "task-grp"):
+        K.set_backend(be)
+        K.transfer_to_gpu(i2, q, r)
+        K.search(i2, q, r)
+        K.transfer_to_cpu(r)
+        assert np.array_equal(r.array(), want), be
+        assert np.array_equal(K.search_stream(i2, reads), want), be
+        assert K.count_blocks(i2, q) > 0
+        loc = K.locate(i2, r)
+        assert np.array_equal(loc.offsets(), off_w) and np.array_equal(loc.positions(), pos_w), be
+        loc.close()
+    K.set_backend("task-mid")
+    q.close()
+    r.close()
+    i2.close()

@@ -22,7 +22,9 @@ def test_dropin_links_against_engine():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("backend,tag,res_tag", [("task", 101, 100), ("coop", 101, 100), ("task-packed", 100, 100),
-                                                 ("task-ac", 201, 200), ("coop-ac", 201, 200)])
+                                                 ("task-ac", 201, 200), ("coop-ac", 201, 200),
+                                                 # the K = 2 file on the K = 4 layout (derived on upload, DESIGN 5d')
+                                                 ("coop-grp", 101, 100), ("task-grp", 100, 100)])
 def test_reference_driver_runs_on_engine(tmp_path, backend, tag, res_tag):
     if not DROPIN.exists():
         pytest.fail("oracle/_ref/searchQueries_dropin missing on the GPU box")

@@ -99,10 +99,13 @@ def test_grp_rejects_other_k_and_takes_any_m(kfmi_mod, k4):
     K = kfmi_mod
     t, i4, i2 = k4
     q = _reads(t, 100, 100, 3)
-    for backend, idx in (("task-grp", i2), ("coop-grp", i2), ("task-mid", i4), ("coop", i4)):
+    for backend, idx in (("task-mid", i4), ("coop", i4)):
         with pytest.raises(K.KfmiError) as e:
             K.search_array(idx, q, backend)
         assert e.value.code == 33, backend
+    # the grouped backends take a K = 2 index too: its K = 4 index is derived on upload (DESIGN 5d')
+    for backend in GRP:
+        assert np.array_equal(K.search_array(i2, q, backend), K.search_array(i2, q, "task-mid")), backend
     # 102 % 4 = 2 (reference defect B6): the last 2 bases from the remainder
     # table (tests/test_remainder.py), the interval equals the K = 2 one
     q = _reads(t, 2000, 102, 1)
