@@ -264,7 +264,9 @@ __global__ __launch_bounds__(256) void pack_queries_kernel(const uint8_t* __rest
   const bool whole = gridDim.y == 1;
   const uint32_t lo = whole ? 0u : (m - rem) - K * s1, len = whole ? m : K * (s1 - s0);
   const uint32_t pitch = pack_pitch(m, len);
-  const bool al = ((m | lo) & 15u) == 0 && ((((uintptr_t) q) & 15u) == 0);
+  /* 16-B copies only where the whole slice is 16-B words (K = 3 slices are
+   * 15-base words: a 1,020-byte chunk, or a short last one, takes bytes) */
+  const bool al = ((m | lo | len) & 15u) == 0 && ((((uintptr_t) q) & 15u) == 0);
   if (whole) {
     const uint64_t bytes = nq * m;
     const uint8_t* src = q + q0 * m;

@@ -67,7 +67,10 @@ def test_k3_matches_oracle(kfmi_mod, oracle_mod, k3, backend, fused, split, monk
     t, i3, i1 = k3
     for m, n in ((99, 20_000), (150, 4_000), (3, 500), (15, 2_000), (126, 2_000), (129, 2_000), (255, 1_000),
                  (300, 1_000), (100, 3_000), (101, 3_000), (1, 300), (2, 300), (256, 1_000),
-                 (1020, 300), (1500, 300), (3001, 150)):
+                 (1020, 300), (1500, 300), (3001, 150),
+                 # m % 16 == 0: 16-B aligned slices whose length is not (the
+                 # last chunk of 1,040 / 1,056, chunk 3 of 4,128)
+                 (1040, 200), (1056, 200), (4128, 100)):
         q = _reads(t, n, m, m + 3)
         want = oracle_mod.search(i3.image() if m % 3 == 0 else i1.image(), q)[0]
         got = K.search_array(i3, q, backend)
