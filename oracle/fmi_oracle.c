@@ -34,6 +34,7 @@
 #define OR_OK            0
 #define OR_E_HEADER      5   /* E_READING_FMI, common.h:41 */
 #define OR_E_BADARG      99  /* E_NOT_IMPLEMENTED */
+#define OR_E_UNDEFINED   98  /* a step reads past the index: the reference's result is undefined */
 
 typedef struct {
   uint32_t tag, steps, bwtsize, ncounters, nentries, chunk;
@@ -128,11 +129,16 @@ static inline uint32_t code_of(uint8_t x)
   return (b1 | b0) >> 1;
 }
 
-/* One LF step of one interval end. */
-static inline uint32_t lf_step(const ofmi_t *f, uint32_t X, uint32_t code)
+/* One LF step of one interval end.  An entry past the image (the reference
+ * reads past its file there) sets *oob and returns 0 instead. */
+static inline uint32_t lf_step(const ofmi_t *f, uint32_t X, uint32_t code, int *oob)
 {
   uint32_t d = f->chunk, b = X / d, s;
   int32_t shift = (int32_t) (X % d);
+  if (b >= f->nentries || (f->ac && b + 1 >= f->nentries && (((b & 1u) != 0) == (code < f->nc / 2)))) {
+    *oob = 1;
+    return 0;
+  }
   if (!f->ac) {
     /* fmIndexCPUBaseline.c:227-257 */
     const uint32_t *ent = f->e + (uint64_t) b * f->ew;
@@ -169,11 +175,12 @@ int32_t oracle_search(const void *image, uint64_t image_bytes, const char *queri
   ofmi_t f;
   int32_t err = parse(image, image_bytes, &f);
   uint64_t blocks = 0;
+  int oob = 0;
   if (err) return err;
   if (m == 0 || (m % f.steps) != 0) return OR_E_BADARG;
   if (nthreads > 0) omp_set_num_threads(nthreads);
 
-  #pragma omp parallel for schedule(static) reduction(+:blocks)
+  #pragma omp parallel for schedule(static) reduction(+:blocks) reduction(|:oob)
   for (int64_t q = 0; q < (int64_t) num; q++) {
     const uint8_t *p = (const uint8_t *) queries + (uint64_t) q * m;
     uint32_t L = 0, R = f.bwtsize;
@@ -181,14 +188,14 @@ int32_t oracle_search(const void *image, uint64_t image_bytes, const char *queri
       uint32_t code = 0, i;
       for (i = 0; i < f.steps; i++) code |= code_of(p[j - i]) << (2 * i);
       blocks += (L / f.chunk == R / f.chunk) ? 1 : 2;
-      L = lf_step(&f, L, code);
-      R = lf_step(&f, R, code);
+      L = lf_step(&f, L, code, &oob);
+      R = lf_step(&f, R, code, &oob);
     }
     results[2 * q] = L;
     results[2 * q + 1] = R;
   }
   if (blocks_out) *blocks_out = blocks;
-  return OR_OK;
+  return oob ? OR_E_UNDEFINED : OR_OK;
 }
 
 /* Header fields for the Python side: out[0..5] = tag, steps, bwtsize,

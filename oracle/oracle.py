@@ -76,6 +76,9 @@ def search(image, queries: np.ndarray, nthreads: int = 0):
     blocks = ctypes.c_uint64(0)
     err = lib().oracle_search(img.ctypes.data, img.nbytes, q.ctypes.data, n, m,
                               res.ctypes.data, int(nthreads), ctypes.byref(blocks))
+    if err == 98:
+        raise ValueError("oracle_search: a step reads past the index, where the reference's result "
+                         "is undefined (SURVEY B5); compare with brute-force suffix ranks instead")
     if err:
         raise ValueError(f"oracle_search failed (error {err})")
     return res, int(blocks.value)

@@ -65,3 +65,25 @@ def test_oracle_rejects_bad_input(oracle_mod):
         oracle_mod.search(img, np.zeros((3, 5), dtype=np.uint8))   # m % K != 0
     with pytest.raises(ValueError):
         oracle_mod.search(img[:30], np.zeros((3, 4), dtype=np.uint8))
+
+
+def test_oracle_refuses_reads_past_the_index(kfmi_mod, oracle_mod):
+    """(n+1) % d == 0: the first step's R lies in block nentries, which the
+    reference reads past its file.  The restatement refuses
+    instead of reading past its image; the same reads one entry further
+    (padding with the end counters, tests/test_alphabet.py padded_image) and
+    every text length off the boundary are answered."""
+    rng = np.random.default_rng(5)
+    for n, d in ((63, 64), (959, 32), (1023, 64), (191, 192)):
+        text = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=n).tobytes()
+        for k in (1, 2):
+            idx = kfmi_mod.Index.build(text, k=k, d=d)
+            q = np.frombuffer(text[:4 * k], np.uint8).reshape(1, -1).copy()
+            with pytest.raises(ValueError, match="past the index"):
+                oracle_mod.search(idx.image(), q)
+            idx.close()
+        text1 = text + b"A"
+        idx = kfmi_mod.Index.build(text1, k=2, d=d)
+        want = util.BruteForce(text1.decode()).interval(text1[:8])
+        assert tuple(oracle_mod.search(idx.image(), np.frombuffer(text1[:8], np.uint8).reshape(1, -1))[0]) == want
+        idx.close()
