@@ -213,6 +213,10 @@ int32_t kfmi_index_header(void *index, uint32_t *out14);
 /* Layout transforms (transformIndexBitmaps.c:269-295, transformIndexAlternateCounters.c:387-479). */
 int32_t kfmi_transform_interleave(void *index100, void **index101);
 int32_t kfmi_transform_ac(void *index100, void **index200, void **index201);
+/* The inverse of kfmi_transform_ac: a tag-200/201 (AltCounters) index back to
+ * the tag-100 file it came from, byte for byte (no reference counterpart; the
+ * AltCounters-semantics MID128 backends take AltCounters files through it). */
+int32_t kfmi_transform_plain(void *index_ac, void **index100);
 
 /* Queries/results handles over caller memory-resident data (the FFI form of
  * loadQueries/initResults).  `ascii` is num*size bytes, query q at q*size. */

@@ -656,8 +656,9 @@ static bool end_counters(const kfmi_fmi_t* f, uint32_t* out)
 }
 
 /* Host image of the entries for a layout, converting tags as needed.
- * INTER/PACKED need plain counters (tag 100/101); AC needs tag 201 (a
- * tag-100/101 input goes through the tfmiAC transform first). */
+ * INTER/PACKED/MID/GRP need plain counters (tag 100/101); MIDAC takes those or
+ * an AltCounters file (tag 200/201, turned back into its tag-100 file); AC
+ * needs tag 201 (a tag-100/101 input goes through the tfmiAC transform first). */
 static int32_t host_entries_for(const kfmi_fmi_t* f, int lay, kfmi_fmi_t** owned, const kfmi_fmi_t** use)
 {
   *owned = nullptr;
@@ -672,6 +673,15 @@ static int32_t host_entries_for(const kfmi_fmi_t* f, int lay, kfmi_fmi_t** owned
       return KFMI_SUCCESS;
     }
     if (f->tag == 101 || f->tag == 100) return KFMI_SUCCESS;
+    if (lay == LAY_MIDAC) {
+      /* AltCounters semantics from an AltCounters file (the reference's -AC
+       * searchers' input): its tag-100 file back (kfmi_transform_plain), whose
+       * MID128 lines and AC tail the layout is built from */
+      int32_t e = kfmi_transform_plain((void*) f, (void**) owned);
+      if (e) return e;
+      *use = *owned;
+      return KFMI_SUCCESS;
+    }
     return KFMI_INDEX_VER_INTERLEAVE;   /* an AC file cannot feed a plain-counter backend */
   }
   /* AC, AC128 */

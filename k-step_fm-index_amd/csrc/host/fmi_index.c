@@ -444,3 +444,62 @@ int32_t kfmi_transform_ac(void *index100, void **index200, void **index201)
   if (index201) *index201 = g[1]; else freeIndex((void **) &g[1]);
   return KFMI_SUCCESS;
 }
+
+/* tag 200 / 201 -> 100: kfmi_transform_ac undone, so that an AltCounters file
+ * (the input of the reference's -AC searchers) feeds the layouts built from
+ * plain counters.  Entry i keeps cnt_i of its parity's half; the other half
+ * is the next entry's (cnt_{i+1}) less block i's rows of each code -- every
+ * row read from the planes, a '$' row once however many D_s share it, as the
+ * plain counters exclude it -- and, for the last real entry E-1, the
+ * sentinel's less exactly what the transform added to it (its first
+ * (n+1) mod d rows from the planes, the padding rows as code 0).  Byte-equal
+ * to the tag-100 file the transform was run on (tests/test_host.py). */
+int32_t kfmi_transform_plain(void *index_ac, void **index100)
+{
+  kfmi_fmi_t *f = (kfmi_fmi_t *) index_ac, *g;
+  uint32_t nb, K, nc, half, i, s, t, w, c, nbw, last, rem, j, k;
+  int32_t err;
+  if (!f || !index100 || (f->tag != 200 && f->tag != 201)) return KFMI_INDEX_VER_BASELINE_AC;
+  if (f->nentries < 2) return KFMI_E_READING_FMI;
+  if ((err = kfmi_host_entries(f)) != KFMI_SUCCESS) return err;
+  nb = f->nbitmaps; K = f->steps; nc = 1u << (2 * K); half = nc / 2; nbw = 2 * nb * K;
+  if (f->ncounters != half) return KFMI_E_READING_FMI;
+  last = f->nentries - 1;      /* the sentinel */
+  rem = f->bwtsize % f->chunk;
+  err = kfmi_index_alloc(100, K, f->bwtsize, last, f->chunk, f->dollarPositionBWT, f->dollarBaseBWT, &g);
+  if (err) return err;
+  for (i = 0; i < last; i++) {   /* planes and the stored half */
+    const uint32_t *src = f->h_index + (uint64_t) i * f->entry_words;
+    uint32_t *dst = g->h_index + (uint64_t) i * g->entry_words;
+    for (w = 0; w < nb; w++)
+      for (s = 0; s < K; s++)
+        for (t = 0; t < 2; t++)
+          dst[kfmi_plane_index(100, K, nb, s, t, w)] = src[half + kfmi_plane_index(f->tag, K, nb, s, t, w)];
+    for (c = 0; c < half; c++) dst[nbw + (i & 1u) * half + c] = src[c];
+  }
+  for (i = 0; i < last; i++) {   /* the other half, from entry i+1 (or the sentinel) */
+    const uint32_t off = ((i + 1) & 1u) * half;
+    const uint32_t *nxt = f->h_index + (uint64_t) (i + 1) * f->entry_words;
+    uint32_t *dst = g->h_index + (uint64_t) i * g->entry_words;
+    for (c = 0; c < half; c++) {
+      const uint32_t code = off + c;
+      uint32_t sub;
+      if (i + 1 < last) {
+        sub = count_entry100(g, i, code, (int32_t) f->chunk);
+        for (j = 0; j < K; j++) {   /* '$' rows of block i with this stored code, each row once */
+          const uint32_t p = f->dollarPositionBWT[j];
+          int seen = 0;
+          for (k = 0; k < j; k++) seen |= f->dollarPositionBWT[k] == p;
+          if (!seen && p / f->chunk == i && count_entry100(g, i, code, (int32_t) (p % f->chunk) + 1) !=
+                                                   count_entry100(g, i, code, (int32_t) (p % f->chunk)))
+            sub--;
+        }
+      } else {
+        sub = (code == 0 ? f->chunk - rem : 0u) + (rem ? count_entry100(g, f->bwtsize / f->chunk, code, (int32_t) rem) : 0u);
+      }
+      dst[nbw + code] = nxt[c] - sub;
+    }
+  }
+  *index100 = g;
+  return KFMI_SUCCESS;
+}

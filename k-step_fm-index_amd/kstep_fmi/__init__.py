@@ -91,6 +91,7 @@ def load() -> ctypes.CDLL:
         "kfmi_index_header": (i32, [vp, vp]),
         "kfmi_transform_interleave": (i32, [vp, pvp]),
         "kfmi_transform_ac": (i32, [vp, pvp, pvp]),
+        "kfmi_transform_plain": (i32, [vp, pvp]),
         "kfmi_queries_from_buffer": (i32, [vp, u64, u32, pvp]),
         "kfmi_load_queries_gpu": (i32, [ctypes.c_char_p, u32, u64, pvp]),
         "kfmi_results_alloc": (i32, [u64, pvp]),
@@ -322,6 +323,12 @@ class Index(_Handle):
         a, b = ctypes.c_void_p(), ctypes.c_void_p()
         _check(load().kfmi_transform_ac(self._p, ctypes.byref(a), ctypes.byref(b)), "transform_ac")
         return Index(a.value), Index(b.value)
+
+    def plain(self) -> "Index":
+        """The tag-100 index an AltCounters (tag 200/201) index was transformed from."""
+        p = ctypes.c_void_p()
+        _check(load().kfmi_transform_plain(self._p, ctypes.byref(p)), "transform_plain")
+        return Index(p.value)
 
     def device_bytes(self) -> int:
         return int(load().kfmi_device_index_bytes(self._p))
