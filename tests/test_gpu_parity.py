@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 
 PLAIN = ("task", "coop", "task-packed", "coop-packed", "task-mid", "coop-mid")
 ALT = ("task-ac", "coop-ac", "task-ac128", "coop-ac128", "task-ac-mid", "coop-ac-mid")
-ACMID = ("task-ac-mid", "coop-ac-mid")     # AltCounters semantics on MID128 lines: built from tag 100/101
+ACMID = ("task-ac-mid", "coop-ac-mid")     # AltCounters semantics on MID128 lines: from tag 100/101 (or 200/201, test_ac_inverse.py)
 
 
 def coop_supported(backend, k, d):
