@@ -308,8 +308,16 @@ __global__ __launch_bounds__(256) void ftab_build_kernel(IdxArgs ix, uint32_t fs
       const uint32_t c = (uint32_t) (v >> (2 * G::K * t)) & (uint32_t) (G::NC - 1);
       uint32_t sx[2 * G::K];
       plane_xor<G::K>(c, sx);
-      L = lf_stream<G>(ix, L, c, sx);
-      R = lf_stream<G>(ix, R, c, sx);
+      if constexpr (G::SMALL) {   /* the task kernels' own step (fetch_block, lf_from_block) */
+        Blk<G> kl, kr;
+        fetch_block<G>(ix, L / (uint32_t) G::D, c, kl);
+        fetch_block<G>(ix, R / (uint32_t) G::D, c, kr);
+        L = lf_from_block<G>(ix, kl, L, c, sx);
+        R = lf_from_block<G>(ix, kr, R, c, sx);
+      } else {
+        L = lf_stream<G>(ix, L, c, sx);
+        R = lf_stream<G>(ix, R, c, sx);
+      }
     }
     out[v] = make_uint2(L, R);
   }

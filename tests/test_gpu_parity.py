@@ -366,3 +366,35 @@ def test_split_gathers_equal_oracle(gpu, oracle_mod, random_index, backend, spli
             got = gpu.search_array(idx, q, backend)
             monkeypatch.delenv("KFMI_FTAB")
             assert np.array_equal(got, want), (backend, k, d, "ftab")
+
+
+@pytest.mark.parametrize("backend,k,d,bases", [("task-ac", 1, 64, 12), ("task-ac", 2, 64, 12), ("task", 1, 32, 10),
+                                               ("task", 1, 64, 10), ("task-mid", 2, 64, 10), ("task-ac128", 1, 64, 10),
+                                               ("task-packed", 2, 64, 10), ("coop-ac-mid", 1, 64, 10),
+                                               ("task", 2, 192, 8)])
+def test_ftab_table_every_entry(gpu, random_index, backend, k, d, bases):
+    """Every entry of a freshly built jump-start table, three builds: the
+    bases-long read of each code searched with the table (one lookup, no step)
+    equals the search without it.  Round 5 found the table of task-ac at K = 1,
+    d = 64 wrong in ~40 of 4^12 entries per build, different entries each time,
+    while built with its own per-end step (lf_stream); it is now built with the
+    task kernels' step (fetch_block + lf_from_block) and checked here entry by
+    entry."""
+    text, idxs = random_index
+    if (k, d) not in idxs:
+        idxs[(k, d)] = gpu.Index.build(text, k=k, d=d)
+    idx = idxs[(k, d)]
+    codes = np.arange(4 ** bases, dtype=np.uint32)
+    q = np.frombuffer(b"ACGT", np.uint8)[(codes[:, None] >> (2 * np.arange(bases - 1, -1, -1))[None, :]) & 3].copy()
+    gpu.set_ftab(0)
+    want = gpu.search_array(idx, q, backend)
+    try:
+        for build in range(3):
+            idx.free_gpu()
+            gpu.set_ftab(bases)
+            got = gpu.search_array(idx, q, backend)
+            gpu.set_ftab(0)
+            bad = np.flatnonzero(got != want)
+            assert bad.size == 0, (backend, k, d, bases, build, int(bad.size), int(bad[0] // 2))
+    finally:
+        gpu.set_ftab(0)
