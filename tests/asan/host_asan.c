@@ -85,6 +85,12 @@ int main(int argc, char **argv)
   snprintf(q, sizeof q, "%s/%s/k%u_d%u.200.fmi", g, cs, k, d); CHECK(same_image(t200, q), "200 bytes");
   snprintf(q, sizeof q, "%s/%s/k%u_d%u.201.fmi", g, cs, k, d); CHECK(same_image(t201, q), "201 bytes");
   CHECK(kfmi_transform_interleave(t101, &re) == KFMI_INDEX_VER_BASELINE, "transform needs tag 100");
+  /* the inverse of the AltCounters transform: both AC files back to the .fmi */
+  CHECK(kfmi_transform_plain(t200, &re) == 0 && same_image(re, p), "200 -> 100 bytes");
+  freeIndex(&re);
+  CHECK(kfmi_transform_plain(t201, &re) == 0 && same_image(re, p), "201 -> 100 bytes");
+  freeIndex(&re);
+  CHECK(kfmi_transform_plain(idx, &re) == KFMI_INDEX_VER_BASELINE_AC && re == NULL, "inverse needs tag 200/201");
 
   /* 2. save + reload round trip under the reference file names */
   snprintf(q, sizeof q, "%s/x.fmi", tmp);
