@@ -48,7 +48,7 @@ def world(kfmi_mod, oracle_mod):
     idx.close()
 
 
-@pytest.mark.parametrize("seed", [1, 2, 3])
+@pytest.mark.parametrize("seed", [1, 2, 3, 4])
 def test_thread_chaos(world, seed):
     K, idx, sa, batches = world
     errs = []
@@ -56,7 +56,7 @@ def test_thread_chaos(world, seed):
     def worker(w):
         rng = np.random.default_rng(seed * 100 + w)
         try:
-            for op in range(25):
+            for op in range(60):
                 q, want = batches[int(rng.integers(0, len(batches)))]
                 kind = rng.choice(["search", "search", "search", "ftab", "stream", "locate", "handles"])
                 b = str(rng.choice(BACKENDS))
