@@ -4,8 +4,13 @@ table itself) vs without ftab, over several fresh builds; (b) the stress
 batches with ftab 0 for task-ac."""
 import sys, time, itertools, numpy as np
 sys.path.insert(0, "tests"); sys.path.insert(0, "k-step_fm-index_amd"); sys.path.insert(0, ".")
+import os
+from pathlib import Path
 import kstep_fmi as K
+if os.environ.get("KFMI_DIAG_LIB"):   # an A/B library build (scripts/diag/oldpkg)
+    K.LIB_PATH = Path(os.environ["KFMI_DIAG_LIB"])
 from oracle import oracle
+print("library", K.LIB_PATH, flush=True)
 K.set_device(0)
 rng = np.random.default_rng(2026)
 text = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), size=3_000_001).tobytes()
