@@ -124,9 +124,11 @@ __global__ __launch_bounds__(256) void fa_rows(const uint8_t* __restrict__ raw, 
       const uint32_t ch = s < n ? raw[s] : (uint32_t) '\n';   /* past the end: the read is short */
       bool bad = ch == '\n';
       if (j == m - 1 && !bad) {   /* what follows the read: '\r'* then '\n' or the end of the file */
+        /* and the read's last byte is not one of the line's trailing '\r's
+         * (the host reader strips those first: "ACG\r" is a 3-base read) */
         uint64_t p = s + 1;
         while (p < n && raw[p] == '\r') ++p;
-        bad = !(p >= n || raw[p] == '\n');
+        bad = ch == '\r' || !(p >= n || raw[p] == '\n');
       }
       if (bad) atomicMin(first_bad, (unsigned long long) q);
       word |= ch << (8 * b);

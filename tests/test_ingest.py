@@ -171,6 +171,8 @@ def test_gpu_parse_golden_and_large(kfmi_mod, gpu_idx, tmp_path):
     (b">\n>\nACGT\n", 1, True),
     (b">a\nACGTA\n>b\nTTTT\n", 2, False),              # long line
     (b">a\nAC\rT\n", 1, True),                         # '\r' inside the read is a base, as on the host
+    (b">a\nACG\r\n>b\nTTTT\n", 2, False),             # ... but a trailing one is not: a 3-base read
+    (b">a\nACG\r\r\n", 1, False),
 ])
 def test_gpu_parse_edge_cases_match_host(kfmi_mod, gpu_idx, tmp_path, body, n, ok):
     K = kfmi_mod
