@@ -412,19 +412,22 @@ __device__ __forceinline__ uint32_t load_counter(const IdxArgs& ix, const Where<
   }
 }
 
-// AltCounters semantics past the last real block: the searcher counts back
-// from the tfmiAC sentinel, whose counters include the '$' rows of block E-1
-// and the padding, so a step can land up to K rows past n+1; there, and when
-// (n+1) % d == 0, the reference reads past its own file and its
-// result is undefined -- a wrapped value would send the next load out of the
-// table.  Every AltCounters-semantics step is therefore capped at n+d rows
-// (bwtsize + d - 1), which no defined result reaches (they stay within n+1+K)
-// and which keeps the block index at most E, the sentinel, even when
-// (n+1) % d == 0: inside every layout's padding.
+// AltCounters semantics past the last real block: the tfmiAC file ends with a
+// sentinel entry S = ceil((n+1)/d) whose rows read as code 0, so on a text
+// that ends in a run of A a step's result drifts past n+1 -- by up to K rows a
+// step (a homopolymer of A walks R = n+1, n+3, ... at K=2) -- and stays
+// defined while the step reads inside the file: block S counted forward, or
+// any block below S.  Results reach (S+1)*d + K at most there.  Past that the
+// reference reads past its own file (also B5) and its result is undefined; a
+// wrapped value would send the next load out of the table.  Every
+// AltCounters-semantics step is therefore capped at (S+2)*d - 1, which keeps
+// every defined result and keeps the block index at most S+1, whose planes
+// and counters every layout holds as zero padding (LAY_AC: entries S+1, S+2;
+// LAY_AC128: line S+1; LAY_MIDAC: the MID padding line and ac_tail row 2).
 template <class G>
 __device__ __forceinline__ uint32_t ac_clamp(const IdxArgs& ix, uint32_t v)
 {
-  const uint32_t cap = ix.bwtsize + (uint32_t) G::D - 1u;
+  const uint32_t cap = ((ix.bwtsize + (uint32_t) G::D - 1u) / (uint32_t) G::D + 2u) * (uint32_t) G::D - 1u;
   return v > cap ? cap : v;
 }
 

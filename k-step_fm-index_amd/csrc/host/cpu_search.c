@@ -24,8 +24,9 @@
  * once) and rows that read as code 0 -- on a 'ref'-mode index
  * whose walk is not a permutation a step can land past n+1
  * (tests/test_alphabet.py dup_dollar_last_block_indexes) -- and the AltCounters step
- * reads zero counters past the sentinel and is capped at n + d rows, as the
- * GPU's AltCounters backends do.  Reads with m % K != 0 take
+ * reads zero planes and counters past the sentinel S and is capped at
+ * (S+2)*d - 1 rows, as the GPU's AltCounters backends do (kfmi_device.h
+ * ac_clamp).  Reads with m % K != 0 take
  * their last m % K bases from a remainder table (the true suffix-array
  * interval, as every plain GPU backend); the AltCounters tags
  * reject them (kfmi_last_error 33), the reference reads query[-1] (B6).
@@ -148,9 +149,12 @@ CS_INLINE uint32_t cs_lf(const cs_idx_t *ix, uint32_t K, uint32_t NB, int inter,
   } else {
     const uint32_t e = cs_ac_e(K, b, c), half = (1u << (2u * K)) >> 1;
     const uint32_t cnt = b + e < ix->nent ? cs_entry(ix, b + e)[ix->cnt_off + (c & (half - 1u))] : 0u;
-    const uint32_t cap = ix->bwtsize + d - 1u;
+    const uint32_t cap = ((ix->bwtsize + d - 1u) / d + 2u) * d - 1u;   /* kfmi_device.h ac_clamp */
     uint32_t v;
-    pop = cs_count(K, NB, inter, cs_entry(ix, b) + ix->pl_off, o, c, (int) e);
+    if (b < ix->nent)
+      pop = cs_count(K, NB, inter, cs_entry(ix, b) + ix->pl_off, o, c, (int) e);
+    else   /* block S+1, past the sentinel: zero planes, rows of code 0 (the GPU layouts' padding) */
+      pop = c == 0 ? (e ? d - o : o) : 0u;
     for (s = 0; s < K; ++s)
       if (ix->dblk[s] == b && ix->dbase[s] == c)
         corr += e ? (X <= ix->dpos[s]) : (X > ix->dpos[s]);

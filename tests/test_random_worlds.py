@@ -15,9 +15,9 @@ index and this build reads the padding entry's end counters.
 The AltCounters searchers (fmIndexCPUBaseline-AltCounters.c:145-310) differ
 from the true rank past the last real block (their sentinel counts the '$'
 rows as stored codes): they are checked against the AltCounters restatement
-on the transformed index where the reference's result is defined
-((n+1) % d not in {0} and < d - K, as tests/test_gpu_parity.py
-test_ac_tail_blocks), else against task-ac and kept in bounds.  A geometry a
+on the transformed index where the reference's result is defined (the
+restatement refuses a search that reads past the file), else against the
+host search and kept below the cap (tests/test_ac_drift.py).  A geometry a
 backend does not take must be refused with code 33, never answered.
 The host search (searchIndexCPU) runs in the CPU suite; the GPU
 backends in the GPU suite."""
@@ -95,6 +95,24 @@ def world(i):
     return n, k, d, m, t.tobytes(), q, want
 
 
+def _ac_cap(n, d):
+    """The AltCounters step cap, (S+2)*d - 1 rows past the sentinel S
+    (kfmi_device.h ac_clamp; tests/test_ac_drift.py)."""
+    return ((n + 1 + d - 1) // d + 2) * d - 1
+
+
+def _ac_want(K, oracle_mod, acs, q, n, d):
+    """The AltCounters restatement on the tag-200 file where the reference is
+    defined; where a step reads past its file, the host search (every GPU
+    backend must agree with it there), kept below the cap."""
+    try:
+        return oracle_mod.search(acs[0].image(), q)[0]
+    except ValueError:
+        got = K.search_cpu_array(acs[0], q, 2)
+        assert q.shape[0] == 0 or int(got.max()) <= _ac_cap(n, d)
+        return got
+
+
 @pytest.mark.parametrize("i", range(WORLDS))
 def test_random_world_host_search(kfmi_mod, i):
     """searchIndexCPU (the library's host search, csrc/host/cpu_search.c) on
@@ -112,6 +130,27 @@ def test_random_world_host_search(kfmi_mod, i):
         idx.close()
 
 
+@pytest.mark.parametrize("i", range(WORLDS))
+def test_random_world_host_search_ac(kfmi_mod, oracle_mod, i):
+    """searchIndexCPU on the world's AltCounters files (tags 200, 201) against
+    the AltCounters restatement wherever the reference is defined."""
+    K = kfmi_mod
+    n, k, d, m, text, q, want = world(i)
+    if k > 2 or m % k:
+        pytest.skip("AltCounters files exist for K = 1, 2 and take m % K == 0 only")
+    idx = K.Index.build(text, k=k, d=d)
+    acs = idx.alt_counters()
+    try:
+        w = _ac_want(K, oracle_mod, acs, q, n, d)
+        for a in acs:
+            got = K.search_cpu_array(a, q, 2)
+            bad = np.flatnonzero(got != w)
+            assert bad.size == 0, dict(world=i, n=n, k=k, d=d, m=m, tag=a.header()["tag"], first=int(bad[0]))
+    finally:
+        for x in (idx,) + tuple(acs):
+            x.close()
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("i", range(WORLDS))
 def test_random_world_gpu(kfmi_mod, oracle_mod, i):
@@ -121,13 +160,11 @@ def test_random_world_gpu(kfmi_mod, oracle_mod, i):
     K.set_device(0)
     n, k, d, m, text, q, want = world(i)
     idx = K.Index.build(text, k=k, d=d)
-    r = (n + 1) % d
-    ac_defined = r != 0 and r < d - k
     acs = ()
     want_ac = None
-    if k <= 2 and m % k == 0 and ac_defined:
+    if k <= 2 and m % k == 0:
         acs = idx.alt_counters()   # tags 200 and 201
-        want_ac = oracle_mod.search(acs[0].image(), q)[0]
+        want_ac = _ac_want(K, oracle_mod, acs, q, n, d)
     try:
         order = ("task-ac",) + tuple(b for b in PLAIN + ALT + GRP if b != "task-ac")
         for b in order:
@@ -140,9 +177,6 @@ def test_random_world_gpu(kfmi_mod, oracle_mod, i):
                 continue
             got = K.search_array(idx, q, b)
             if b in ALT:
-                if want_ac is None:            # the reference's result is undefined: agree, stay in bounds
-                    want_ac = got
-                    assert q.shape[0] == 0 or int(got.max()) <= n + d, (i, b)
                 w = want_ac
             else:
                 w = want
