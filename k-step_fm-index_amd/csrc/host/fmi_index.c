@@ -42,6 +42,22 @@ static int valid_geometry(uint32_t tag, uint32_t steps, uint32_t chunk, uint32_t
   }
 }
 
+/* A header the reference's tools could have written: nentries = ceil(bwtsize /
+ * chunk) (genFMindex.c:477), one more for the AltCounters tags' sentinel
+ * (transformIndexAlternateCounters.c:138), every '$' row inside [0, bwtsize)
+ * and every '$' code a K-mer code.  The reference's loaders take any header and
+ * read past their buffers on a damaged one; here it is KFMI_E_READING_FMI. */
+static int consistent_header(const uint32_t *h)
+{
+  const uint32_t tag = h[0], steps = h[1], bwtsize = h[2], nentries = h[4], chunk = h[5];
+  const uint64_t want = ((uint64_t) bwtsize + chunk - 1) / chunk + (tag >= 200 ? 1u : 0u);
+  uint32_t s;
+  if (bwtsize < 2 || nentries != want) return 0;
+  for (s = 0; s < steps; s++)
+    if (h[6 + s] >= bwtsize || h[6 + steps + s] >= (1u << (2 * steps))) return 0;
+  return 1;
+}
+
 int32_t kfmi_index_alloc(uint32_t tag, uint32_t steps, uint32_t bwtsize, uint32_t nentries,
                          uint32_t chunk, const uint32_t *dpos, const uint32_t *dbase,
                          kfmi_fmi_t **out)
@@ -114,6 +130,7 @@ static int32_t from_image(const uint8_t *img, uint64_t bytes, uint32_t required_
   if (required_tag && tag != required_tag) return (int32_t) required_tag;
   if (!valid_geometry(tag, steps, chunk, ncounters)) return KFMI_E_READING_FMI;
   hb = 24 + 8 * steps;
+  if (bytes < hb || !consistent_header(h)) return KFMI_E_READING_FMI;
   ew = kfmi_entry_words(tag, steps, chunk);
   if (bytes < hb + 4ull * ew * nentries) return KFMI_E_READING_FMI;
   err = kfmi_index_alloc(tag, steps, h[2], nentries, chunk, h + 6, h + 6 + steps, &f);
@@ -141,7 +158,10 @@ static int32_t load_file(const char *fn, uint32_t required_tag, void **index)
   if (required_tag && hdr[0] != required_tag) { fclose(fp); return (int32_t) required_tag; }
   steps = hdr[1];
   if (!valid_geometry(hdr[0], steps, hdr[5], hdr[3])) { fclose(fp); return KFMI_E_READING_FMI; }
-  if (fread(hdr + 6, 4, 2 * steps, fp) != 2 * steps) { fclose(fp); return KFMI_E_READING_FMI; }
+  if (fread(hdr + 6, 4, 2 * steps, fp) != 2 * steps || !consistent_header(hdr)) {
+    fclose(fp);
+    return KFMI_E_READING_FMI;
+  }
   err = kfmi_index_alloc(hdr[0], steps, hdr[2], hdr[4], hdr[5], hdr + 6, hdr + 6 + steps, &f);
   if (err) { fclose(fp); return err; }
   hb = f->header_bytes;

@@ -237,6 +237,71 @@ int main(int argc, char **argv)
     kfmi_big_free(NULL);
   }
 
+  /* 9. damaged headers: every tag's image with one header word replaced (the
+   *    size fields, a '$' row or its code; the body cut to what the header then
+   *    asks for) either fails to load or loads, searches and transforms inside
+   *    its own buffers -- ASan reports any read or write outside them */
+  {
+    void *qs = NULL;
+    uint32_t lcg = 12345u + k * 7u + d;
+    snprintf(q, sizeof q, "%s/%s/q%u.qry", g, cs, m);
+    CHECK(loadQueries(q, m, num < 64 ? num : 64, &qs) == 0, "fuzz queries");
+    for (tag = 100; tag <= 201; tag += (tag == 101 ? 99 : 1)) {
+      size_t len = 0;
+      unsigned char *img;
+      uint32_t trial, loaded = 0;
+      snprintf(p, sizeof p, "%s/%s/k%u_d%u.%u.fmi", g, cs, k, d, tag);
+      img = slurp(p, &len);
+      CHECK(img != NULL, "fuzz image %u", tag);
+      if (!img) continue;
+      for (trial = 0; trial < 600; trial++) {
+        uint32_t h[6 + 2 * KFMI_MAX_STEPS], word, val, steps = ((uint32_t *) img)[1];
+        unsigned char *b = (unsigned char *) malloc(len);
+        uint64_t blen = len, need;
+        void *x = NULL, *y = NULL, *z = NULL, *rs = NULL;
+        memcpy(b, img, len);
+        memcpy(h, img, 4 * (6 + 2 * steps));
+        lcg = lcg * 1664525u + 1013904223u;
+        word = (lcg >> 8) % 5;   /* bwtsize, nentries, a '$' row, a '$' code, two fields */
+        lcg = lcg * 1664525u + 1013904223u;
+        switch ((lcg >> 4) % 6) {
+          case 0: val = 0; break;
+          case 1: val = 1; break;
+          case 2: val = 0xFFFFFFFFu - (lcg >> 28); break;
+          case 3: val = h[2] + (lcg >> 20) % (3 * d) - (3 * d) / 2; break;
+          case 4: val = h[4] + (lcg >> 24) % 5 - 2; break;
+          default: val = lcg >> 7; break;
+        }
+        if (word == 0) h[2] = val;
+        else if (word == 1) h[4] = val;
+        else if (word == 2) h[6 + (lcg >> 3) % steps] = val;
+        else if (word == 3) h[6 + steps + (lcg >> 3) % steps] = val % 7u;
+        else { h[2] = val; h[6 + (lcg >> 3) % steps] = val - (lcg >> 29); }
+        memcpy(b, h, 4 * (6 + 2 * steps));
+        need = 4ull * (6 + 2 * steps) + 4ull * kfmi_entry_words(tag, steps, d) * h[4];
+        if (need < blen) blen = need;   /* a smaller nentries: the file ends there */
+        if (kfmi_index_from_image(b, blen, &x) == 0) {
+          loaded++;
+          if (initResults(num < 64 ? num : 64, &rs) == 0) {
+            (void) kfmi_search_cpu(x, qs, rs, 2);
+            freeResults(&rs);
+          }
+          if (tag == 100) {
+            if (kfmi_transform_interleave(x, &y) == 0) freeIndex(&y);
+            if (kfmi_transform_ac(x, &y, &z) == 0) { freeIndex(&y); freeIndex(&z); }
+          } else if (tag >= 200 && kfmi_transform_plain(x, &y) == 0) {
+            freeIndex(&y);
+          }
+          freeIndex(&x);
+        }
+        free(b);
+      }
+      CHECK(loaded > 0, "fuzz: some damaged %u headers still load", tag);
+      free(img);
+    }
+    freeQueries(&qs);
+  }
+
   freeIndex(&idx); freeIndex(&t101); freeIndex(&t200); freeIndex(&t201);
   printf("%s %d checks, %d failures\n", failures ? "FAILED" : "OK", checks, failures);
   return failures ? 1 : 0;
