@@ -132,12 +132,16 @@ int32_t saveRef(const char *fn, void *reference)
   return KFMI_SUCCESS;
 }
 
-/* common.c:313-322 */
+/* common.c:313-322 frees the text and keeps the handle (its ref_t leaks); here
+ * both are freed and the handle cleared */
 int32_t freeReference(void **reference, void **index)
 {
   kfmi_ref_t *ref = reference ? (kfmi_ref_t *) *reference : NULL;
   (void) index;
-  if (ref && ref->h_reference) { free(ref->h_reference); ref->h_reference = NULL; }
+  if (!ref) return KFMI_SUCCESS;
+  free(ref->h_reference);
+  free(ref);
+  *reference = NULL;
   return KFMI_SUCCESS;
 }
 

@@ -302,6 +302,37 @@ int main(int argc, char **argv)
     freeQueries(&qs);
   }
 
+  /* 10. damaged text files: random bytes drawn mostly from ">\n\rACGTN" (and
+   *     any byte now and then), 0-5000 of them, through loadQueries, loadRef
+   *     and loadResults with random sizes -- each either fails or returns a
+   *     buffer of the size asked, never reading or writing outside */
+  {
+    uint32_t lcg = 777u + k + d, trial, okq = 0, okr = 0;
+    static const char alpha[] = ">\n\r\nACGTNacgt 0123456789";
+    snprintf(q, sizeof q, "%s/junk.txt", tmp);
+    for (trial = 0; trial < 400; trial++) {
+      uint32_t len, i, mq, nq, nr;
+      FILE *fp = fopen(q, "wb");
+      void *qs = NULL, *ref = NULL, *rs = NULL;
+      lcg = lcg * 1664525u + 1013904223u;
+      len = (lcg >> 8) % 5001u;
+      for (i = 0; i < len; i++) {
+        lcg = lcg * 1664525u + 1013904223u;
+        fputc((lcg >> 24) < 8 ? (int) (lcg >> 16) & 0xff : alpha[(lcg >> 16) % (sizeof alpha - 1)], fp);
+      }
+      fclose(fp);
+      lcg = lcg * 1664525u + 1013904223u;
+      mq = 1 + (lcg >> 8) % 40u;
+      nq = 1 + (lcg >> 16) % 50u;
+      nr = 1 + (lcg >> 4) % 3000u;
+      if (loadQueries(q, mq, nq, &qs) == 0) { okq++; freeQueries(&qs); }
+      if (loadRef(q, nr, &ref) == 0) { okr++; freeReference(&ref, NULL); }
+      if (loadResults(q, &rs) == 0) freeResults(&rs);
+    }
+    CHECK(trial == 400, "junk files");
+    (void) okq; (void) okr;
+  }
+
   freeIndex(&idx); freeIndex(&t101); freeIndex(&t200); freeIndex(&t201);
   printf("%s %d checks, %d failures\n", failures ? "FAILED" : "OK", checks, failures);
   return failures ? 1 : 0;
