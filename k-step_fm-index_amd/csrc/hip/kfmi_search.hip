@@ -875,6 +875,10 @@ int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx, kfmi_dev_
   if (!nb_supported(f->nbitmaps)) return KFMI_E_BAD_ARGUMENT;
   const int lay = layout_of(backend);
   if (!geometry_supported(backend, f->steps, f->nbitmaps, lay)) return KFMI_E_BAD_ARGUMENT;
+  /* rows are u32 on the device: every layout's padding blocks and the
+   * AltCounters cap, (S+2)*d - 1 (ac_clamp), must stay below 2^32 -- which
+   * leaves out only the last ~3d rows of the u32 range */
+  if (((uint64_t) f->nentries + 3u) * f->chunk > 0xFFFFFFFFull) return KFMI_E_BAD_ARGUMENT;
   kfmi_fmi_t* owned = nullptr;
   const kfmi_fmi_t* src = nullptr;
   int32_t err = host_entries_for(f, lay, &owned, &src);

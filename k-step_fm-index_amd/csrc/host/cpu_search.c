@@ -149,7 +149,7 @@ CS_INLINE uint32_t cs_lf(const cs_idx_t *ix, uint32_t K, uint32_t NB, int inter,
   } else {
     const uint32_t e = cs_ac_e(K, b, c), half = (1u << (2u * K)) >> 1;
     const uint32_t cnt = b + e < ix->nent ? cs_entry(ix, b + e)[ix->cnt_off + (c & (half - 1u))] : 0u;
-    const uint32_t cap = ((ix->bwtsize + d - 1u) / d + 2u) * d - 1u;   /* kfmi_device.h ac_clamp */
+    const uint64_t cap = (((uint64_t) ix->bwtsize + d - 1u) / d + 2u) * d - 1u;   /* kfmi_device.h ac_clamp */
     uint32_t v;
     if (b < ix->nent)
       pop = cs_count(K, NB, inter, cs_entry(ix, b) + ix->pl_off, o, c, (int) e);
@@ -159,7 +159,7 @@ CS_INLINE uint32_t cs_lf(const cs_idx_t *ix, uint32_t K, uint32_t NB, int inter,
       if (ix->dblk[s] == b && ix->dbase[s] == c)
         corr += e ? (X <= ix->dpos[s]) : (X > ix->dpos[s]);
     v = e ? cnt - (pop - (uint32_t) corr) : cnt + (pop - (uint32_t) corr);
-    return v > cap ? cap : v;
+    return v > cap ? (uint32_t) cap : v;
   }
 }
 
