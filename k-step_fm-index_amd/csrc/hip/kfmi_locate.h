@@ -52,6 +52,18 @@ __device__ __forceinline__ uint32_t row_code(const IdxArgs& ix, uint32_t X)
   return c;
 }
 
+// A walk that cannot end at a suffix: its row is past n+1 (no suffix there --
+// rows an AltCounters interval can reach past the sentinel, §3) or it has taken
+// more steps than the text is long (a 'ref'-mode index whose BWT is not a
+// permutation).  Such a slot reports LOST_POS instead of walking on; on an
+// ACGT index every walk from a row below n+1 ends within n/K steps.
+constexpr uint32_t LOST_POS = 0xFFFFFFFFu;
+
+__device__ __forceinline__ bool walk_lost(const IdxArgs& ix, uint32_t r, uint32_t steps)
+{
+  return r >= ix.bwtsize || steps >= ix.bwtsize;
+}
+
 // LF_K of one row (X must not be a '$' row D_s).
 template <class G>
 __device__ __forceinline__ uint32_t lf_row(const IdxArgs& ix, uint32_t X)
@@ -134,16 +146,17 @@ __global__ __launch_bounds__(256) void locate_kernel(IdxArgs ix, const uint32_t*
   uint32_t r_next = i + stride < total ? rows[i + stride] : 0u;
   uint32_t steps = 0;
   for (;;) {   // a lane leaves once all its slots are done
-    const bool smp = (r & mask) == 0u;
+    const bool lost = walk_lost(ix, r, steps);
+    const bool smp = !lost && (r & mask) == 0u;
     int ds = -1;   /* r = D_s (SA = s): the walk cannot step past it */
 #pragma unroll
     for (int s = G::K - 1; s >= 0; --s)
       if (r == ix.dl.dpos[s]) ds = s;
     uint32_t p = 0, nr = 0;
     if (smp) p = sa[r >> rate_log2];
-    else if (ds < 0) nr = lf_row<G>(ix, r);
-    if (smp || ds >= 0) {
-      pos[i] = (smp ? p : (uint32_t) ds) + steps;
+    else if (ds < 0 && !lost) nr = lf_row<G>(ix, r);
+    if (smp || ds >= 0 || lost) {
+      pos[i] = lost ? LOST_POS : (smp ? p : (uint32_t) ds) + steps;
       i += stride;
       if (i >= total) break;
       r = r_next;
@@ -220,12 +233,13 @@ __global__ __launch_bounds__(256) void locate_coop_kernel(IdxArgs ix, const uint
   uint32_t steps = 0;
   const int g = lane / TPR, k = lane % TPR;
   while (__ballot(act)) {   // wave-uniform: until every lane of the wave has no slot left
-    const bool smp = act && (r & mask) == 0u;
+    const bool lost = act && walk_lost(ix, r, steps);
+    const bool smp = act && !lost && (r & mask) == 0u;
     int ds = -1;   /* r = D_s (SA = s): the walk cannot step past it */
 #pragma unroll
     for (int s = G::K - 1; s >= 0; --s)
       if (r == ix.dl.dpos[s]) ds = s;
-    const bool step = act && !smp && ds < 0;
+    const bool step = act && !smp && ds < 0 && !lost;
     uint32_t p = 0;
     if (smp) p = sa[r >> rate_log2];
     const uint32_t mine = step ? r / (uint32_t) (2 * G::D) : 0xFFFFFFFFu;   // this lane's MID line, or none
@@ -238,9 +252,9 @@ __global__ __launch_bounds__(256) void locate_coop_kernel(IdxArgs ix, const uint
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint32_t nr = step ? lf_row_line<G>(ix, wl + lane * LB, r) : 0u;
-    const bool fin = smp || (act && ds >= 0);
+    const bool fin = smp || (act && (ds >= 0 || lost));
     if (fin) {
-      pos[i] = (smp ? p : (uint32_t) ds) + steps;
+      pos[i] = lost ? LOST_POS : (smp ? p : (uint32_t) ds) + steps;
       i = i_n;
       r = r_n;
       act = i < total;

@@ -21,18 +21,21 @@ namespace kfmi {
 
 /* locate bookkeeping kernels (slot counts, owners, first rows); the walk itself
  * is locate_kernel in kfmi_locate.h */
-// Positions each query reports: min(R - L, max_occ) (max_occ 0 = all).  The
-// count array has num + 1 slots and the last one is 0, so the exclusive scan's
-// last element is the total.
+// Positions each query reports: min(min(R, n+1) - L, max_occ) (max_occ 0 =
+// all; rows from n+1 on hold no suffix -- an AltCounters interval can reach
+// past the sentinel, §3).  The count array has num + 1 slots and the last one
+// is 0, so the exclusive scan's last element is the total.
 static __global__ __launch_bounds__(256) void loc_count_kernel(const uint32_t* __restrict__ res, uint64_t num,
-                                                        uint32_t max_occ, uint64_t* __restrict__ cnt)
+                                                        uint32_t max_occ, uint32_t nrows,
+                                                        uint64_t* __restrict__ cnt)
 {
   const uint64_t q = (uint64_t) blockIdx.x * 256 + threadIdx.x;
   if (q > num) return;
   uint64_t c = 0;
   if (q < num) {
     const uint2 lr = *reinterpret_cast<const uint2*>(res + 2 * q);
-    c = lr.y > lr.x ? (uint64_t) (lr.y - lr.x) : 0u;
+    const uint32_t hi = lr.y < nrows ? lr.y : nrows;
+    c = hi > lr.x ? (uint64_t) (hi - lr.x) : 0u;
     if (max_occ && c > max_occ) c = max_occ;
   }
   cnt[q] = c;
@@ -139,7 +142,7 @@ static int32_t locate_on(kfmi_fmi_t* f, kfmi_dev_index* di, uint32_t* d_res, uin
   if (!ok) return done(KFMI_E_DEVICE_ALLOC);
   if (hipEventRecord(ev[0], st) != hipSuccess) return done(KFMI_E_KERNEL);
   hipLaunchKernelGGL(loc_count_kernel, dim3((uint32_t) ((num + 1 + 255) / 256)), dim3(256), 0, st, d_res, num,
-                     max_occ, d_cnt);
+                     max_occ, di->bwtsize, d_cnt);
   ok = hipGetLastError() == hipSuccess &&
        rocprim::exclusive_scan(tmp, tb, d_cnt, d_off, (uint64_t) 0, (size_t) (num + 1), rocprim::plus<uint64_t>(),
                                st) == hipSuccess &&

@@ -178,3 +178,37 @@ def test_ac_drift_gpu(kfmi_mod, oracle_mod, case):
     finally:
         for x in (idx,) + tuple(acs):
             x.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,rate", [(2, 1), (2, 8), (1, 32)])
+def test_ac_drift_locate(kfmi_mod, k, rate):
+    """Locate of AltCounters intervals that reach past n+1: rows from n+1 on
+    hold no suffix, so each query reports the rows of [L, min(R, n+1)) -- no
+    read of the sampled SA past its end, no walk from a row with no suffix
+    (kfmi_locate.h walk_lost)."""
+    K = kfmi_mod
+    if K.device_count() < 1:
+        pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
+    K.set_device(0)
+    n, d = 1001, 64
+    text = b"A" * n
+    full = K.Index.build(text, k=k, d=d, sa_rate=1)
+    sa = np.array(full.sa()[1], dtype=np.uint32)
+    full.close()
+    idx = K.Index.build(text, k=k, d=d, gpu=True, sa_rate=rate)
+    try:
+        for m in (2 * k, 64, 80):
+            q = np.full((5, m), ord("A"), np.uint8)
+            for b in ("task-ac", "task-ac-mid", "coop-ac-mid", "task-ac128"):
+                res, off, pos = K.locate_array(idx, q, b)
+                assert int(res[1]) > n + 1 or m == 2 * k, (b, m, res[:2])   # the drift reaches past n+1
+                w_pos, w_off = [], [0]
+                for j in range(q.shape[0]):
+                    lo, hi = int(res[2 * j]), min(int(res[2 * j + 1]), n + 1)
+                    w_pos.append(sa[lo:hi] if hi > lo else sa[:0])
+                    w_off.append(w_off[-1] + max(0, hi - lo))
+                assert np.array_equal(off, np.array(w_off, np.uint64)), (b, m)
+                assert np.array_equal(pos, np.concatenate(w_pos)), (b, m)
+    finally:
+        idx.close()
