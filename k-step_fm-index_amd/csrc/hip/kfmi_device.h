@@ -117,7 +117,9 @@ struct IdxArgs {
   const uint2* __restrict__ ftab;
   uint32_t ftab_steps, ftab_mask;
   // LAY_MIDAC: AltCounters counters of entries E-1, E (sentinel), E+1 (zero),
-  // NC each, and E-1 = the first block that takes the AltCounters formula
+  // NC each, and E-1 = the first block that takes the AltCounters formula;
+  // every AltCounters layout: row 3, the locate walk's correction of a step
+  // backward from the sentinel (kfmi_search.hip ac_locate_fix)
   const uint32_t* __restrict__ ac_tail;
   uint32_t ac_tail_b0;
   // reads with m % K = rem != 0: [L, R) after their last rem bases (code of

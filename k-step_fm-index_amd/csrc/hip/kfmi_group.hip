@@ -123,7 +123,7 @@ static int32_t replicate_index(const kfmi_dev_index* src, int dev, hipStream_t s
   struct Buf { uint32_t* const* from; uint32_t** to; uint64_t bytes; };
   const Buf bufs[4] = {{&src->ent, &di->ent, src->ent_bytes}, {&src->sb, &di->sb, src->sb_bytes},
                        {&src->sa, &di->sa, src->sa ? src->sa_bytes + 4 : 0},
-                       {&src->ac_tail, &di->ac_tail, src->ac_tail ? 12ull * (1u << (2 * src->K)) : 0}};
+                       {&src->ac_tail, &di->ac_tail, src->ac_tail ? 16ull * (1u << (2 * src->K)) : 0}};
   for (const Buf& b : bufs) {
     if (!*b.from || !b.bytes) continue;
     if (hipMalloc((void**) b.to, b.bytes) != hipSuccess) {

@@ -64,14 +64,25 @@ __device__ __forceinline__ bool walk_lost(const IdxArgs& ix, uint32_t r, uint32_
   return r >= ix.bwtsize || steps >= ix.bwtsize;
 }
 
-// LF_K of one row (X must not be a '$' row D_s).
+// LF_K of one row (X must not be a '$' row D_s).  On the AltCounters layouts
+// a step taken backward from the sentinel -- the last real block, the codes
+// whose counter sits in the next entry -- differs from the plain LF by a
+// constant per code (the sentinel counts that block's '$' rows as their
+// stored code, and under B5 its padding, transformIndexAlternateCounters.c:
+// 420-431, §3); a walk needs the plain LF, so it is taken off (ac_tail row 3).
 template <class G>
 __device__ __forceinline__ uint32_t lf_row(const IdxArgs& ix, uint32_t X)
 {
   const uint32_t c = row_code<G>(ix, X);
   uint32_t sx[2 * G::K];
   plane_xor<G::K>(c, sx);
-  return lf_stream<G>(ix, X, c, sx);
+  uint32_t v = lf_stream<G>(ix, X, c, sx);
+  if constexpr (G::ACRULE || G::LAY == LAY_MIDAC) {
+    const uint32_t b = X / (uint32_t) G::D;
+    if (b + 1u == (ix.bwtsize + (uint32_t) G::D - 1u) / (uint32_t) G::D && ac_rule_e<G>(b, c))
+      v -= ix.ac_tail[3u * (uint32_t) G::NC + c];
+  }
+  return v;
 }
 
 // Wave-level slot queue.  `want` lanes receive the next slots of the wave's

@@ -53,7 +53,8 @@ struct kfmi_dev_index {
   /* remainder tables: [L, R) of every r-base read suffix, r = m % K in 1..3
    * (same lifetime rule as the ftabs, same mutex) */
   uint2* rtab[4] = {};
-  uint32_t* ac_tail = nullptr; /* LAY_MIDAC: 3 x NC AltCounters counters of entries E-1, E, E+1 */
+  uint32_t* ac_tail = nullptr; /* AltCounters layouts, 4 x NC: (LAY_MIDAC) the counters of entries E-1, E,
+                                 E+1; row 3 the locate walk's sentinel correction (ac_locate_fix) */
   uint32_t ac_tail_b0 = 0xFFFFFFFFu;
 };
 

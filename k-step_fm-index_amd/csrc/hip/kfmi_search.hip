@@ -604,6 +604,57 @@ static inline const uint32_t* host_index(const kfmi_fmi_t* f)
   return __atomic_load_n(&f->h_index, __ATOMIC_ACQUIRE);
 }
 
+/* Locate walks need the plain LF.  On the AltCounters layouts a step taken
+ * backward from the sentinel -- in the last real block L, for the codes the
+ * AC rule sends to entry L+1 -- differs from it by a constant per code c: the
+ * sentinel holds cnt_L[c] plus (n+1) mod d rows of block L read from the
+ * planes ('$' rows included) plus the padding rows for code 0
+ * (kfmi_transform_ac; when (n+1) mod d == 0, B5, the transform's masked read
+ * adds no rows and the padding is a whole block), where the plain LF counts
+ * every row of block L below X and leaves each D_s out.  out[c] = that
+ * difference, which kfmi_locate.h lf_row takes off such a step. */
+static bool ac_locate_fix(const kfmi_fmi_t* f, uint32_t* out)
+{
+  const uint32_t nc = 1u << (2 * f->steps), nb = f->nbitmaps, d = f->chunk;
+  const uint32_t last = (uint32_t) (((uint64_t) f->bwtsize + d - 1) / d) - 1u, rem = f->bwtsize % d;
+  const uint32_t poff = f->tag >= 200 ? nc / 2 : 0u;   /* tag 200/201 entries: [counters | planes] */
+  std::vector<uint32_t> ent;
+  const uint32_t* e;
+  if (last >= f->nentries) return false;
+  if (const uint32_t* hi = host_index(f)) {
+    e = hi + (uint64_t) last * f->entry_words;
+  } else {   /* entries only in HBM: fetch that one */
+    ent.assign(f->entry_words, 0u);
+    DeviceGuard dg;
+    if (hipSetDevice(f->d_entries_dev) != hipSuccess ||
+        hipMemcpy(ent.data(), f->d_entries + (uint64_t) last * f->entry_words, 4ull * f->entry_words,
+                  hipMemcpyDeviceToHost) != hipSuccess)
+      return false;
+    e = ent.data();
+  }
+  for (uint32_t c = 0; c < nc; ++c) {
+    uint32_t all = 0, head = 0;   /* rows of code c in the block, in its first rem rows */
+    for (uint32_t w = 0; w < nb; ++w) {
+      uint32_t m = 0xFFFFFFFFu;
+      for (uint32_t st = 0; st < f->steps; ++st)
+        for (uint32_t t = 0; t < 2; ++t) {
+          const uint32_t pl = e[poff + kfmi_plane_index(f->tag, f->steps, nb, st, t, w)];
+          m &= ((c >> (2 * st + t)) & 1u) ? pl : ~pl;
+        }
+      int sh = (int) rem - 32 * (int) w;
+      sh = sh < 0 ? 0 : (sh > 32 ? 32 : sh);
+      all += (uint32_t) __builtin_popcount(m);
+      head += (uint32_t) __builtin_popcount(m & (uint32_t) (0xFFFFFFFF00000000ull >> sh));
+    }
+    uint32_t dollar = 0;
+    for (uint32_t st = 0; st < f->steps; ++st)
+      dollar += (f->dollarPositionBWT[st] / d == last && f->dollarBaseBWT[st] == c) ? 1u : 0u;
+    const uint32_t added = head + (c == 0 ? d - rem : 0u);   /* what the transform adds to cnt_L */
+    out[c] = added - all + dollar;
+  }
+  return true;
+}
+
 /* Counters at row n+1 (one past the last row) from a tag-100/101 index:
  * cnt_{E-1} + rows of each code in the last block, $ rows excluded -- each
  * distinct row once, as the builder's counters exclude them (a 'ref'-mode index
@@ -1011,17 +1062,6 @@ int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx, kfmi_dev_
     (void) hipFree(tmp);
     (void) hipFree(d_ext);
     if (!ok) return fail(KFMI_E_KERNEL);
-    if (lay == LAY_MIDAC) {   /* the AltCounters searcher's counters past the last real block */
-      std::vector<uint32_t> tail(3 * nc);
-      if (kfmi_ac_tail(src, tail.data(), &di->ac_tail_b0) != KFMI_SUCCESS) return fail(KFMI_E_BAD_ARGUMENT);
-      if (hipMalloc((void**) &di->ac_tail, 12ull * nc) != hipSuccess) {
-        di->ac_tail = nullptr;
-        return fail(KFMI_E_DEVICE_ALLOC);
-      }
-      if (hipMemcpyAsync(di->ac_tail, tail.data(), 12ull * nc, hipMemcpyHostToDevice, ctx->st) != hipSuccess ||
-          hipStreamSynchronize(ctx->st) != hipSuccess)
-        return fail(KFMI_E_KERNEL);
-    }
   } else {
     /* packed: build on the device from tag-101 entries (+ the padding entry) */
     const uint32_t ne = src->nentries + 1;
@@ -1057,6 +1097,22 @@ int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx, kfmi_dev_
       fprintf(stderr, "kstepfmi: packed layout delta overflow (%u) -- corrupt counters\n", over);
       return fail(KFMI_E_READING_FMI);
     }
+  }
+  if (lay == LAY_AC || lay == LAY_AC128 || lay == LAY_MIDAC) {
+    /* 4 x NC words: LAY_MIDAC's AltCounters counters of entries E-1, E, E+1
+     * (kfmi_ac_tail), and on every AltCounters layout row 3, the locate walk's
+     * correction of a backward step from the sentinel (ac_locate_fix) */
+    std::vector<uint32_t> tail(4 * nc, 0u);
+    if (lay == LAY_MIDAC && kfmi_ac_tail(src, tail.data(), &di->ac_tail_b0) != KFMI_SUCCESS)
+      return fail(KFMI_E_BAD_ARGUMENT);
+    if (!ac_locate_fix(src, tail.data() + 3 * nc)) return fail(KFMI_E_KERNEL);
+    if (hipMalloc((void**) &di->ac_tail, 16ull * nc) != hipSuccess) {
+      di->ac_tail = nullptr;
+      return fail(KFMI_E_DEVICE_ALLOC);
+    }
+    if (hipMemcpyAsync(di->ac_tail, tail.data(), 16ull * nc, hipMemcpyHostToDevice, ctx->st) != hipSuccess ||
+        hipStreamSynchronize(ctx->st) != hipSuccess)
+      return fail(KFMI_E_KERNEL);
   }
   if (owned) freeIndex((void**) &owned);
   if (f->h_sa) {

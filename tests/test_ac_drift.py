@@ -212,3 +212,51 @@ def test_ac_drift_locate(kfmi_mod, k, rate):
                 assert np.array_equal(pos, np.concatenate(w_pos)), (b, m)
     finally:
         idx.close()
+
+
+def _locate_case(name):
+    rng = np.random.default_rng(99)
+    if name == "A1023-B5":
+        return b"A" * 1023
+    if name == "T-head":   # the whole-text suffix sorts last: its '$' rows sit in the last block
+        t = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=3000)
+        t[:60] = ord("T")
+        return t.tobytes()
+    if name == "T-head-B5":
+        t = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=4095)
+        t[:60] = ord("T")
+        return t.tobytes()
+    return b"A" * 1001
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["A1023-B5", "T-head", "T-head-B5", "A1001"])
+@pytest.mark.parametrize("k", [1, 2])
+def test_locate_walks_on_altcounters_layouts(kfmi_mod, name, k):
+    """A locate walk steps with the plain LF on every layout: on the
+    AltCounters ones a step backward from the sentinel (the last real block)
+    takes off what the sentinel adds there -- the block's '$' rows, and under
+    B5 its padding (kfmi_search.hip ac_locate_fix).  Texts whose '$' rows sit in
+    the last block (a homopolymer, a text that opens with a run of T), with and
+    without (n+1) % d == 0; every row of every interval the walk can reach."""
+    K = kfmi_mod
+    if K.device_count() < 1:
+        pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
+    K.set_device(0)
+    text = _locate_case(name)
+    n, d = len(text), 64
+    t = np.frombuffer(text, np.uint8)
+    full = K.Index.build(text, k=k, d=d, sa_rate=1)
+    sa = np.array(full.sa()[1], dtype=np.uint32)
+    full.close()
+    idx = K.Index.build(text, k=k, d=d, gpu=True, sa_rate=16)
+    try:
+        st = np.arange(0, n - 4 * k + 1, 7)
+        q = np.ascontiguousarray(np.concatenate([t[st[:, None] + np.arange(2 * k)[None, :]],
+                                                 np.full((1, 2 * k), ord("T"), np.uint8)]))
+        for b in ("task-ac", "task-ac128", "task-ac-mid", "task-mid"):
+            res, off, pos = K.locate_array(idx, q, b)
+            w_pos = [sa[int(res[2 * j]):min(int(res[2 * j + 1]), n + 1)] for j in range(q.shape[0])]
+            assert np.array_equal(pos, np.concatenate(w_pos)), (name, k, b)
+    finally:
+        idx.close()
