@@ -23,6 +23,37 @@ from test_random_worlds import GRP, PLAIN, _takes  # noqa: E402
 K = D.K
 
 
+def run_world(w, gpu):
+    """[(searcher, first differing read or None)] for world w."""
+    rng = np.random.default_rng(860_000 + w)
+    k = int(rng.choice([1, 2, 2, 3, 4]))
+    d = 64 if k > 2 else int(rng.choice([32, 64, 128, 192]))
+    n = int(rng.integers(2 * k + 2, 40)) if rng.random() < 0.25 else int(rng.integers(40, 4000))
+    t, kind = D.text(rng, n)
+    m = int(rng.integers(1, 120))
+    q = D.reads(rng, t, m, int(rng.integers(1, 200)))
+    bf = util.BruteForce(t.tobytes().decode())
+    want = np.array([x for r in q for x in bf.interval(r.tobytes())], dtype=np.uint32)
+    idx = K.Index.build(t.tobytes(), k=k, d=d, gpu=gpu and bool(rng.integers(0, 2)))
+    got = {"host": K.search_cpu_array(idx, q, 2)}
+    if gpu:
+        bases = k * int(rng.integers(0, 8 // k + 1))
+        K.set_ftab(bases if m % k == 0 else 0)
+        try:
+            for b in PLAIN + GRP:
+                if _takes(b, k, d, n):
+                    got[b] = K.search_array(idx, q, b)
+        finally:
+            K.set_ftab(0)
+    idx.close()
+    out = []
+    for b, g in got.items():
+        diff = np.flatnonzero(g != want)
+        out.append((b, None if diff.size == 0 else
+                    f"K={k} d={d} n={n} kind={kind} m={m} read {int(diff[0]) // 2}"))
+    return out
+
+
 def main():
     limit = float(sys.argv[1]) if len(sys.argv) > 1 else 120
     gpu = "--gpu" in sys.argv
@@ -31,34 +62,11 @@ def main():
     t0 = time.time()
     w = calls = bad = 0
     while time.time() - t0 < limit:
-        rng = np.random.default_rng(860_000 + w)
-        k = int(rng.choice([1, 2, 2, 3, 4]))
-        d = 64 if k > 2 else int(rng.choice([32, 64, 128, 192]))
-        n = int(rng.integers(2 * k + 2, 40)) if rng.random() < 0.25 else int(rng.integers(40, 4000))
-        t, kind = D.text(rng, n)
-        m = int(rng.integers(1, 120))
-        q = D.reads(rng, t, m, int(rng.integers(1, 200)))
-        bf = util.BruteForce(t.tobytes().decode())
-        want = np.array([x for r in q for x in bf.interval(r.tobytes())], dtype=np.uint32)
-        idx = K.Index.build(t.tobytes(), k=k, d=d, gpu=gpu and bool(rng.integers(0, 2)))
-        got = {"host": K.search_cpu_array(idx, q, 2)}
-        if gpu:
-            bases = k * int(rng.integers(0, 8 // k + 1))
-            K.set_ftab(bases if m % k == 0 else 0)
-            try:
-                for b in PLAIN + GRP:
-                    if _takes(b, k, d, n):
-                        got[b] = K.search_array(idx, q, b)
-            finally:
-                K.set_ftab(0)
-        for b, g in got.items():
+        for b, what in run_world(w, gpu):
             calls += 1
-            if not np.array_equal(g, want):
+            if what:
                 bad += 1
-                j = int(np.flatnonzero(g != want)[0]) // 2
-                print(f"MISMATCH world {w}: K={k} d={d} n={n} kind={kind} m={m} {b}: read {j} "
-                      f"got {g[2 * j:2 * j + 2]} want {want[2 * j:2 * j + 2]}", flush=True)
-        idx.close()
+                print(f"MISMATCH world {w}: {b}: {what}", flush=True)
         w += 1
         if w % 50 == 0:
             print(f"{w} worlds, {calls} searches, {bad} bad, {time.time() - t0:.0f}s", flush=True)
