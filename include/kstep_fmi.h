@@ -362,8 +362,11 @@ int32_t kfmi_load_sa(const char *fn, void *index);
  * query (the first rows; 0 = all) -- from results still on the device (after
  * searchIndexGPU / kfmi_search) and an index with samples on the device.
  * Query q's positions are positions[offsets[q] .. offsets[q+1]), in row order
- * (positions[offsets[q] + j] = SA[L_q + j]).  kfmi_last_timing: total, scan,
- * locate kernel (ms).  Errors: 34 before transfer/search, 33 without samples. */
+ * (positions[offsets[q] + j] = SA[L_q + j]).  Rows from n+1 on hold no
+ * suffix and are not reported (an AltCounters interval can end past n+1); a
+ * walk that cannot reach a suffix (a 'ref'-mode index whose BWT is not a
+ * permutation) reports 0xFFFFFFFF.  kfmi_last_timing: total, scan, locate
+ * kernel (ms).  Errors: 34 before transfer/search, 33 without samples. */
 int32_t         kfmi_locate(void *index, void *results, uint32_t max_occ, void **locations);
 uint64_t        kfmi_locations_total(void *locations);
 const uint64_t *kfmi_locations_offsets(void *locations);    /* num + 1 */
