@@ -1,9 +1,12 @@
-"""Plain-semantics search on degenerate texts (scripts/diag/dropin_degenerate.py's
+"""Search on degenerate texts (scripts/diag/dropin_degenerate.py's
 generator: homopolymers of each letter, two and three letters, short periods,
 runs at the end, texts of a few bases) with any read length -- m % K != 0
 through the remainder table -- and a random ftab, against brute-force suffix
 ranks: the host search, and with --gpu every plain GPU backend the geometry
-takes (K 1-4; the grouped layout at K 3, 4 and from K = 2 by derivation).
+takes (K 1-4; the grouped layout at K 3, 4 and from K = 2 by derivation);
+at K <= 2 also the AltCounters files through the host search and every
+AltCounters backend, against the restatement (oracle/) where the reference
+is defined and the host search where it is not.
 
 usage: python3 scripts/diag/search_degenerate.py SECONDS [--gpu]"""
 import sys
@@ -18,7 +21,8 @@ import dropin_degenerate as D  # noqa: E402
 REPO = Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(REPO / "tests"))
 import util  # noqa: E402
-from test_random_worlds import GRP, PLAIN, _takes  # noqa: E402
+from test_random_worlds import ALT, GRP, PLAIN, _takes  # noqa: E402
+from oracle import oracle  # noqa: E402
 
 K = D.K
 
@@ -45,10 +49,28 @@ def run_world(w, gpu):
                     got[b] = K.search_array(idx, q, b)
         finally:
             K.set_ftab(0)
+    wants = {b: want for b in got}
+    if k <= 2 and m % k == 0:   # AltCounters semantics: the restatement where defined, else the host search
+        acs = idx.alt_counters()
+        try:
+            try:
+                want_ac = oracle.search(acs[0].image(), q)[0]
+            except ValueError:
+                want_ac = K.search_cpu_array(acs[0], q, 2)
+            got["host-ac"] = K.search_cpu_array(acs[1], q, 2)
+            wants["host-ac"] = want_ac
+            if gpu:
+                for b in ALT:
+                    if _takes(b, k, d, n):
+                        got[b] = K.search_array(idx, q, b)
+                        wants[b] = want_ac
+        finally:
+            for x in acs:
+                x.close()
     idx.close()
     out = []
     for b, g in got.items():
-        diff = np.flatnonzero(g != want)
+        diff = np.flatnonzero(g != wants[b])
         out.append((b, None if diff.size == 0 else
                     f"K={k} d={d} n={n} kind={kind} m={m} read {int(diff[0]) // 2}"))
     return out
