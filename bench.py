@@ -546,6 +546,13 @@ def cpu_model() -> str:
     return "unknown"
 
 
+def cores_used(threads: int) -> int:
+    """CPUs a run of `threads` OS threads actually had: the thread count capped
+    by what this process can use (affinity mask and cgroup quota).  256 threads
+    on a 16-CPU quota ran on 16 cores; `threads` is reported beside it."""
+    return max(1, min(int(threads), cpu_effective()))
+
+
 def baseline_thread_counts() -> list:
     """Thread counts the CPU baseline is timed at: every core of the affinity
     mask and, when the cgroup grants fewer CPUs than that (the GPU boxes show
@@ -593,15 +600,16 @@ def cpu_reference_baseline(idx, reads, ns, k, d, thr, res_gpu):
             t_iter = float(p.stdout.split("TIME:")[1].split()[0])
             vals = np.array((Path(str(ip) + ".res.cpu")).read_bytes().split(), dtype=np.uint64)
             ok = int(vals[0]) == ns and bool(np.array_equal(vals[1:].astype(np.uint32), res_gpu[:2 * ns]))
-            runs.append({"value": round(ns / t_iter / 1e6, 4), "unit": "Mqueries/s", "cores": thr,
-                         "kind": "reference",
+            runs.append({"value": round(ns / t_iter / 1e6, 4), "unit": "Mqueries/s", "cores": cores_used(thr),
+                         "threads": thr, "kind": "reference",
                          "sample": f"first {ns} of the same 10M reads; oracle/_ref/cpu_{k}_{d} = the reference's "
                                    f"searchQueries.c + fmIndexCPUBaseline.c built from its sources, OMP "
                                    f"threads={thr}, 5 iterations, TIME {t_iter:.3f} s/iteration",
                          "parity_with_gpu": ok})
     best = max(runs, key=lambda x: x["value"])
     if len(runs) > 1:
-        best = dict(best, other_runs=[{"cores": x["cores"], "value": x["value"]} for x in runs if x is not best])
+        best = dict(best, other_runs=[{"cores": x["cores"], "threads": x["threads"], "value": x["value"]}
+                                      for x in runs if x is not best])
     return best
 
 
@@ -781,8 +789,8 @@ def cpu_product_rows(idx, reads: np.ndarray, want: np.ndarray, thrs: list) -> li
         t = time.perf_counter()
         got = K.search_cpu_array(idx, reads, nthreads=thr)
         s_ = time.perf_counter() - t
-        rows.append({"value": round(reads.shape[0] / s_ / 1e6, 4), "unit": "Mqueries/s", "cores": thr,
-                     "kind": "product (searchIndexCPU)", "equal_gpu": bool(np.array_equal(got, want))})
+        rows.append({"value": round(reads.shape[0] / s_ / 1e6, 4), "unit": "Mqueries/s", "cores": cores_used(thr),
+                     "threads": thr, "kind": "product (searchIndexCPU)", "equal_gpu": bool(np.array_equal(got, want))})
     return rows
 
 
@@ -809,7 +817,7 @@ def config1_leg(backend: str, thr, steps: int = 5) -> dict:
     thrs = thr if isinstance(thr, (list, tuple)) else [thr]
     ref = cpu_reference_baseline(idx, reads, reads.shape[0], 2, 64, thrs, res)
     if ref:
-        out["cpu_reference"] = {k: ref[k] for k in ("value", "unit", "cores", "parity_with_gpu")}
+        out["cpu_reference"] = {k: ref[k] for k in ("value", "unit", "cores", "threads", "parity_with_gpu")}
     # config #1 is the reference's CPU searcher: the product's searchIndexCPU
     # beside it, at the same thread counts (the faster run reported)
     rows = cpu_product_rows(idx, reads, res, thrs)
@@ -1184,8 +1192,10 @@ def config_rows(detail: dict, a=None) -> dict:
                                                    ("frac", c1.get("frac")), ("md5", c1.get("results_md5_pinned")))
                                  if x is not None},
                          "cpu_ref": {k: x for k, x in (("mqps", ref.get("value")), ("cores", ref.get("cores")),
+                                                       ("threads", ref.get("threads")),
                                                        ("eq", ref.get("parity_with_gpu"))) if x is not None},
                          "cpu_product": {k: x for k, x in (("mqps", prod.get("value")), ("cores", prod.get("cores")),
+                                                           ("threads", prod.get("threads")),
                                                            ("eq", prod.get("equal_gpu"))) if x is not None}}
     for key, what, pair in (("2", "Task-2Step, 3 Gbase, 10M x 100 bp",
                              ("task-mid", "task", "task-mid+ftab16", "derived_k4")),
@@ -1252,7 +1262,7 @@ def compact_line(detail: dict, detail_path: str | None) -> dict:
     line["roofline"]["frac_is"] = "achieved HBM fraction: SURVEY 8(d) algorithmic bytes / LF time / 8 TB/s"
     cpu = detail.get("cpu_baseline")
     if cpu:
-        line["cpu_baseline"] = {k: cpu.get(k) for k in ("value", "unit", "cores", "kind", "cpu_model",
+        line["cpu_baseline"] = {k: cpu.get(k) for k in ("value", "unit", "cores", "threads", "kind", "cpu_model",
                                                         "cgroup_cpu_quota", "parity_with_gpu")}
         line["cpu_baseline"]["sample"] = str(cpu.get("sample", ""))[:200]
     else:
@@ -1730,14 +1740,15 @@ def main():
             t = time.perf_counter()
             cres, _ = oracle.search(img, reads[:ns], nthreads=thr)
             cpu_s = time.perf_counter() - t
-            ports.append({"value": round(ns / cpu_s / 1e6, 4), "unit": "Mqueries/s", "cores": thr, "kind": "port",
+            ports.append({"value": round(ns / cpu_s / 1e6, 4), "unit": "Mqueries/s", "cores": cores_used(thr),
+                          "threads": thr, "kind": "port",
                           "sample": f"first {ns} of the same 10M reads, 1 pass, oracle/fmi_oracle.c "
                                     f"(restatement of fmIndexCPUBaseline.c), OMP threads={thr}, {cpu_s:.2f}s",
                           "parity_with_gpu": bool(np.array_equal(cres, res[:2 * ns]))})
         port = max(ports, key=lambda x: x["value"])
         if len(ports) > 1:
-            port = dict(port, other_runs=[{"cores": x["cores"], "value": x["value"]} for x in ports if x is not port])
-        thr = port["cores"]
+            port = dict(port, other_runs=[{"cores": x["cores"], "threads": x["threads"], "value": x["value"]}
+                                          for x in ports if x is not port])
         log(f"cpu baseline (port) {port}")
         cpu = None
         if not a.cpu_port_only:
@@ -1764,13 +1775,14 @@ def main():
         t = time.perf_counter()
         oracle.search(img, reads[:n1], nthreads=1)
         extra["cpu_port_1thread"] = {"value": round(n1 / (time.perf_counter() - t) / 1e6, 4),
-                                     "unit": "Mqueries/s", "cores": 1, "sample": f"first {n1} reads"}
+                                     "unit": "Mqueries/s", "cores": 1, "threads": 1, "sample": f"first {n1} reads"}
         # the product's own host search (searchIndexCPU, csrc/host/cpu_search.c: batched
         # prefetch, the reference CPU driver's drop-in) on the same sample and cores
         extra["cpu_product"] = cpu_product_rows(idx, reads[:ns], res[:2 * ns], thrs)
         log(f"cpu product {extra['cpu_product']}")
         log(f"cpu baseline {cpu}")
-        log(f"cpu baseline: {cpu.get('value')} Mq/s on {cpu.get('cores')} threads ({cpu.get('kind')})", brief=True)
+        log(f"cpu baseline: {cpu.get('value')} Mq/s, {cpu.get('threads')} threads on {cpu.get('cores')} cores "
+            f"({cpu.get('kind')})", brief=True)
     ph.mark("rank0_n1_legs_and_cpu_baseline")
     # per-rank phase wall times and peak host RSS (the N = 8 budget: DESIGN.md 7)
     ph_rows = D.gather({"rank": D.rank, "phases_s": ph.rows, "peak_rss_gb": Phases.peak_rss_gb(),

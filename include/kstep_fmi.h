@@ -174,9 +174,20 @@ int32_t     kfmi_search_cpu(void *index, void *queries, void *results, int32_t n
  * up [L, R) after the first `bases` bases of each query in a table of all
  * 4^bases codes (8 B each: 134 MB at 12) built on the device with the search's
  * own LF steps, then continue from there -- results are unchanged.  0 = off
- * (default; KFMI_FTAB sets it process-wide), at most 16, a multiple of K to
+ * (default; KFMI_FTAB, read once at the first search, sets it process-wide),
+ * at most 16, a multiple of K to
  * take effect; per calling thread like the backend. */
 int32_t     kfmi_set_ftab(uint32_t bases);
+/* Test knobs of the search path (not in the reference), process-wide; their
+ * environment variables are read once, at the first search, and these setters
+ * switch them afterwards.  Split class (KFMI_SPLIT): the fetch form the task
+ * kernels use for an index of that table-size class -- 0 = by the uploaded
+ * table's size (default), 1 (< 2 GB), 2 (2-3.5 GB), 4 (larger); other values
+ * KFMI_E_BAD_ARGUMENT.  Fused packing (KFMI_FUSED): 1 = reads of up to 256
+ * K-step bases are packed inside the search kernel (default), 0 = always the
+ * separate pack launch.  Results are identical either way. */
+int32_t     kfmi_set_split_class(uint32_t cls);
+int32_t     kfmi_set_fused(int32_t on);
 /* Every entry point leaves the caller's current HIP device as it found it
  * (hipGetDevice before == after), whichever devices it used inside. */
 /* Device groups (runtime multi-GPU behind the same handles; the reference

@@ -135,13 +135,21 @@ __device__ __forceinline__ uint64_t dbl_key(const uint32_t* __restrict__ rank, u
   return (uint64_t) i + h < n ? (uint64_t) rank[i + h] + h : n - 1 - (uint64_t) i;
 }
 
+/* Compiler barrier between the loads of element j and its neighbour j - 1:
+ * merged, they become one load at half its width's alignment (a 16-byte load
+ * of two u64 keys at an 8-mod-16 address), the load form kfmi_device.h
+ * load_words keeps out of every kernel.  No instruction. */
+__device__ __forceinline__ void apart() { asm volatile("" ::: "memory"); }
+
 /* head value (j if j starts a key group, else 0) for the max-scan of group starts */
 __global__ __launch_bounds__(256) void k_head_values(const uint64_t* __restrict__ keys, uint64_t n,
                                                      uint32_t* __restrict__ hv)
 {
   const uint64_t j = (uint64_t) blockIdx.x * 256 + threadIdx.x;
   if (j >= n) return;
-  hv[j] = (j == 0 || keys[j] != keys[j - 1]) ? (uint32_t) j : 0u;
+  const uint64_t kj = keys[j];
+  apart();
+  hv[j] = (j == 0 || kj != keys[j - 1]) ? (uint32_t) j : 0u;
 }
 
 /* rank[sa[j]] = gs[j]; active[j] = j lies in a group of two or more */
@@ -152,8 +160,11 @@ __global__ __launch_bounds__(256) void k_rank_init(const uint64_t* __restrict__ 
   const uint64_t j = (uint64_t) blockIdx.x * 256 + threadIdx.x;
   if (j >= n) return;
   rank[sa[j]] = gs[j];
-  const bool head = j == 0 || keys[j] != keys[j - 1];
-  const bool last = j + 1 == n || keys[j + 1] != keys[j];
+  const uint64_t kj = keys[j];
+  apart();
+  const bool head = j == 0 || kj != keys[j - 1];
+  apart();
+  const bool last = j + 1 == n || keys[j + 1] != kj;
   active[j] = (head && last) ? 0 : 1;
 }
 
@@ -192,7 +203,10 @@ __global__ __launch_bounds__(256) void k_dbl_apply(const uint32_t* __restrict__ 
   if (k >= m) return;
   const uint32_t i = suf[k];
   sa[act[k]] = i;
-  bool hd = k == 0 || grp[k] != grp[k - 1];
+  const uint32_t gk = grp[k];
+  apart();
+  bool hd = k == 0 || gk != grp[k - 1];
+  apart();
   if (!hd) hd = dbl_key(rank, n, h, i) != dbl_key(rank, n, h, suf[k - 1]);
   head[k] = hd ? 1 : 0;
   hv[k] = hd ? act[k] : 0u;

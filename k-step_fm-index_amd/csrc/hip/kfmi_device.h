@@ -158,6 +158,53 @@ __device__ __forceinline__ uint32_t ld1(const uint32_t* p)
   else return *p;
 }
 
+// Bytes of alignment every block's bit planes are guaranteed to have (the
+// layouts live in hipMalloc'd buffers, >= 256-byte aligned): the largest power
+// of two dividing both 4*EW and 4*BOFF, at most 16.  Only the tag-201 layout
+// at K = 1 falls short: its 4*(b*EW + HALF)-byte planes (EW = 2 + 2*NB words)
+// are 8-byte aligned.
+template <class G>
+__host__ __device__ constexpr int plane_align()
+{
+  int a = 16;
+  while (a > 4 && ((4 * G::EW) % a || (4 * G::BOFF) % a)) a >>= 1;
+  return a;
+}
+
+// N consecutive index words at p as loads no wider than their alignment A
+// (bytes).  Below 16, every load is fenced off by a compiler barrier: without
+// it LLVM (load/store vectorizer, SILoadStoreOptimizer; unaligned-access-mode
+// is on for gfx950) merges adjacent 8-byte loads into one 16-byte
+// global_load_dwordx4 at an 8-mod-16 address, and that form, consumed under
+// the partial s_waitcnt vmcnt(N > 0) the compiler schedules, is the round-5
+// intermittent ftab table (one end one row off in ~1e-7 of the LF steps of
+// lf_stream at K = 1, d = 64, tag 201).  The barrier emits no
+// instruction; it only keeps the loads apart.
+template <int A, int N, bool NT = false>
+__device__ __forceinline__ void load_words(const uint32_t* __restrict__ p, uint32_t* __restrict__ out)
+{
+  if constexpr (A >= 16 && N % 4 == 0) {
+#pragma unroll
+    for (int i = 0; i < N / 4; ++i) {
+      const v4u v = ld4<NT>(p + 4 * i);
+      out[4 * i + 0] = v.x; out[4 * i + 1] = v.y; out[4 * i + 2] = v.z; out[4 * i + 3] = v.w;
+    }
+  } else if constexpr (A >= 8 && N % 2 == 0) {
+#pragma unroll
+    for (int i = 0; i < N / 2; ++i) {
+      asm volatile("" ::: "memory");
+      const v2u v = ld2<NT>(p + 2 * i);
+      out[2 * i + 0] = v.x; out[2 * i + 1] = v.y;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      asm volatile("" ::: "memory");
+      out[i] = ld1<NT>(p + i);
+    }
+  }
+}
+
 // base2index restated on a byte (genFMindex.c:71-84)
 __device__ __forceinline__ uint32_t code_of(uint32_t x)
 {
@@ -540,22 +587,7 @@ struct Blk {
 template <class G, bool NT = false>
 __device__ __forceinline__ void load_planes(const uint32_t* __restrict__ p, uint32_t (&bm)[G::BMW])
 {
-  if constexpr (G::BMW % 4 == 0 && ((G::BOFF + 0) % 4 == 0) && (G::EW % 4 == 0)) {
-#pragma unroll
-    for (int i = 0; i < G::BMW / 4; ++i) {
-      const v4u v = ld4<NT>(p + 4 * i);
-      bm[4 * i + 0] = v.x; bm[4 * i + 1] = v.y; bm[4 * i + 2] = v.z; bm[4 * i + 3] = v.w;
-    }
-  } else if constexpr (G::BMW % 2 == 0 && (G::BOFF % 2 == 0) && (G::EW % 2 == 0)) {
-#pragma unroll
-    for (int i = 0; i < G::BMW / 2; ++i) {
-      const v2u v = ld2<NT>(p + 2 * i);
-      bm[2 * i + 0] = v.x; bm[2 * i + 1] = v.y;
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < G::BMW; ++i) bm[i] = ld1<NT>(p + i);
-  }
+  load_words<plane_align<G>(), G::BMW, NT>(p, bm);
 }
 
 template <class G, bool NT = false>
@@ -607,7 +639,9 @@ __device__ __forceinline__ uint32_t lf_from_block(const IdxArgs& ix, const Blk<G
 // Streaming LF for large blocks (d >= 192 with K=2): the planes are loaded in
 // chunks of up to 8 words, every load of a chunk issued before any of its
 // popcounts so the chunk's lines are in flight together; all words are read
-// (as the reference does) and masked.
+// (as the reference does) and masked.  Also the per-row step of the ftab,
+// remainder-table, derivation, statistics and locate kernels.  Loads follow
+// load_words' alignment rule (the round-5 ftab hazard).
 // ---------------------------------------------------------------------------
 template <class G>
 __device__ __forceinline__ uint32_t lf_stream(const IdxArgs& ix, uint32_t X, uint32_t c,
@@ -627,16 +661,7 @@ __device__ __forceinline__ uint32_t lf_stream(const IdxArgs& ix, uint32_t X, uin
     for (int j = 0; j < CH; ++j) {
       const int w = w0 + j;
       if (w >= G::NB) break;
-      if constexpr (G::PW == 4 && (G::BOFF % 4 == 0) && (G::EW % 4 == 0)) {
-        const uint4 q = *reinterpret_cast<const uint4*>(pl + 4 * w);
-        v[j][0] = q.x; v[j][1] = q.y; v[j][2] = q.z; v[j][3] = q.w;
-      } else if constexpr (G::PW == 2 && (G::BOFF % 2 == 0) && (G::EW % 2 == 0)) {
-        const uint2 q = *reinterpret_cast<const uint2*>(pl + 2 * w);
-        v[j][0] = q.x; v[j][1] = q.y;
-      } else {
-#pragma unroll
-        for (int p = 0; p < G::PW; ++p) v[j][p] = pl[G::PW * w + p];
-      }
+      load_words<plane_align<G>(), G::PW>(pl + G::PW * w, v[j]);   /* never wider than the planes' alignment */
     }
 #pragma unroll
     for (int j = 0; j < CH; ++j) {

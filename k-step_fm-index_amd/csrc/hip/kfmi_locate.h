@@ -46,9 +46,13 @@ __device__ __forceinline__ uint32_t row_code(const IdxArgs& ix, uint32_t X)
   const uint32_t o = X - b * (uint32_t) G::D;
   const uint32_t* pl = locate<G>(ix, b, 0u).planes + (o >> 5) * G::PW;
   const uint32_t bit = 31u - (o & 31u);
+  /* the word group of row X: aligned to the planes and to its own 4*PW bytes */
+  constexpr int A = plane_align<G>() < ((4 * G::PW) & -(4 * G::PW)) ? plane_align<G>() : ((4 * G::PW) & -(4 * G::PW));
+  uint32_t w[G::PW];
+  load_words<A, G::PW>(pl, w);
   uint32_t c = 0;
 #pragma unroll
-  for (int p = 0; p < G::PW; ++p) c |= ((pl[p] >> bit) & 1u) << p;
+  for (int p = 0; p < G::PW; ++p) c |= ((w[p] >> bit) & 1u) << p;
   return c;
 }
 

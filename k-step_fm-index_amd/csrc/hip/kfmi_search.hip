@@ -17,6 +17,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <atomic>
 #include <mutex>
 #include <new>
 #include <vector>
@@ -151,9 +152,58 @@ extern "C" int32_t kfmi_set_ftab(uint32_t bases)
 uint32_t ftab_bases(void)
 {
   if (t_ftab >= 0) return (uint32_t) t_ftab;
-  const char* e = getenv("KFMI_FTAB");
-  const int v = e ? atoi(e) : 0;
-  return v > 0 && v <= 16 ? (uint32_t) v : 0u;
+  static const uint32_t env = [] {   /* KFMI_FTAB, read once per process */
+    const char* e = getenv("KFMI_FTAB");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 && v <= 16 ? (uint32_t) v : 0u;
+  }();
+  return env;
+}
+
+/* Test knobs of the search path: read from the environment once per process
+ * (KFMI_SPLIT, KFMI_FUSED) and switched through their setters afterwards, so
+ * no search reads the environment.  -2 = not read yet. */
+static std::atomic<int> g_split_class{-2};   /* 0 = by table size (split_for), 1/2/4 = that class */
+static std::atomic<int> g_fused{-2};         /* 1 = fused packing where it fits, 0 = pack kernel */
+
+static int knob_once(std::atomic<int>& k, int (*read_env)())
+{
+  int v = k.load(std::memory_order_relaxed);
+  if (v == -2) {
+    int expect = -2;
+    k.compare_exchange_strong(expect, read_env(), std::memory_order_relaxed);
+    v = k.load(std::memory_order_relaxed);
+  }
+  return v;
+}
+
+static int split_class_from_env()
+{
+  const char* e = getenv("KFMI_SPLIT");
+  if (!e || !*e) return 0;
+  const int v = atoi(e);
+  if (v != 1 && v != 2 && v != 4)
+    fprintf(stderr, "kstepfmi: KFMI_SPLIT=%s: only 1, 2 or 4 (table-size class) are read; using 1\n", e);
+  return (v == 2 || v == 4) ? v : 1;
+}
+
+static int fused_from_env()
+{
+  const char* e = getenv("KFMI_FUSED");
+  return (e && !atoi(e)) ? 0 : 1;
+}
+
+extern "C" int32_t kfmi_set_split_class(uint32_t cls)
+{
+  if (cls != 0 && cls != 1 && cls != 2 && cls != 4) return KFMI_E_BAD_ARGUMENT;
+  g_split_class.store((int) cls, std::memory_order_relaxed);
+  return KFMI_SUCCESS;
+}
+
+extern "C" int32_t kfmi_set_fused(int32_t on)
+{
+  g_fused.store(on ? 1 : 0, std::memory_order_relaxed);
+  return KFMI_SUCCESS;
 }
 extern "C" int32_t kfmi_last_error(void) { return t_last_error; }
 
@@ -423,14 +473,13 @@ __global__ __launch_bounds__(256) void build_ac128_kernel(const uint32_t* __rest
 }
 
 /* Code registers the task kernel needs to pack a query itself (0: use the
- * pack kernel).  KFMI_FUSED=0 forces the separate pack launch. */
+ * pack kernel).  KFMI_FUSED=0 / kfmi_set_fused(0) forces the separate pack launch. */
 /* Fused packing keeps 16 bases per register word (MAXW words): 8 words up to
  * 128 K-step bases, 16 up to 256, else the pack kernel. */
 int fused_maxw(int backend, uint32_t bases)
 {
   (void) backend;   /* task and coop kernels both pack in-kernel (m <= 256 fits either's LDS staging) */
-  const char* e = getenv("KFMI_FUSED");
-  if (e && !atoi(e)) return 0;
+  if (!knob_once(g_fused, fused_from_env)) return 0;
   return bases <= 128 ? 8 : (bases <= 256 ? 16 : 0);
 }
 
@@ -1147,7 +1196,7 @@ int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx, kfmi_dev_
  * profiles/r02/sweep_split_r2ah.jsonl, sweep_split150_r2aj.jsonl; the asm
  * forms: profiles/r03/sweep_r3n.jsonl, sweep150_r3n.jsonl.  The ftab lookup
  * (one gather per read) is never split: that measured slower.
- * KFMI_SPLIT=1|2|4 (a test knob) answers in place of the table size, so that
+ * KFMI_SPLIT=1|2|4 / kfmi_set_split_class (a test knob) answers in place of the table size, so that
  * a small test index runs the fetch form a table of that size class gets
  * (launch_task: one form per geometry and class). */
 /* Knobs of earlier rounds' experiments that no longer exist, and KFMI_SPLIT
@@ -1160,20 +1209,14 @@ static void warn_stale_knobs_once()
   std::call_once(once, [] {
     for (const char* k : {"KFMI_REORDER", "KFMI_LDS_PAD", "KFMI_COOP_ISSUE", "KFMI_QPT", "KFMI_NT_FROM"})
       if (getenv(k)) fprintf(stderr, "kstepfmi: %s is no longer read (removed experiment knob); ignored\n", k);
-    const char* e = getenv("KFMI_SPLIT");
-    if (e && *e && strcmp(e, "1") && strcmp(e, "2") && strcmp(e, "4"))
-      fprintf(stderr, "kstepfmi: KFMI_SPLIT=%s: only 1, 2 or 4 (table-size class) are read; using 1\n", e);
   });
 }
 
 static uint32_t split_for(uint64_t table_bytes, int layout)
 {
   warn_stale_knobs_once();
-  const char* e = getenv("KFMI_SPLIT");
-  if (e && *e) {
-    const int v = atoi(e);
-    return (v == 2 || v == 4) ? (uint32_t) v : 1u;
-  }
+  const int cls = knob_once(g_split_class, split_class_from_env);
+  if (cls) return (uint32_t) cls;
   if (table_bytes > 3500000000ull) return 4u;
   if (table_bytes > 2000000000ull) return (layout == LAY_MID || layout == LAY_MIDAC) ? 2u : 4u;
   return 1u;

@@ -119,6 +119,8 @@ def load() -> ctypes.CDLL:
         "kfmi_get_devices": (i32, [ctypes.POINTER(ctypes.c_int32), i32]),
         "kfmi_build_index_ex": (i32, [vp, u64, u32, u32, u32, i32, pvp]),
         "kfmi_set_ftab": (i32, [u32]),
+        "kfmi_set_split_class": (i32, [u32]),
+        "kfmi_set_fused": (i32, [i32]),
         "kfmi_set_alphabet": (i32, [ctypes.c_char_p]),
         "kfmi_index_sa": (i32, [vp, pvp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32)]),
         "kfmi_save_sa": (i32, [ctypes.c_char_p, vp]),
@@ -159,6 +161,18 @@ def get_backend() -> str:
 def set_ftab(bases: int) -> None:
     """Bowtie-style jump-start table of `bases` bases for the task backends (0 = off)."""
     _check(load().kfmi_set_ftab(int(bases)), f"set_ftab({bases})")
+
+
+def set_split_class(cls: int) -> None:
+    """Fetch form of the task kernels by table-size class (0 = by the uploaded
+    table's size, 1 / 2 / 4 = that class); process-wide test knob (KFMI_SPLIT)."""
+    _check(load().kfmi_set_split_class(int(cls)), f"set_split_class({cls})")
+
+
+def set_fused(on: bool) -> None:
+    """In-kernel query packing where it fits (True, default) or always the
+    separate pack launch (False); process-wide test knob (KFMI_FUSED)."""
+    _check(load().kfmi_set_fused(1 if on else 0), f"set_fused({on})")
 
 
 def set_alphabet(mode: str | None) -> None:

@@ -29,6 +29,24 @@ def kfmi_mod():
     return kstep_fmi
 
 
+@pytest.fixture
+def knobs(kfmi_mod):
+    """Switch the search path's process-wide test knobs (kfmi_set_split_class,
+    kfmi_set_fused: their KFMI_SPLIT / KFMI_FUSED variables are read once per
+    process) and put the defaults back afterwards."""
+    class Knobs:
+        @staticmethod
+        def split(cls):
+            kfmi_mod.set_split_class(int(cls) if cls else 0)
+
+        @staticmethod
+        def fused(on):
+            kfmi_mod.set_fused(str(on) != "0")
+    yield Knobs
+    kfmi_mod.set_split_class(0)
+    kfmi_mod.set_fused(True)
+
+
 def pytest_collection_modifyitems(config, items):
     # OMP inside the oracle: keep CPU tests bounded on small boxes.
     os.environ.setdefault("OMP_NUM_THREADS", "8")

@@ -20,6 +20,7 @@ import os
 import numpy as np
 import pytest
 
+import ref_fill
 import util
 from test_gpu_parity import coop_supported
 
@@ -44,9 +45,21 @@ def load_ref_text(K, n):
     return text
 
 
+def ref_build(K, text, ent, gpu):
+    """The 'ref'-mode build of `text` as the reference tool wrote it: the
+    product's image (its defined fill) with the unvisited rows patched to the
+    golden's fill byte (tests/ref_fill.py); the product index itself when no
+    patch applies."""
+    idx = K.Index.build(text, k=ent["k"], d=ent["d"], gpu=gpu)
+    if ent["fill"] is None or ent["k"] < 2:
+        return idx
+    img = ref_fill.patch(idx.image(), text, ref_fill.full_sa(K, text, ent["k"], ent["d"]), ent["fill"])
+    idx.close()
+    return K.Index.from_image(img)
+
+
 @pytest.fixture
-def ref_mode(kfmi_mod, monkeypatch):
-    monkeypatch.delenv("KFMI_REF_FILL", raising=False)
+def ref_mode(kfmi_mod):
     kfmi_mod.set_alphabet("ref")
     yield kfmi_mod
     kfmi_mod.set_alphabet(None)
@@ -66,12 +79,10 @@ def test_loadref_ref_mode_is_readref(ref_mode):
 
 
 @pytest.mark.parametrize("key,ent", builds())
-def test_host_builder_ref_mode_equals_reference(ref_mode, monkeypatch, key, ent):
+def test_host_builder_ref_mode_equals_reference(ref_mode, key, ent):
     K = ref_mode
     text = load_ref_text(K, man()["n"])
-    if ent["fill"] is not None:
-        monkeypatch.setenv("KFMI_REF_FILL", str(ent["fill"]))
-    idx = K.Index.build(text, k=ent["k"], d=ent["d"], gpu=False)
+    idx = ref_build(K, text, ent, gpu=False)
     assert hashlib.md5(idx.image().tobytes()).hexdigest() == ent["md5"]["100"]
     if "101" in ent["files"]:
         i101 = idx.interleave()
@@ -143,18 +154,20 @@ def test_set_alphabet_rejects_unknown(kfmi_mod):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("key,ent", builds())
-def test_gpu_builder_ref_mode_equals_reference(ref_mode, monkeypatch, key, ent):
+def test_gpu_builder_ref_mode_equals_reference(ref_mode, key, ent):
     K = ref_mode
     if K.device_count() < 1:
         pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
     K.set_device(0)
     text = load_ref_text(K, man()["n"])
-    if ent["fill"] is not None:
-        monkeypatch.setenv("KFMI_REF_FILL", str(ent["fill"]))
-    idx = K.Index.build(text, k=ent["k"], d=ent["d"], gpu=True)
+    idx = ref_build(K, text, ent, gpu=True)
     assert hashlib.md5(idx.image().tobytes()).hexdigest() == ent["md5"]["100"]
-    idx2 = K.Index.build(text, k=ent["k"], d=ent["d"], gpu=True, sa_rate=4)   # with SA samples
-    assert np.array_equal(idx2.image(), idx.image())
+    # the GPU builder's own image (its defined fill) equals the host builder's,
+    # with SA samples too
+    plain = K.Index.build(text, k=ent["k"], d=ent["d"], gpu=True)
+    idx2 = K.Index.build(text, k=ent["k"], d=ent["d"], gpu=True, sa_rate=4)
+    assert np.array_equal(idx2.image(), plain.image())
+    assert np.array_equal(plain.image(), K.Index.build(text, k=ent["k"], d=ent["d"], gpu=False).image())
 
 
 PLAIN = ("task", "coop", "task-mid", "coop-mid", "task-packed", "coop-packed")
@@ -163,7 +176,7 @@ AC = ("task-ac", "coop-ac", "task-ac128", "coop-ac128", "task-ac-mid", "coop-ac-
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("key,ent", builds())
-def test_gpu_search_on_reference_indexes(ref_mode, monkeypatch, key, ent):
+def test_gpu_search_on_reference_indexes(ref_mode, key, ent):
     """Every backend on the reference-built indexes of the alpha text equals
     the reference's CPU searchers (plain: cpu_*, AltCounters: cpuac_*).  The
     index is the committed reference file, or -- where only its md5 is
@@ -173,9 +186,7 @@ def test_gpu_search_on_reference_indexes(ref_mode, monkeypatch, key, ent):
     if "100" in ent["files"]:
         idx = K.Index.load(ALPHA / ent["files"]["100"]["file"])
     else:
-        if ent["fill"] is not None:
-            monkeypatch.setenv("KFMI_REF_FILL", str(ent["fill"]))
-        idx = K.Index.build(load_ref_text(K, man()["n"]), k=ent["k"], d=ent["d"], gpu=False)
+        idx = ref_build(K, load_ref_text(K, man()["n"]), ent, gpu=False)
         assert hashlib.md5(idx.image().tobytes()).hexdigest() == ent["md5"]["100"]
     for rk, r in sorted(ent["results"].items()):
         m, tag = (int(x) for x in rk.split("."))

@@ -20,7 +20,7 @@ def test_reference_cpu_baseline_matches_oracle(kfmi_mod, k):
     want, _ = oracle.search(idx.image(), reads)
     out = bench.cpu_reference_baseline(idx, reads, 2000, k, 64, 2, want)
     assert out is not None and out["kind"] == "reference" and out["parity_with_gpu"]
-    assert out["value"] > 0
+    assert out["value"] > 0 and out["threads"] == 2 and out["cores"] == min(2, bench.cpu_effective())
 
 
 def test_cpu_product_rows_equal_oracle(kfmi_mod):
@@ -32,7 +32,32 @@ def test_cpu_product_rows_equal_oracle(kfmi_mod):
     reads = t[rng.integers(0, len(t) - 100, size=2000)[:, None] + np.arange(100)]
     want, _ = oracle.search(idx.image(), reads)
     rows = bench.cpu_product_rows(idx, reads, want, [1, 3])
-    assert [r["cores"] for r in rows] == [1, 3] and all(r["equal_gpu"] and r["value"] > 0 for r in rows)
+    assert [r["threads"] for r in rows] == [1, 3] and all(r["equal_gpu"] and r["value"] > 0 for r in rows)
+    assert [r["cores"] for r in rows] == [1, min(3, bench.cpu_effective())]
+
+
+def test_cores_never_exceed_usable_cpus(monkeypatch):
+    """cpu_baseline.cores is the CPUs a run actually had: the
+    thread count capped by the affinity mask and the cgroup quota -- 256
+    threads on a box with a 16-CPU quota report cores 16, threads 256."""
+    monkeypatch.setattr(bench, "cpu_threads", lambda: 256)
+    monkeypatch.setattr(bench, "cpu_quota", lambda: 16.0)
+    assert bench.cpu_effective() == 16
+    assert bench.baseline_thread_counts() == [256, 16]
+    assert [bench.cores_used(t) for t in (256, 16, 4, 1)] == [16, 16, 4, 1]
+    monkeypatch.setattr(bench, "cpu_quota", lambda: None)      # no quota: the affinity mask bounds it
+    assert bench.cores_used(512) == 256 and bench.cores_used(8) == 8
+
+
+def test_real_quota_bounds_cores():
+    """Whatever this host's cgroup grants: every reported core count is at
+    most the quota when one exists."""
+    q = bench.cpu_quota()
+    for t in bench.baseline_thread_counts():
+        c = bench.cores_used(t)
+        assert 1 <= c <= t and c <= bench.cpu_threads()
+        if q:
+            assert c <= max(1, int(round(q)))
 
 
 def test_variant_roofline_and_pmc_file(tmp_path, monkeypatch):

@@ -65,7 +65,7 @@ def test_line_fits_the_driver_tail(tmp_path, name, n):
     for k in ("bound", "achieved", "peak", "frac", "bytes_per_launch", "traffic", "traffic_over_algorithmic",
               "line_requests_per_query", "line_request_frac", "lf_ms"):
         assert k in line["roofline"], k
-    for k in ("value", "cores", "kind", "cpu_model", "cgroup_cpu_quota", "parity_with_gpu"):
+    for k in ("value", "cores", "threads", "kind", "cpu_model", "cgroup_cpu_quota", "parity_with_gpu"):
         assert k in line["cpu_baseline"], k
     assert line["parity"]["results_md5_pinned"] is True and line["ranks"]["n"] == n
     assert json.loads((tmp_path / "detail.json").read_text())["variants"] == d["variants"]

@@ -106,7 +106,7 @@ def test_3g_backend_full_scale(gpu, g3, reads, backend, tmp_path):
 
 
 @pytest.mark.parametrize("split", ["", "1"])
-def test_3g_kstep4_full_scale(gpu, g3, reads, split, tmp_path, monkeypatch):
+def test_3g_kstep4_full_scale(gpu, g3, reads, split, tmp_path, knobs):
     """K = 4 on the same 3 Gbase text (LAY_GRP, 96 GB of lines, device-resident
     build): the same suffix-array intervals, so the q1M results file md5 and
     the q10M results equal the K = 2 pins; 150 bp (150 % 4 = 2 bases from the
@@ -115,7 +115,7 @@ def test_3g_kstep4_full_scale(gpu, g3, reads, split, tmp_path, monkeypatch):
     from kstep_fmi import synth
     text, idx2 = g3
     if split:
-        monkeypatch.setenv("KFMI_SPLIT", split)
+        knobs.split(split)
     idx2.free_gpu()
     i4 = gpu.Index.build(text, k=4, d=64, gpu=True, host_image=False)
     try:

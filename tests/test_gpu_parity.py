@@ -325,19 +325,19 @@ def test_coop_backends_equal_oracle(gpu, oracle_mod, random_index, backend, monk
             got = gpu.search_array(idx, q, backend)
             assert np.array_equal(got, want), (backend, k, d, m)
         if d == 64:
-            monkeypatch.setenv("KFMI_FTAB", str(4 * k))
+            gpu.set_ftab(4 * k)
             q = _reads(text, 5003, 100, seed=19 + k)
             want, _ = oracle_mod.search(ref_img, q)
             got = gpu.search_array(idx, q, backend)
-            monkeypatch.delenv("KFMI_FTAB")
+            gpu.set_ftab(0)
             assert np.array_equal(got, want), (backend, k, d, "ftab")
 
 
 @pytest.mark.parametrize("split", ["1", "2", "4"])
 @pytest.mark.parametrize("backend", ["task-mid", "task", "task-packed", "task-ac", "task-ac128", "task-ac-mid"])
-def test_split_gathers_equal_oracle(gpu, oracle_mod, random_index, backend, split, monkeypatch):
+def test_split_gathers_equal_oracle(gpu, oracle_mod, random_index, backend, split, knobs):
     """Every fetch form on small indexes, by forcing the table-size class
-    (KFMI_SPLIT = 1: under 2 GB, 2: 2-3.5 GB, 4: larger): the asm
+    (kfmi_set_split_class = 1: under 2 GB, 2: 2-3.5 GB, 4: larger): the asm
     fetch in one group (class 1) or two (classes 2, 4) where it applies (K=2
     d=64, K=1 d=128), else the C++ fetch, in four 16-lane groups for class 4
     (and class 2 in the 8-word fused kernel).  The same results as the
@@ -345,7 +345,7 @@ def test_split_gathers_equal_oracle(gpu, oracle_mod, random_index, backend, spli
     (remainder table), fused and pack-kernel reads, and the ftab jump start;
     d = 192 has no split path (lf_stream) and must be unaffected."""
     text, idxs = random_index
-    monkeypatch.setenv("KFMI_SPLIT", split)
+    knobs.split(split)
     for k, d in ((2, 64), (1, 64), (1, 32), (1, 128), (2, 128), (2, 192)):
         idx = idxs[(k, d)]
         if not coop_supported(backend, k, d):
@@ -361,11 +361,11 @@ def test_split_gathers_equal_oracle(gpu, oracle_mod, random_index, backend, spli
             got = gpu.search_array(idx, q, backend)
             assert np.array_equal(got, want), (backend, k, d, m)
         if d == 64:
-            monkeypatch.setenv("KFMI_FTAB", str(4 * k))
+            gpu.set_ftab(4 * k)
             q = _reads(text, 5003, 100, seed=17 + k)
             want, _ = oracle_mod.search(ref_img, q)
             got = gpu.search_array(idx, q, backend)
-            monkeypatch.delenv("KFMI_FTAB")
+            gpu.set_ftab(0)
             assert np.array_equal(got, want), (backend, k, d, "ftab")
 
 

@@ -60,9 +60,9 @@ def test_k3_gpu_builder_equals_host_builder(kfmi_mod, k3):
 @pytest.mark.parametrize("split", ["1", "4"])
 @pytest.mark.parametrize("fused", ["1", "0"])
 @pytest.mark.parametrize("backend", GRP)
-def test_k3_matches_oracle(kfmi_mod, oracle_mod, k3, backend, fused, split, monkeypatch):
-    monkeypatch.setenv("KFMI_FUSED", fused)
-    monkeypatch.setenv("KFMI_SPLIT", split)   # 4: exec-masked gather groups (task-grp; coop ignores it)
+def test_k3_matches_oracle(kfmi_mod, oracle_mod, k3, backend, fused, split, knobs):
+    knobs.fused(fused)
+    knobs.split(split)   # 4: exec-masked gather groups (task-grp; coop ignores it)
     K = kfmi_mod
     t, i3, i1 = k3
     for m, n in ((99, 20_000), (150, 4_000), (3, 500), (15, 2_000), (126, 2_000), (129, 2_000), (255, 1_000),

@@ -79,11 +79,11 @@ def k4(kfmi_mod):
 @pytest.mark.gpu
 @pytest.mark.parametrize("split", ["1", "4"])
 @pytest.mark.parametrize("backend", GRP)
-def test_grp_matches_oracle_and_k2(kfmi_mod, oracle_mod, k4, backend, split, monkeypatch):
+def test_grp_matches_oracle_and_k2(kfmi_mod, oracle_mod, k4, backend, split, knobs):
     """split 4: per-lane gathers as 4 exec-masked groups (the default for the
     96 GB GRP table at 3 Gbase; the coop kernel ignores it)."""
     K = kfmi_mod
-    monkeypatch.setenv("KFMI_SPLIT", split)
+    knobs.split(split)
     t, i4, i2 = k4
     for m, n in ((100, 20_000), (16, 4_000), (4, 2_000), (256, 1_000), (300, 1_000), (8, 500), (102, 1_001),
                  (150, 777)):

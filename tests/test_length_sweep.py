@@ -59,8 +59,8 @@ def sweep(kfmi_mod, oracle_mod):
 
 @pytest.mark.parametrize("fused", ["1", "0"])
 @pytest.mark.parametrize("k", [1, 2, 3, 4])
-def test_lengths_every_backend(sweep, k, fused, monkeypatch):
-    monkeypatch.setenv("KFMI_FUSED", fused)
+def test_lengths_every_backend(sweep, k, fused, knobs):
+    knobs.fused(fused)
     K, idx, cases = sweep
     for b in BACKENDS[k]:
         for m, (q, want) in cases.items():

@@ -51,8 +51,8 @@ def _reads(text, n, m, seed):
 
 
 @pytest.mark.parametrize("fused", ["1", "0"])
-def test_rem_matches_k1_oracle(gpu, oracle_mod, texts, fused, monkeypatch):
-    monkeypatch.setenv("KFMI_FUSED", fused)
+def test_rem_matches_k1_oracle(gpu, oracle_mod, texts, fused, knobs):
+    knobs.fused(fused)
     text, idx = texts
     img1 = idx[(1, 64)].image()
     cases = [((2, 64), PLAIN2, (1, 3, 5, 17, 99, 101, 151, 255, 257, 301, 1025, 2049, 4001)),

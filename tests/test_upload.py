@@ -83,10 +83,10 @@ def test_ascii_and_packed_uploads_agree(gpu, oracle_mod, data, monkeypatch):
             w = want if kd == (2, 64) else oracle_mod.search(idx[kd].image(), q)[0]
             assert np.array_equal(R.array(), w), (form, kd)
         assert gpu.count_blocks(idx[(2, 64)], Q) == blocks, form
-        monkeypatch.setenv("KFMI_FTAB", "8")
+        gpu.set_ftab(8)
         gpu.search(idx[(2, 64)], Q, R)
         gpu.transfer_to_cpu(R)
-        monkeypatch.delenv("KFMI_FTAB")
+        gpu.set_ftab(0)
         assert np.array_equal(R.array(), want), (form, "ftab")
     Q.close()
     R.close()
