@@ -692,7 +692,7 @@ int32_t build_gpu(const char* text, uint64_t n, uint32_t k, uint32_t d, uint32_t
     BHIP(hipStreamSynchronize(st));
     sa.release();
     kfmi_fmi_t* f = nullptr;
-    int32_t err = kfmi_index_ref_walk(text, sa_full.data(), n, k, d, kfmi_ref_fill(), &f);
+    int32_t err = kfmi_index_ref_walk(text, sa_full.data(), n, k, d, &f);
     if (err) return err;
     if (sa_rate) {
       err = kfmi_sa_alloc(f, sa_rate);

@@ -295,199 +295,14 @@ __global__ __launch_bounds__(256) void task_kernel(IdxArgs ix, const uint32_t* _
   }
 }
 
-/* DIAG (round 6 ftab experiment, removed after): lf_stream variants */
-template <class G, int VAR>
-__device__ __forceinline__ uint32_t lf_stream_diag(const IdxArgs& ix, uint32_t X, uint32_t c,
-                                                   const uint32_t (&sx)[2 * G::K])
-{
-  const uint32_t b = X / (uint32_t) G::D;
-  const int o = (int) (X - b * (uint32_t) G::D);
-  const Where<G> wh = locate<G>(ix, b, c);
-  uint32_t cnt;
-  if constexpr (VAR == 5) cnt = __hip_atomic_load(wh.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else cnt = load_counter<G>(ix, wh, b, c);
-  const uint32_t* pl = wh.planes;
-  uint32_t v[G::NB][G::PW];
-  if constexpr (VAR == 7) {   /* 16-byte-aligned loads only (K=1, d=64 AC: planes at 24b+8) */
-    const uintptr_t a = (uintptr_t) pl;
-    const v4u* q = reinterpret_cast<const v4u*>(a & ~(uintptr_t) 15);
-    const v4u x0 = q[0];
-    if (a & 15) {
-      const v4u x1 = q[1];
-      v[0][0] = x0.z; v[0][1] = x0.w; v[1][0] = x1.x; v[1][1] = x1.y;
-    } else {
-      v[0][0] = x0.x; v[0][1] = x0.y; v[1][0] = x0.z; v[1][1] = x0.w;
-    }
-  } else
-#pragma unroll
-  for (int w = 0; w < G::NB; ++w)
-#pragma unroll
-    for (int p = 0; p < G::PW; ++p) {
-      if constexpr (VAR == 12) {
-        if (p == 0 && w > 0) asm volatile("" ::: "memory");
-        v[w][p] = pl[G::PW * w + p];
-      } else
-      if constexpr (VAR == 3) v[w][p] = reinterpret_cast<const volatile uint32_t*>(pl)[G::PW * w + p];
-      else if constexpr (VAR == 5) v[w][p] = __hip_atomic_load(pl + G::PW * w + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else v[w][p] = pl[G::PW * w + p];
-    }
-  if constexpr (VAR == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  uint32_t pop = 0;
-#pragma unroll
-  for (int w = 0; w < G::NB; ++w) {
-    uint32_t m = row_mask(o - 32 * w);
-    if constexpr (G::TWO_SIDED) m = wh.e ? ~m : m;
-    pop += __popc(m & select_rows<G::K>(v[w], sx));
-  }
-  return finish<G>(ix, cnt, pop, b, c, X, wh.e);
-}
-
-/* DIAG VAR 10: both ends' loads issued in lf_stream's order from one asm
- * block (L planes, R planes, L counter, R counter), each destination copied
- * right after the partial wait the compiler emits for it (vmcnt 3, 2, 1), then
- * vmcnt(0); a copy that differs from the final register = a VGPR written after
- * vmcnt counted its load complete.  Returns the mismatch mask (bit 0 L planes,
- * 1 R planes, 2 L counter, 3 R counter); L, R from the copies (as the
- * compiler's code would use them). */
-template <class G>
-__device__ __forceinline__ uint32_t lf_pair_probe(const IdxArgs& ix, uint32_t& L, uint32_t& R, uint32_t c,
-                                                  const uint32_t (&sx)[2 * G::K])
-{
-  const uint32_t bl = L / (uint32_t) G::D, br = R / (uint32_t) G::D;
-  const Where<G> wl = locate<G>(ix, bl, c), wr = locate<G>(ix, br, c);
-  uint32_t sl[4], sr[4], fl[4], fr[4], scl, scr, fcl, fcr;
-  asm volatile(
-      "global_load_dwordx4 v[10:13], %[apl], off\n"
-      "global_load_dwordx4 v[14:17], %[apr], off\n"
-      "global_load_dword v18, %[acl], off\n"
-      "global_load_dword v19, %[acr], off\n"
-      "s_waitcnt vmcnt(3)\n"
-      "v_mov_b32 %[sl0], v10\nv_mov_b32 %[sl1], v11\nv_mov_b32 %[sl2], v12\nv_mov_b32 %[sl3], v13\n"
-      "s_waitcnt vmcnt(2)\n"
-      "v_mov_b32 %[sr0], v14\nv_mov_b32 %[sr1], v15\nv_mov_b32 %[sr2], v16\nv_mov_b32 %[sr3], v17\n"
-      "s_waitcnt vmcnt(1)\n"
-      "v_mov_b32 %[scl], v18\n"
-      "s_waitcnt vmcnt(0)\n"
-      "v_mov_b32 %[scr], v19\n"
-      "v_mov_b32 %[fl0], v10\nv_mov_b32 %[fl1], v11\nv_mov_b32 %[fl2], v12\nv_mov_b32 %[fl3], v13\n"
-      "v_mov_b32 %[fr0], v14\nv_mov_b32 %[fr1], v15\nv_mov_b32 %[fr2], v16\nv_mov_b32 %[fr3], v17\n"
-      "v_mov_b32 %[fcl], v18\nv_mov_b32 %[fcr], v19\n"
-      : [sl0] "=&v"(sl[0]), [sl1] "=&v"(sl[1]), [sl2] "=&v"(sl[2]), [sl3] "=&v"(sl[3]), [sr0] "=&v"(sr[0]),
-        [sr1] "=&v"(sr[1]), [sr2] "=&v"(sr[2]), [sr3] "=&v"(sr[3]), [scl] "=&v"(scl), [scr] "=&v"(scr),
-        [fl0] "=&v"(fl[0]), [fl1] "=&v"(fl[1]), [fl2] "=&v"(fl[2]), [fl3] "=&v"(fl[3]), [fr0] "=&v"(fr[0]),
-        [fr1] "=&v"(fr[1]), [fr2] "=&v"(fr[2]), [fr3] "=&v"(fr[3]), [fcl] "=&v"(fcl), [fcr] "=&v"(fcr)
-      : [apl] "v"(wl.planes), [apr] "v"(wr.planes), [acl] "v"(wl.cnt), [acr] "v"(wr.cnt)
-      : "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "memory");
-  uint32_t mask = 0;
-  for (int i = 0; i < 4; ++i) {
-    mask |= sl[i] != fl[i] ? 1u : 0u;
-    mask |= sr[i] != fr[i] ? 2u : 0u;
-  }
-  mask |= scl != fcl ? 4u : 0u;
-  mask |= scr != fcr ? 8u : 0u;
-  /* the step from the copies, as the compiler's code reads them */
-  const uint32_t X[2] = {L, R};
-  const uint32_t b2[2] = {bl, br};
-  const Where<G> w2[2] = {wl, wr};
-  uint32_t out2[2];
-  for (int end = 0; end < 2; ++end) {
-    const uint32_t* v = end ? sr : sl;
-    const int o = (int) (X[end] - b2[end] * (uint32_t) G::D);
-    uint32_t pop = 0;
-#pragma unroll
-    for (int w = 0; w < G::NB; ++w) {
-      uint32_t m = row_mask(o - 32 * w);
-      if constexpr (G::TWO_SIDED) m = w2[end].e ? ~m : m;
-      pop += __popc(m & select_rows<G::K>(&v[w * G::PW], sx));
-    }
-    out2[end] = finish<G>(ix, end ? scr : scl, pop, b2[end], c, X[end], w2[end].e);
-  }
-  L = out2[0];
-  R = out2[1];
-  return mask;
-}
-
-template <class G, int VAR>
-__global__ __launch_bounds__(256) void ftab_diag_kernel(IdxArgs ix, uint32_t fsteps, uint64_t n, uint2* __restrict__ out)
-{
-  for (uint64_t g = (uint64_t) blockIdx.x * 256 + threadIdx.x; g < n; g += (uint64_t) gridDim.x * 256) {
-    const uint64_t v = VAR == 4 ? n - 1 - g : g;
-    uint32_t L = 0, R = ix.bwtsize;
-    uint32_t rec = 0, recx = 0;
-    for (uint32_t t = 0; t < fsteps; ++t) {
-      const uint32_t c = (uint32_t) (v >> (2 * G::K * t)) & (uint32_t) (G::NC - 1);
-      uint32_t sx[2 * G::K];
-      plane_xor<G::K>(c, sx);
-      if constexpr (VAR == 10) {
-        const uint32_t bl = L / (uint32_t) G::D, br = R / (uint32_t) G::D, X = R;
-        const uint32_t mk = lf_pair_probe<G>(ix, L, R, c, sx);
-        if (mk && !rec) {
-          rec = 0x80000000u | (t << 26) | (mk << 22) | ((br & 15u) << 18) | ((bl & 15u) << 14) |
-                ((bl == br) ? 0x2000u : 0u) | (X % (uint32_t) G::D);
-          recx = X;
-        }
-        continue;
-      }
-      if constexpr (VAR == 13) {   /* lf_stream's loads for both ends, then one full wait before any use */
-        const uint32_t bl = L / (uint32_t) G::D, br = R / (uint32_t) G::D;
-        const Where<G> wl = locate<G>(ix, bl, c), wr = locate<G>(ix, br, c);
-        uint32_t vl[G::BMW], vr[G::BMW];
-#pragma unroll
-        for (int i = 0; i < G::BMW; ++i) vl[i] = wl.planes[i];
-#pragma unroll
-        for (int i = 0; i < G::BMW; ++i) vr[i] = wr.planes[i];
-        const uint32_t cl = *wl.cnt, cr = *wr.cnt;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        uint32_t pl_ = 0, pr_ = 0;
-        const int ol = (int) (L - bl * (uint32_t) G::D), orr = (int) (R - br * (uint32_t) G::D);
-#pragma unroll
-        for (int w = 0; w < G::NB; ++w) {
-          uint32_t ml = row_mask(ol - 32 * w), mr = row_mask(orr - 32 * w);
-          if constexpr (G::TWO_SIDED) { ml = wl.e ? ~ml : ml; mr = wr.e ? ~mr : mr; }
-          pl_ += __popc(ml & select_rows<G::K>(&vl[w * G::PW], sx));
-          pr_ += __popc(mr & select_rows<G::K>(&vr[w * G::PW], sx));
-        }
-        const uint32_t nl = finish<G>(ix, cl, pl_, bl, c, L, wl.e);
-        R = finish<G>(ix, cr, pr_, br, c, R, wr.e);
-        L = nl;
-        continue;
-      }
-      if constexpr (VAR == 14) {   /* lf_stream, R's step first */
-        R = lf_stream<G>(ix, R, c, sx);
-        L = lf_stream<G>(ix, L, c, sx);
-        continue;
-      }
-      if constexpr (VAR == 6) {   /* lf_stream vs the dword-load step, first mismatch recorded */
-        const uint32_t l1 = lf_stream<G>(ix, L, c, sx);
-        const uint32_t r1 = lf_stream<G>(ix, R, c, sx);
-        const uint32_t l3 = lf_stream_diag<G, 3>(ix, L, c, sx);
-        const uint32_t r3 = lf_stream_diag<G, 3>(ix, R, c, sx);
-        if (!rec && (l1 != l3 || r1 != r3)) {
-          const uint32_t end = l1 != l3 ? 0u : 1u, X = end ? R : L, b = X / (uint32_t) G::D;
-          const bool e = ac_rule_e<G>(b, c);
-          const uint32_t diff = (end ? r1 - r3 : l1 - l3) & 0xFFu;
-          rec = 0x80000000u | (t << 26) | (end << 25) | ((uint32_t) e << 24) | (c << 22) | ((b & 15u) << 18) |
-                ((X % (uint32_t) G::D) << 12) | ((L / (uint32_t) G::D == R / (uint32_t) G::D) ? 0x800u : 0u) | diff;
-          recx = X;
-        }
-        L = l3;
-        R = r3;
-        continue;
-      }
-      if constexpr (VAR == 1 || VAR == 4) {
-        L = lf_stream<G>(ix, L, c, sx);
-        R = lf_stream<G>(ix, R, c, sx);
-      } else {
-        L = lf_stream_diag<G, VAR>(ix, L, c, sx);
-        R = lf_stream_diag<G, VAR>(ix, R, c, sx);
-      }
-    }
-    out[v] = rec ? make_uint2(rec, recx) : make_uint2(L, R);
-  }
-}
-
 /* ftab construction: [L, R) of every code stream v of ftab_steps K-steps
- * (the search's own first steps, from [0, n+1)). */
+ * (the search's own first steps, from [0, n+1)), each end by lf_stream --
+ * the per-row step of every non-search kernel.  Round 5 detoured this build
+ * through the task kernels' fetch when lf_stream's K = 1, d = 64 AltCounters
+ * form returned wrong entries; the cause was the 16-byte load at 8-byte
+ * alignment LLVM formed from two 8-byte plane loads, which
+ * load_words now keeps out, so the build is lf_stream's again and
+ * test_ftab_table_every_entry checks its tables entry by entry. */
 template <class G>
 __global__ __launch_bounds__(256) void ftab_build_kernel(IdxArgs ix, uint32_t fsteps, uint64_t n,
                                                          uint2* __restrict__ out)
@@ -499,16 +314,8 @@ __global__ __launch_bounds__(256) void ftab_build_kernel(IdxArgs ix, uint32_t fs
       const uint32_t c = (uint32_t) (v >> (2 * G::K * t)) & (uint32_t) (G::NC - 1);
       uint32_t sx[2 * G::K];
       plane_xor<G::K>(c, sx);
-      if constexpr (G::SMALL) {   /* the task kernels' own step (fetch_block, lf_from_block) */
-        Blk<G> kl, kr;
-        fetch_block<G>(ix, L / (uint32_t) G::D, c, kl);
-        fetch_block<G>(ix, R / (uint32_t) G::D, c, kr);
-        L = lf_from_block<G>(ix, kl, L, c, sx);
-        R = lf_from_block<G>(ix, kr, R, c, sx);
-      } else {
-        L = lf_stream<G>(ix, L, c, sx);
-        R = lf_stream<G>(ix, R, c, sx);
-      }
+      L = lf_stream<G>(ix, L, c, sx);
+      R = lf_stream<G>(ix, R, c, sx);
     }
     out[v] = make_uint2(L, R);
   }
@@ -833,21 +640,6 @@ template <class G>
 static hipError_t launch_ftab(const SearchLaunch& a)
 {
   const uint64_t blocks = (a.ftab_n + 255) / 256;
-  if constexpr (G::K == 1 && G::NB == 2 && G::LAY == LAY_AC) {   /* DIAG (round 6 experiment) */
-    const char* e = getenv("KFMI_FTAB_DIAG");
-    const int var = e ? atoi(e) : 0;
-    const dim3 gr(grid_blocks(blocks, 1u << 20));
-#define KFMI_DIAG_CASE(V) \
-    case V: hipLaunchKernelGGL((ftab_diag_kernel<G, V>), gr, dim3(256), 0, a.st, a.ix, a.ftab_steps, a.ftab_n, a.ftab_out); \
-      return hipGetLastError();
-    switch (var) {
-      KFMI_DIAG_CASE(1) KFMI_DIAG_CASE(2) KFMI_DIAG_CASE(3) KFMI_DIAG_CASE(4) KFMI_DIAG_CASE(5)
-      KFMI_DIAG_CASE(6) KFMI_DIAG_CASE(7) KFMI_DIAG_CASE(10) KFMI_DIAG_CASE(12) KFMI_DIAG_CASE(13)
-      KFMI_DIAG_CASE(14) KFMI_DIAG_CASE(15)
-      default: break;
-    }
-#undef KFMI_DIAG_CASE
-  }
   hipLaunchKernelGGL((ftab_build_kernel<G>), dim3(grid_blocks(blocks, 1u << 20)), dim3(256), 0,
                      a.st, a.ix, a.ftab_steps, a.ftab_n, a.ftab_out);
   return hipGetLastError();

@@ -26,10 +26,11 @@
  *          and counters through base2index (:86-99, :184-260, :402-424), and for
  *          K >= 2 the reference's own LF walk (generateOthersBWTs :327-400),
  *          which for non-ACGT text is not a permutation: rows it never visits
- *          keep whatever malloc returned there (:342).  That byte is
- *          KFMI_REF_FILL here (default 0); the reference run under glibc's
- *          MALLOC_PERTURB_=p fills it with p ^ 0xff, which pins the output
- *          (tests/golden/alpha).  For ACGT-only text the three modes agree.
+ *          keep whatever malloc returned there (:342).  This builder writes
+ *          a defined byte there (0, base2index -> A); the reference run under
+ *          glibc's MALLOC_PERTURB_=p holds p ^ 0xff, which pins its output
+ *          (tests/golden/alpha; the test harness patches our image with that
+ *          byte, tests/ref_fill.py).  For ACGT-only text the three modes agree.
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -281,12 +282,6 @@ int32_t kfmi_set_alphabet(const char *name)
   return KFMI_SUCCESS;
 }
 
-uint8_t kfmi_ref_fill(void)
-{
-  const char *e = getenv("KFMI_REF_FILL");
-  return (uint8_t) (e ? strtol(e, NULL, 0) : 0);
-}
-
 /* 2-bit codes of the text: exact A/C/G/T only (acgt; -1 on any other byte), or
  * base2index of every byte (map, ref; ref rejects NUL, which would tie with
  * the '$' sentinel of the raw-byte sort).  *acgt_only: no byte outside A/C/G/T. */
@@ -322,10 +317,11 @@ static inline int64_t ref_mod(int64_t x, int64_t m) { return (x % m + m) % m; } 
  * BWT_0 from the sort, BWT_1..BWT_{k-1} by the walk of generateOthersBWTs
  * (:327-400) on the chunk-32 counters of precalculateBasesPreviousBWT
  * (:262-325, exact 'A'/'C'/'G'/'T' only; any other byte sends the walk to row
- * 0 + its in-chunk count), rows the walk never writes holding `fill`; '$' -> A
+ * 0 + its in-chunk count), rows the walk never writes holding 0 (the
+ * reference: uninitialised memory, :342); '$' -> A
  * at every D_s (:505-509); then counters, planes and dollarBaseBWT through
  * base2index (precalculateBasesKSteps :184-260, bwt2bin :427-455, :518-520). */
-int32_t kfmi_index_ref_walk(const char *text, const uint32_t *sa, uint64_t n, uint32_t k, uint32_t d, uint8_t fill,
+int32_t kfmi_index_ref_walk(const char *text, const uint32_t *sa, uint64_t n, uint32_t k, uint32_t d,
                             kfmi_fmi_t **out)
 {
   const uint64_t rows = n + 1;
@@ -347,7 +343,7 @@ int32_t kfmi_index_ref_walk(const char *text, const uint32_t *sa, uint64_t n, ui
   for (s = 0; s < k; s++) {
     bwt[s] = (uint8_t *) malloc(rows);
     if (!bwt[s]) goto done;
-    if (s) memset(bwt[s], fill, rows);
+    if (s) memset(bwt[s], 0, rows);   /* a defined byte where the walk never writes */
   }
   for (s = 0; s < k; s++) { dpos[s] = 0; dbase[s] = 0; }
   /* BWT_0 with '$' at its primary index (:482-494) */
@@ -514,7 +510,7 @@ int32_t kfmi_build_index_cpu_sa(const char *text, uint64_t n, uint32_t k, uint32
   kfmi_big_free(sym);
   if (!err) {
     if (mode == KFMI_ALPHA_REF && !acgt_only && k > 1)
-      err = kfmi_index_ref_walk(text, sa, n, k, d, kfmi_ref_fill(), (kfmi_fmi_t **) index);
+      err = kfmi_index_ref_walk(text, sa, n, k, d, (kfmi_fmi_t **) index);
     else
       err = kfmi_index_from_sa(codes, sa, n, k, d, (kfmi_fmi_t **) index);
   }

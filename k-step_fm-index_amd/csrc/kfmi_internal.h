@@ -148,8 +148,7 @@ int32_t kfmi_build_index_gpu_sa(const char *text, uint64_t n, uint32_t k, uint32
 /* alphabet modes of the builders (fmi_build.c; KFMI_ALPHABET / kfmi_set_alphabet) */
 enum { KFMI_ALPHA_ACGT = 0, KFMI_ALPHA_MAP = 1, KFMI_ALPHA_REF = 2 };
 int     kfmi_alphabet_mode(void);
-uint8_t kfmi_ref_fill(void);   /* KFMI_REF_FILL: the byte of rows the reference walk never writes */
-int32_t kfmi_index_ref_walk(const char *text, const uint32_t *sa, uint64_t n, uint32_t k, uint32_t d, uint8_t fill,
+int32_t kfmi_index_ref_walk(const char *text, const uint32_t *sa, uint64_t n, uint32_t k, uint32_t d,
                             kfmi_fmi_t **out);
 
 /* suffix array construction, fmi_build.c */

@@ -1,12 +1,23 @@
 """Round-6 ftab experiment: the K=1, d=64 AltCounters jump-start table built
 inside the library by lf_stream variants (KFMI_FTAB_DIAG, kfmi_kernels.h
-ftab_diag_kernel), every 12-mer entry checked against the C oracle.
+ftab_diag_kernel), every 12-mer entry checked against the C oracle.  The
+variant kernels existed only for the experiment (commit "ftab root cause:
+in-library lf_stream variants"); they are gone from the library, which now
+ignores KFMI_FTAB_DIAG -- every row of this script then times the product's
+lf_stream build.  Logs: profiles/r06/ftab_var_r6[a-e].log.
   0 task step (fetch_block + lf_from_block, the round-5 build)
-  1 lf_stream as is (the round-5 failing build)
+  1 lf_stream as is (the round-5 failing build; from r6e on, the fixed one)
   2 lf_stream + s_waitcnt vmcnt(0) after each end's loads
   3 lf_stream with volatile 4-byte plane loads (no merged 16-B load)
   4 lf_stream, entries walked in reverse grid order
   5 lf_stream with agent-scope (sc1) loads
+  6 lf_stream and the dword step side by side, first difference recorded
+  7 lf_stream with 16-byte-aligned loads only
+ 10 both ends' loads in one asm block, registers copied after each partial wait
+ 12 lf_stream with a compiler barrier between the 8-byte plane loads
+ 13 lf_stream's loads, one full vmcnt(0) before any use
+ 14 lf_stream, R's step before L's
+ 15 the old load form (merged 16-byte load at 8-byte alignment), control
 """
 import os, sys, time, numpy as np
 sys.path.insert(0, "tests"); sys.path.insert(0, "k-step_fm-index_amd"); sys.path.insert(0, ".")

@@ -9,7 +9,8 @@ IUPAC letters -- and builds it with the reference tool and with this build's
 host builder (and GPU builder in the GPU suite) in 'ref' mode; the index files
 must be byte-identical.  For K >= 2 the reference leaves rows of BWT_1..
 uninitialised on such texts (tests/test_alphabet.py), so it runs under glibc's
-MALLOC_PERTURB_=p and this build takes KFMI_REF_FILL = p ^ 0xff, the byte the
+MALLOC_PERTURB_=p and the product's image (whose builder writes a defined
+byte there) is patched by tests/ref_fill.py with p ^ 0xff, the byte the
 fresh allocation then holds (tests/golden/make_golden_alpha.py) -- with the
 thread cache off (GLIBC_TUNABLES=glibc.malloc.tcache_count=0): a small chunk
 the cache hands back is not perturbed and holds what its last owner left
@@ -22,6 +23,7 @@ import subprocess
 import numpy as np
 import pytest
 
+import ref_fill
 from util import REPO
 
 REF = REPO / "oracle" / "_ref"
@@ -95,43 +97,43 @@ def _reference_md5(tmp_path, k, d, fasta, n, pert):
     return hashlib.md5((tmp_path / f"ref.fa.{n}.{d}fmi{k}steps.fmi").read_bytes()).hexdigest()
 
 
-def _ours(K, tmp_path, k, d, n, pert, gpu, monkeypatch):
+def _ours(K, tmp_path, k, d, n, pert, gpu):
     L = K.load()
     ref = ctypes.c_void_p()
     assert L.loadRef(str(tmp_path / "ref.fa").encode(), n, ctypes.byref(ref)) == 0
     r = _Ref.from_address(ref.value)
     text = ctypes.string_at(r.p, r.size)
     L.freeReference(ctypes.byref(ref), None)
-    if pert is not None:
-        monkeypatch.setenv("KFMI_REF_FILL", str(pert ^ 0xFF))
     idx = K.Index.build(text, k=k, d=d, gpu=gpu)
-    h = hashlib.md5(idx.image().tobytes()).hexdigest()
+    img = idx.image()
+    if pert is not None:   # the reference's unvisited rows under MALLOC_PERTURB_ (tests/ref_fill.py)
+        img = ref_fill.patch(img, text, ref_fill.full_sa(K, text, k, d), pert ^ 0xFF)
+    h = hashlib.md5(img.tobytes()).hexdigest()
     idx.close()
     return h
 
 
 @pytest.fixture
-def ref_mode(kfmi_mod, monkeypatch):
-    monkeypatch.delenv("KFMI_REF_FILL", raising=False)
+def ref_mode(kfmi_mod):
     kfmi_mod.set_alphabet("ref")
     yield kfmi_mod
     kfmi_mod.set_alphabet(None)
 
 
 @pytest.mark.parametrize("i", range(WORLDS))
-def test_alphabet_world_host(ref_mode, tmp_path, monkeypatch, i):
+def test_alphabet_world_host(ref_mode, tmp_path, i):
     k, d, fasta, n, pert = world(i)
     want = _reference_md5(tmp_path, k, d, fasta, n, pert)
-    assert _ours(ref_mode, tmp_path, k, d, n, pert, False, monkeypatch) == want, dict(world=i, k=k, d=d, n=n, p=pert)
+    assert _ours(ref_mode, tmp_path, k, d, n, pert, False) == want, dict(world=i, k=k, d=d, n=n, p=pert)
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("i", range(WORLDS))
-def test_alphabet_world_gpu(ref_mode, tmp_path, monkeypatch, i):
+def test_alphabet_world_gpu(ref_mode, tmp_path, i):
     K = ref_mode
     if K.device_count() < 1:
         pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
     K.set_device(0)
     k, d, fasta, n, pert = world(i)
     want = _reference_md5(tmp_path, k, d, fasta, n, pert)
-    assert _ours(K, tmp_path, k, d, n, pert, True, monkeypatch) == want, dict(world=i, k=k, d=d, n=n, p=pert)
+    assert _ours(K, tmp_path, k, d, n, pert, True) == want, dict(world=i, k=k, d=d, n=n, p=pert)

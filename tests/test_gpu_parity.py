@@ -376,11 +376,8 @@ def test_split_gathers_equal_oracle(gpu, oracle_mod, random_index, backend, spli
 def test_ftab_table_every_entry(gpu, random_index, backend, k, d, bases):
     """Every entry of a freshly built jump-start table, three builds: the
     bases-long read of each code searched with the table (one lookup, no step)
-    equals the search without it.  Round 5 found the table of task-ac at K = 1,
-    d = 64 wrong in ~40 of 4^12 entries per build, different entries each time,
-    while built with its own per-end step (lf_stream); it is now built with the
-    task kernels' step (fetch_block + lf_from_block) and checked here entry by
-    entry."""
+    equals the search without it.  The tables are built by lf_stream (DESIGN.md
+    5a; the 3 Mbase K = 1 AltCounters case is test_ftab_lf_stream_k1_ac_table)."""
     text, idxs = random_index
     if (k, d) not in idxs:
         idxs[(k, d)] = gpu.Index.build(text, k=k, d=d)
@@ -399,3 +396,32 @@ def test_ftab_table_every_entry(gpu, random_index, backend, k, d, bases):
             assert bad.size == 0, (backend, k, d, bases, build, int(bad.size), int(bad[0] // 2))
     finally:
         gpu.set_ftab(0)
+
+
+def test_ftab_lf_stream_k1_ac_table(gpu, oracle_mod):
+    """The round-5 intermittent table, at the size it showed on: a 3 Mbase
+    random text, K = 1, d = 64, tag 201 (task-ac), 12-base table (4^12
+    entries) built inside the library by lf_stream, four fresh builds, every
+    entry equal to the C oracle's search of that 12-mer
+    (fmIndexCPUBaseline-AltCounters.c:218-266).  The old load form (a 16-byte
+    load at 8-byte alignment, consumed under a partial vmcnt wait) gave 15-69
+    wrong entries in every build on the same code path (profiles/r06/
+    ftab_var_r6*.log, var 1 / 15); load_words keeps it out."""
+    rng = np.random.default_rng(2026)
+    text = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), size=3_000_001).tobytes()
+    idx = gpu.Index.build(text, k=1, d=64)
+    acimg = idx.alt_counters()[0].image()
+    codes = np.arange(4 ** 12, dtype=np.uint32)
+    q = np.frombuffer(b"ACGT", np.uint8)[(codes[:, None] >> (2 * np.arange(11, -1, -1))[None, :]) & 3].copy()
+    want, _ = oracle_mod.search(acimg, q)
+    try:
+        for build in range(4):
+            idx.free_gpu()
+            gpu.set_ftab(12)
+            got = gpu.search_array(idx, q, "task-ac")
+            gpu.set_ftab(0)
+            bad = np.flatnonzero(got != want)
+            assert bad.size == 0, (build, int(bad.size), int(bad[0] // 2), got[bad[0]], want[bad[0]])
+    finally:
+        gpu.set_ftab(0)
+        idx.close()
