@@ -101,8 +101,8 @@ def parse():
                    help="reads per rank checked against the CPU oracle after the timed region (0 = skip)")
     p.add_argument("--cpu-port-only", action="store_true",
                    help="time only our restatement, not the reference's CPU binary (oracle/_ref)")
-    p.add_argument("--variants", default="task,coop,task-ac,coop-ac,task-ac128,coop-ac128,task-ac-mid,coop-ac-mid,"
-                                         "task-packed,coop-packed,task-mid,coop-mid,task-mid+ftab14,task-mid+ftab16",
+    p.add_argument("--variants", default="task,coop,task-ac,coop-ac,task-ac-mid,coop-ac-mid,"
+                                         "task-mid,coop-mid,task-mid+ftab14,task-mid+ftab16",
                    help="other backends timed on rank 0 at N=1 (empty = none)")
     p.add_argument("--variant-steps", type=int, default=5)
     p.add_argument("--config5-queries", type=int, default=10_000_000,
@@ -707,9 +707,8 @@ VARIANTS_PMC = next((p for p in (ROOT / "profiles" / r / "traffic_variants.json"
 VARIANTS_PMC_Q150 = ROOT / "profiles" / "r05" / "traffic_variants_q150.json"
 
 # backend -> layout id of its kernels' Geo<K, NB, LAY> (kfmi_device.h Layout)
-LAYOUT = {"task": 0, "coop": 0, "task-ac": 1, "coop-ac": 1, "task-packed": 2, "coop-packed": 2, "task-mid": 3,
-          "coop-mid": 3, "task-ac128": 4, "coop-ac128": 4, "task-ac-mid": 5, "coop-ac-mid": 5, "task-grp": 6,
-          "coop-grp": 6}
+LAYOUT = {"task": 0, "coop": 0, "task-ac": 1, "coop-ac": 1, "task-mid": 3, "coop-mid": 3, "task-ac-mid": 5,
+          "coop-ac-mid": 5, "task-grp": 6, "coop-grp": 6}   # 2 and 4: the retired packed / ac128 layouts
 
 
 def kernel_prefix(backend: str, k: int, d: int, qlen: int) -> str:
@@ -763,7 +762,7 @@ def variant_roofline(blocks: int, b_lf: int, lf_ms: float, a, backend: str, pmc:
         # no ceiling fraction here: the probe's ceiling is measured on uniformly
         # random 64/128-B lines, and other layouts' request mixes (64-B lines,
         # an L2-resident superblock table, 96 GB tables) sit on either side of
-        # it -- coop-packed issues 58.6 G/s, coop-grp 49.9
+        # it -- the retired coop-packed issued 58.6 G/s, coop-grp 49.9
         out.update({"fabric_read_requests_per_launch": req,
                     "line_requests_per_query": round(req / (queries or a.queries), 2),
                     "line_requests_G_per_s": round(req / (lf_ms / 1e3) / 1e9, 2),
@@ -1444,7 +1443,7 @@ def main():
         from oracle import oracle
         t = time.perf_counter()
         sel = np.linspace(0, reads.shape[0] - 1, ns_par).astype(np.int64)
-        ac = a.backend in ("task-ac", "coop-ac", "task-ac128", "coop-ac128")
+        ac = a.backend in ("task-ac", "coop-ac")
         img_idx = idx.alt_counters()[0] if ac else None
         want, _ = oracle.search(img_idx.image() if ac else img, reads[sel],
                                 nthreads=max(1, cpu_effective() // D.world))
@@ -1506,7 +1505,7 @@ def main():
     c5 = None
     if a.config5_queries > 0:
         c5 = config5_leg(D, idx, text, a.backend, a.config5_qlen, a.config5_queries, a.steps, 5,
-                         a.backend in ("task-ac", "coop-ac", "task-ac128", "coop-ac128", "task-ac-mid",
+                         a.backend in ("task-ac", "coop-ac", "task-ac-mid",
                                        "coop-ac-mid"), oracle_img=img, ingest=ingest_on, k=a.k, d=a.d, pmc=pmc150)
         log(f"rank {D.rank}: config #5 leg {c5}")
         log(f"config #5 leg: {c5.get('mqps')} Mq/s", brief=True)

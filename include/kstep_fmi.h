@@ -132,11 +132,8 @@ char    *errorCommon(int32_t e);
  *   "coop"        Coop-{1,2}Step   : wave64 cooperative gather into LDS     (tag 101 semantics)
  *   "task-ac"     Task-2Step-AltCounters                                    (tag 201 semantics)
  *   "coop-ac"     Coop-2Step-AltCounters                                    (tag 201 semantics)
- *   "task-packed" task-per-query on the 64-byte-line packed layout          (tag 101 semantics)
- *   "coop-packed" wave64 cooperative gather on the packed layout            (tag 101 semantics)
  *   "task-mid"    task-per-query on the MID128 layout: one 128-byte line per LF (tag 101 semantics)
  *   "coop-mid"    wave64 cooperative gather on the MID128 layout              (tag 101 semantics)
- *   "task-ac128" / "coop-ac128"  one 128-byte line per block, both AC counters (tag 201 semantics)
  *   "task-grp" / "coop-grp"   K = 3 and 4 indexes (d = 64): one 128-byte line per (block,
  *                 16-code group) holding the block's planes and those 16 counters -- one line per
  *                 LF, 25 K-steps for 100 bases at K = 4; 4 (K = 3) or 16 (K = 4) lines per block
@@ -144,6 +141,9 @@ char    *errorCommon(int32_t e);
  *   "task-ac-mid" / "coop-ac-mid" the MID128 lines with AltCounters semantics: the AltCounters
  *                 step only past the last real block, from the tfmiAC sentinel (tag 201 semantics;
  *                 built from a tag 100/101 file, an AC file returns 101)
+ * ("task-packed" / "coop-packed" and "task-ac128" / "coop-ac128", layouts that
+ * lost to task-mid / task-ac on every measurement, were retired in round 6:
+ * kfmi_set_backend returns KFMI_E_BAD_ARGUMENT for them.)
  * The default comes from KFMI_BACKEND, else "task-mid" -- and "coop-grp" for a
  * K = 3 or 4 index while neither KFMI_BACKEND nor kfmi_set_backend has chosen one
  * (kfmi_get_backend still names the selection).  transferCPUtoGPU

@@ -71,25 +71,18 @@ __device__ __forceinline__ const uint8_t* coop_chunk_addr(const IdxArgs& ix, uin
     if (k < C::BC) return base + lb + 16 * k;
     return base + lb + (G::BMW + ((c % G::NCG) & ~3u)) * 4;
   }
-  if constexpr (G::LAY == LAY_AC128) {
-    if (k < C::BC) return base + eb + 4 * k * 4;
-    const bool e = ((b & 1u) != 0) == (c < (uint32_t) G::HALF);
-    return base + eb + (G::BMW + (e ? G::HALF : 0) + ((c & (G::HALF - 1)) & ~3u)) * 4;
-  }
   if (k < C::BC) return base + eb + (G::BOFF + 4 * k) * 4;
   if constexpr (G::LAY == LAY_INTER) {
     return base + eb + (G::BMW + (c & ~3u)) * 4;
-  } else if constexpr (G::LAY == LAY_AC) {
+  } else {   // LAY_AC
     const bool e = ((b & 1u) != 0) == (c < (uint32_t) G::HALF);
     return base + (uint64_t) (b + (e ? 1u : 0u)) * (G::EW * 4) + ((c & (G::HALF - 1)) & ~3u) * 4;
-  } else {
-    return base + eb + 4 * G::BMW + 2 * (c & ~7u);
   }
 }
 
 template <class G>
 __device__ __forceinline__ uint32_t coop_lf(const IdxArgs& ix, const uint8_t* slot, uint32_t b, uint32_t X,
-                                            uint32_t c, const uint32_t (&sx)[2 * G::K], uint32_t sbase)
+                                            uint32_t c, const uint32_t (&sx)[2 * G::K])
 {
   using C = CoopCfg<G>;
   const int o = (int) (X - b * (uint32_t) G::D);
@@ -127,11 +120,7 @@ __device__ __forceinline__ uint32_t coop_lf(const IdxArgs& ix, const uint8_t* sl
       pop += __popc(m & select_rows<G::K>(&pl[w * G::PW], sx));
     }
   }
-  uint32_t cnt;
-  if constexpr (G::LAY == LAY_PACKED)
-    cnt = sbase + reinterpret_cast<const uint16_t*>(slot + 16 * C::BC)[c & 7u];
-  else
-    cnt = reinterpret_cast<const uint32_t*>(slot + 16 * C::BC)[c & 3u];
+  const uint32_t cnt = reinterpret_cast<const uint32_t*>(slot + 16 * C::BC)[c & 3u];
   if constexpr (G::LAY == LAY_MIDAC)
     if (b >= ix.ac_tail_b0) return ac_tail_step<G>(ix, b, c, X, pop, all);
   return finish<G>(ix, cnt, pop, b, c, X, e);
@@ -241,7 +230,6 @@ __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, 
     }
   }
   uint32_t L = 0, R = ix.bwtsize;
-  constexpr int S = sb_shift_for(G::D);
   uint32_t skip = 0;
   if (ix.ftab && steps >= ix.ftab_steps) {   // wave-uniform: jump start from the ftab
     skip = ix.ftab_steps;
@@ -298,11 +286,7 @@ __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, 
       tab[lane] = (Desc) bl * (Desc) G::NC + c;
       if (needR) tab[slotR] = (Desc) br * (Desc) G::NC + c;
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      uint32_t sbL = 0, sbR = 0;
-      if constexpr (G::LAY == LAY_PACKED) {
-        sbL = ix.sb[(uint64_t) (bl >> S) * G::NC + c];
-        sbR = ix.sb[(uint64_t) (br >> S) * G::NC + c];
-      }
+      uint32_t cwL = 0, cwR = 0;   /* NBR: the counter word of an end that steps from block b-1 */
       const uint32_t rounds = (nreq + C::RPR - 1) / C::RPR;
       for (uint32_t r = 0; r < rounds; ++r) {
         const uint32_t s = r * C::RPR + g;
@@ -362,7 +346,7 @@ __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, 
                      ".Lcc1_%=:\n"
                      "s_mov_b64 exec, %[sv]\n"
                      "s_waitcnt vmcnt(0)\n"
-                     : [cl] "=&v"(sbL), [cr] "=&v"(sbR), [sv] "=&s"(sv), [gm] "=&s"(gm)
+                     : [cl] "=&v"(cwL), [cr] "=&v"(cwR), [sv] "=&s"(sv), [gm] "=&s"(gm)
                      : [al] "v"(acL), [ar] "v"(acR), [ml] "s"(mpl), [mr] "s"(mpr)
                      : "memory", "scc");
       } else {
@@ -378,13 +362,13 @@ __global__ __launch_bounds__(64 * CoopCfg<G>::WPB) void coop_kernel(IdxArgs ix, 
          * of 4 words) */
         const uint8_t* sL = wl + lane * C::SLOT;
         const uint8_t* sR = wl + (needR ? slotR : (uint32_t) lane) * C::SLOT;
-        const uint32_t cL = pL ? sbL : reinterpret_cast<const uint32_t*>(sL + 16 * C::BC)[c & 3u];
-        const uint32_t cR = needR ? (pR ? sbR : reinterpret_cast<const uint32_t*>(sR + 16 * C::BC)[c & 3u]) : cL;
+        const uint32_t cL = pL ? cwL : reinterpret_cast<const uint32_t*>(sL + 16 * C::BC)[c & 3u];
+        const uint32_t cR = needR ? (pR ? cwR : reinterpret_cast<const uint32_t*>(sR + 16 * C::BC)[c & 3u]) : cL;
         nL = coop_lf_nbr<G>(ix, sL, bl, L, c, sx, cL, eL, pL);
         nR = coop_lf_nbr<G>(ix, sR, br, R, c, sx, cR, needR ? eR : eL, needR ? pR : pL);
       } else {
-        nL = coop_lf<G>(ix, wl + lane * C::SLOT, bl, L, c, sx, sbL);
-        nR = coop_lf<G>(ix, wl + (needR ? slotR : (uint32_t) lane) * C::SLOT, br, R, c, sx, needR ? sbR : sbL);
+        nL = coop_lf<G>(ix, wl + lane * C::SLOT, bl, L, c, sx);
+        nR = coop_lf<G>(ix, wl + (needR ? slotR : (uint32_t) lane) * C::SLOT, br, R, c, sx);
       }
       L = nL;
       R = nR;

@@ -14,8 +14,6 @@
  *   LAY_INTER  : tag-101 entries as in the file, [planes(w,s,t) | cnt[NC]] u32
  *   LAY_AC     : tag-201 entries as in the file, [cnt_half[NC/2] | planes(w,s,t)];
  *                e = (b odd & c < NC/2) | (b even & c >= NC/2)
- *   LAY_PACKED : one power-of-two line per d-block, [planes(w,s,t) | u16 delta[NC]],
- *                cnt_b[c] = sb[b >> SB_SHIFT][c] + delta_b[c] (sb: small, cache-resident)
  *   LAY_MID    : one power-of-two line per PAIR of d-blocks (2d rows),
  *                [planes of block 2p | planes of block 2p+1 | cnt_{2p+1}[NC]]:
  *                every counter sits at the pair's midpoint, so an even block is
@@ -36,11 +34,11 @@
  *                d=64: 64 B of planes + 64 B of counters = one 128-B line per
  *                LF, 25 K-steps for a 100-bp read instead of 50 -- in 16 x
  *                the index memory (96 GB at 3 Gbase, which one MI355X holds).
- *   LAY_AC128  : tag-201 (AltCounters) semantics, one power-of-two line per
- *                d-block: [planes of block b | cnt_half_b | cnt_half_{b+1}],
- *                so both counters the AC rule may pick (entry b or b+1,
- *                fmIndexCPUBaseline-AltCounters.c:218-225) sit in the block's
- *                own line.  K=2, d=64: 96 B in a 128-B line, one request per LF.
+ * Retired in round 6 (dominated on every measurement): the
+ * packed layout (2: u16 counter deltas + superblock counters, 74 lines per
+ * 100-bp read against MID128's 58) and AC128 (4: tag-201 semantics in one
+ * 128-B line per block, 1,011 Mq/s against task-ac's 1,037-1,067 on the
+ * reference's own tag-201 layout).  Their numbers stay unused.
  */
 #ifndef KFMI_DEVICE_H_
 #define KFMI_DEVICE_H_
@@ -50,8 +48,7 @@
 
 namespace kfmi {
 
-enum Layout : int { LAY_INTER = 0, LAY_AC = 1, LAY_PACKED = 2, LAY_MID = 3, LAY_AC128 = 4, LAY_MIDAC = 5,
-                    LAY_GRP = 6 };
+enum Layout : int { LAY_INTER = 0, LAY_AC = 1, LAY_MID = 3, LAY_MIDAC = 5, LAY_GRP = 6 };
 
 __host__ __device__ constexpr int pow2ceil(int x) { int p = 1; while (p < x) p <<= 1; return p; }
 
@@ -70,17 +67,14 @@ struct Geo {
   static constexpr int NGRP = NC / NCG;                   // lines per block (LAY_GRP)
   static constexpr int EW = LAY == LAY_INTER ? BMW + NC
                           : LAY == LAY_AC    ? HALF + BMW
-                          : LAY == LAY_PACKED ? pow2ceil(BMW + NC / 2)
-                          : LAY == LAY_AC128  ? pow2ceil(BMW + NC)
                           : LAY == LAY_GRP    ? pow2ceil(BMW + NCG)
                           : pow2ceil(2 * BMW + NC);
   static constexpr int BOFF = LAY == LAY_AC ? HALF : 0;   // first bitmap word
-  static constexpr int DELTA16 = 2 * BMW;                 // first u16 delta (packed)
   static constexpr int MIDCNT = 2 * BMW;                  // first mid counter (mid)
-  static constexpr bool ACRULE = LAY == LAY_AC || LAY == LAY_AC128;   // AltCounters direction rule
+  static constexpr bool ACRULE = LAY == LAY_AC;          // AltCounters direction rule
   static constexpr int SPW = 32 / (2 * K);                // K-steps per packed query word
   static constexpr bool SMALL = BMW <= 16;                // whole bitmap fits in registers
-  static constexpr bool TWO_SIDED = LAY == LAY_AC || LAY == LAY_MID || LAY == LAY_AC128 || LAY == LAY_MIDAC;
+  static constexpr bool TWO_SIDED = LAY == LAY_AC || LAY == LAY_MID || LAY == LAY_MIDAC;
   static constexpr bool MIDLINES = LAY == LAY_MID || LAY == LAY_MIDAC;   // pairs of blocks per line
   // the reference's own layouts (tag 101 / 201), register-resident blocks: a
   // block whose counter lies past the 128-B line of its planes is counted
@@ -90,14 +84,6 @@ struct Geo {
   // (BOFF + EW + BMW words: K=2 d=64 and K=1 d<=128)
   static constexpr bool NEIGHBOR = (LAY == LAY_INTER || LAY == LAY_AC) && SMALL && BOFF + EW + BMW <= 32;
 };
-
-// Superblock shift of the packed layout: the largest S with (2^S - 1) * d <= 65535.
-__host__ __device__ constexpr int sb_shift_for(int d)
-{
-  int s = 0;
-  while (((1 << (s + 1)) - 1) * d <= 65535) ++s;
-  return s;
-}
 
 struct DollarArgs {
   uint32_t dpos[4];   // dollarPositionBWT[s], s < K <= 4
@@ -109,7 +95,6 @@ struct DollarArgs {
 
 struct IdxArgs {
   const uint32_t* __restrict__ ent;   // entries / lines (layout per backend)
-  const uint32_t* __restrict__ sb;    // packed layout: superblock counters [nsb][NC]
   uint32_t bwtsize;
   DollarArgs dl;
   // ftab (Bowtie-style jump start): [L, R) after the first ftab_steps K-steps,
@@ -366,7 +351,7 @@ __device__ __forceinline__ int dollar_fix(const DollarArgs& dl, uint32_t b, uint
 template <class G>
 struct Where {
   const uint32_t* planes;
-  const uint32_t* cnt;      // counter word (unused for packed: see delta/sb)
+  const uint32_t* cnt;      // counter word
   bool e;                   // backward (two-sided layouts)
   bool prev = false;        // NEIGHBOR: counted forward from block b-1 (cnt is cnt_{b-1}[c])
   const uint32_t* pplanes = nullptr;   // NEIGHBOR, prev: the planes of block b-1
@@ -425,16 +410,6 @@ __device__ __forceinline__ Where<G> locate(const IdxArgs& ix, uint32_t b, uint32
     w.e = ((b & 1u) != 0) == (c < (uint32_t) G::HALF);
     w.planes = ent + G::BOFF;
     w.cnt = ix.ent + (uint64_t) (b + (w.e ? 1u : 0u)) * G::EW + (c & (G::HALF - 1));
-  } else if constexpr (G::LAY == LAY_AC128) {
-    const uint32_t* line = ix.ent + (uint64_t) b * G::EW;
-    w.e = ((b & 1u) != 0) == (c < (uint32_t) G::HALF);
-    w.planes = line;
-    w.cnt = line + G::BMW + (w.e ? G::HALF : 0) + (c & (G::HALF - 1));
-  } else if constexpr (G::LAY == LAY_PACKED) {
-    const uint32_t* ent = ix.ent + (uint64_t) b * G::EW;
-    w.planes = ent;
-    w.cnt = nullptr;
-    w.e = false;
   } else if constexpr (G::LAY == LAY_GRP) {
     const uint32_t* line = ix.ent + ((uint64_t) b * G::NGRP + c / G::NCG) * G::EW;
     w.planes = line;
@@ -452,13 +427,8 @@ __device__ __forceinline__ Where<G> locate(const IdxArgs& ix, uint32_t b, uint32
 template <class G, bool NT = false>
 __device__ __forceinline__ uint32_t load_counter(const IdxArgs& ix, const Where<G>& w, uint32_t b, uint32_t c)
 {
-  if constexpr (G::LAY == LAY_PACKED) {
-    constexpr int S = sb_shift_for(G::D);
-    const uint32_t* ent = ix.ent + (uint64_t) b * G::EW;
-    return ix.sb[(uint64_t) (b >> S) * G::NC + c] + reinterpret_cast<const uint16_t*>(ent)[G::DELTA16 + c];
-  } else {
-    return ld1<NT>(w.cnt);
-  }
+  (void) ix; (void) b; (void) c;
+  return ld1<NT>(w.cnt);
 }
 
 // AltCounters semantics past the last real block: the tfmiAC file ends with a
@@ -472,7 +442,7 @@ __device__ __forceinline__ uint32_t load_counter(const IdxArgs& ix, const Where<
 // AltCounters-semantics step is therefore capped at (S+2)*d - 1, which keeps
 // every defined result and keeps the block index at most S+1, whose planes
 // and counters every layout holds as zero padding (LAY_AC: entries S+1, S+2;
-// LAY_AC128: line S+1; LAY_MIDAC: the MID padding line and ac_tail row 2).
+// LAY_MIDAC: the MID padding line and ac_tail row 2).
 template <class G>
 __device__ __forceinline__ uint32_t ac_clamp(const IdxArgs& ix, uint32_t v)
 {

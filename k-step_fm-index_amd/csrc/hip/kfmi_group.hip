@@ -115,13 +115,12 @@ static int32_t replicate_index(const kfmi_dev_index* src, int dev, hipStream_t s
   di->nentries = src->nentries;
   di->dl = src->dl;
   di->ent_bytes = src->ent_bytes;
-  di->sb_bytes = src->sb_bytes;
   di->sa_bytes = src->sa_bytes;
   di->sa_log2 = src->sa_log2;
   di->sa_gen = src->sa_gen;
   di->ac_tail_b0 = src->ac_tail_b0;
   struct Buf { uint32_t* const* from; uint32_t** to; uint64_t bytes; };
-  const Buf bufs[4] = {{&src->ent, &di->ent, src->ent_bytes}, {&src->sb, &di->sb, src->sb_bytes},
+  const Buf bufs[3] = {{&src->ent, &di->ent, src->ent_bytes},
                        {&src->sa, &di->sa, src->sa ? src->sa_bytes + 4 : 0},
                        {&src->ac_tail, &di->ac_tail, src->ac_tail ? 16ull * (1u << (2 * src->K)) : 0}};
   for (const Buf& b : bufs) {

@@ -62,7 +62,7 @@ __device__ __forceinline__ void fetch_ends(const IdxArgs& ix, const uint32_t (&L
  */
 template <class G>
 struct X4 {
-  static constexpr bool OK = G::SMALL && G::BMW == 8 && G::LAY != LAY_PACKED && G::BOFF % 4 == 0 && G::EW % 4 == 0;
+  static constexpr bool OK = G::SMALL && G::BMW == 8 && G::BOFF % 4 == 0 && G::EW % 4 == 0;
 };
 
 #define KFMI_X4_BODY(T)                                      \
@@ -414,7 +414,7 @@ __global__ __launch_bounds__(256) void derive_codes_kernel(IdxArgs ix, uint64_t 
 }
 
 /* 128-B lines one LF end's task-kernel fetch touches (fetch_block: the
- * planes, the counter word -- the superblock word for PACKED -- and, when the
+ * planes, the counter word and, when the
  * step is counted forward from block b-1 (line_local_prev), b-1's planes).
  * Returns how many ids it appended to ln; *extra = 1 when the counter lies
  * outside the planes' line(s), *prev = 1 for a line-local step. */
@@ -429,13 +429,7 @@ __device__ __forceinline__ int lf_lines(const IdxArgs& ix, uint32_t X, uint32_t 
   const uint64_t p0 = (uint64_t) (uintptr_t) w.planes >> 7, p1 = (uint64_t) (uintptr_t) (w.planes + G::BMW - 1) >> 7;
   ln[n++] = p0;
   if (p1 != p0) ln[n++] = p1;
-  uint64_t cl;
-  if constexpr (G::LAY == LAY_PACKED) {
-    constexpr int S = sb_shift_for(G::D);
-    cl = (uint64_t) (uintptr_t) (ix.sb + (uint64_t) (b >> S) * G::NC + c) >> 7;
-  } else {
-    cl = (uint64_t) (uintptr_t) w.cnt >> 7;
-  }
+  const uint64_t cl = (uint64_t) (uintptr_t) w.cnt >> 7;
   *extra = (cl != p0 && cl != p1) ? 1u : 0u;
   if (*extra) ln[n++] = cl;
   *prev = w.prev ? 1u : 0u;

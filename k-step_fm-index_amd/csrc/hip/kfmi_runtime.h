@@ -40,8 +40,6 @@ struct kfmi_dev_index {
   kfmi::DollarArgs dl{};
   uint32_t* ent = nullptr;     /* device entries */
   uint64_t ent_bytes = 0;
-  uint32_t* sb = nullptr;      /* packed: superblock counters */
-  uint64_t sb_bytes = 0;
   uint32_t* sa = nullptr;      /* locate: row-sampled suffix array */
   uint64_t sa_bytes = 0;
   uint32_t sa_log2 = 0, sa_gen = 0;

@@ -9,7 +9,7 @@
  * kfmi_stream.hip.
  *
  * Semantics: results are bit-identical to the reference CPU searchers
- * (fmIndexCPUBaseline.c:157-292 for task/coop/packed, -AltCounters.c:145-310
+ * (fmIndexCPUBaseline.c:157-292 for task/coop/mid, -AltCounters.c:145-310
  * for the *-ac backends) -- not to the reference .cu files, which carry the
  * defects B1-B4 of SURVEY.md Appendix B.
  */
@@ -35,8 +35,7 @@ namespace kfmi {
 /* ------------------------------------------------------------------------ */
 
 static const char* kBackendNames[KFMI_BK_COUNT] = {
-    "task", "coop", "task-ac", "coop-ac", "task-packed", "coop-packed", "task-mid", "coop-mid",
-    "task-ac128", "coop-ac128", "task-ac-mid", "coop-ac-mid", "task-grp", "coop-grp"};
+    "task", "coop", "task-ac", "coop-ac", "task-mid", "coop-mid", "task-ac-mid", "coop-ac-mid", "task-grp", "coop-grp"};
 
 static thread_local int t_backend = -1;
 static thread_local bool t_backend_implicit = true;   /* neither KFMI_BACKEND nor kfmi_set_backend chose it */
@@ -55,7 +54,6 @@ static int backend_from_name(const char* n)
   if (!strcmp(n, "coop-2step") || !strcmp(n, "coop-1step")) return KFMI_BK_COOP;
   if (!strcmp(n, "task-2step-ac")) return KFMI_BK_TASK_AC;
   if (!strcmp(n, "coop-2step-ac")) return KFMI_BK_COOP_AC;
-  if (!strcmp(n, "packed")) return KFMI_BK_TASK_PACKED;
   return -1;
 }
 
@@ -80,8 +78,7 @@ int backend_for(uint32_t K)
 
 extern "C" uint32_t kfmi_backend_tag(kfmi_backend_t b)
 {
-  return (b == KFMI_BK_TASK_AC || b == KFMI_BK_COOP_AC || b == KFMI_BK_TASK_AC128 || b == KFMI_BK_COOP_AC128 ||
-          b == KFMI_BK_TASK_AC_MID || b == KFMI_BK_COOP_AC_MID)
+  return (b == KFMI_BK_TASK_AC || b == KFMI_BK_COOP_AC || b == KFMI_BK_TASK_AC_MID || b == KFMI_BK_COOP_AC_MID)
              ? 201u : 101u;
 }
 
@@ -364,35 +361,6 @@ __global__ __launch_bounds__(256) void pack_queries_kernel(const uint8_t* __rest
 }
 
 
-/* ------------------------------------------------------------------------ */
-/* packed layout construction from tag-101 entries (on the device)          */
-/* ------------------------------------------------------------------------ */
-
-template <int K, int NB>
-__global__ __launch_bounds__(256) void build_packed_kernel(const uint32_t* __restrict__ inter, uint32_t nentries,
-                                                           uint32_t* __restrict__ packed, uint32_t* __restrict__ sb,
-                                                           uint32_t* __restrict__ overflow)
-{
-  using GI = Geo<K, NB, LAY_INTER>;
-  using GP = Geo<K, NB, LAY_PACKED>;
-  constexpr int S = sb_shift_for(GI::D);
-  const uint64_t b = (uint64_t) blockIdx.x * 256 + threadIdx.x;
-  if (b >= nentries) return;
-  const uint32_t* src = inter + b * GI::EW;
-  const uint32_t* sup = inter + ((b >> S) << S) * GI::EW;
-  uint32_t* dst = packed + b * GP::EW;
-  for (int i = 0; i < GI::BMW; ++i) dst[i] = src[i];
-  uint16_t* d16 = reinterpret_cast<uint16_t*>(dst);
-  for (int c = 0; c < GI::NC; ++c) {
-    const uint32_t delta = src[GI::BMW + c] - sup[GI::BMW + c];
-    if (delta > 0xFFFFu) atomicAdd(overflow, 1u);
-    d16[GP::DELTA16 + c] = (uint16_t) delta;
-  }
-  for (int i = GI::BMW + GI::NC / 2; i < GP::EW; ++i) dst[i] = 0;
-  if ((b & ((1u << S) - 1)) == 0)
-    for (int c = 0; c < GI::NC; ++c) sb[(b >> S) * GI::NC + c] = src[GI::BMW + c];
-}
-
 /* MID layout construction from tag-101 entries: line p holds the planes of
  * blocks 2p and 2p+1 and the counters sampled at its midpoint (= cnt_{2p+1}).
  * The last odd-count line and one padding line take host-computed counters
@@ -449,29 +417,6 @@ __global__ __launch_bounds__(256) void build_grp_kernel(const uint32_t* __restri
   for (int i = GI::BMW + GG::NCG; i < GG::EW; ++i) dst[i] = 0;
 }
 
-/* AC128 layout construction from tag-201 entries (E + 1 of them, the last
- * being the sentinel): line b = [planes of b | cnt_half_b | cnt_half_{b+1}],
- * the counters of entries past the sentinel read as 0 (as the AC backend's
- * zero padding entries do).  Lines 0 .. E plus one padding line. */
-template <int K, int NB>
-__global__ __launch_bounds__(256) void build_ac128_kernel(const uint32_t* __restrict__ ac, uint32_t nent,
-                                                          uint32_t nlines, uint32_t* __restrict__ lines)
-{
-  using GA = Geo<K, NB, LAY_AC>;
-  using GL = Geo<K, NB, LAY_AC128>;
-  const uint64_t b = (uint64_t) blockIdx.x * 256 + threadIdx.x;
-  if (b >= nlines) return;
-  uint32_t* dst = lines + b * GL::EW;
-  const uint32_t* src = ac + b * GA::EW;
-  const uint32_t* nxt = ac + (b + 1) * GA::EW;
-  for (int i = 0; i < GA::BMW; ++i) dst[i] = b < nent ? src[GA::BOFF + i] : 0u;
-  for (int c = 0; c < GA::HALF; ++c) {
-    dst[GA::BMW + c] = b < nent ? src[c] : 0u;
-    dst[GA::BMW + GA::HALF + c] = b + 1 < nent ? nxt[c] : 0u;
-  }
-  for (int i = GA::BMW + 2 * GA::HALF; i < GL::EW; ++i) dst[i] = 0;
-}
-
 /* Code registers the task kernel needs to pack a query itself (0: use the
  * pack kernel).  KFMI_FUSED=0 / kfmi_set_fused(0) forces the separate pack launch. */
 /* Fused packing keeps 16 bases per register word (MAXW words): 8 words up to
@@ -494,12 +439,8 @@ KFMI_FOR_NB(KFMI_EXTERN, 1, LAY_INTER)
 KFMI_FOR_NB(KFMI_EXTERN, 2, LAY_INTER)
 KFMI_FOR_NB(KFMI_EXTERN, 1, LAY_AC)
 KFMI_FOR_NB(KFMI_EXTERN, 2, LAY_AC)
-KFMI_FOR_NB(KFMI_EXTERN, 1, LAY_PACKED)
-KFMI_FOR_NB(KFMI_EXTERN, 2, LAY_PACKED)
 KFMI_FOR_NB(KFMI_EXTERN, 1, LAY_MID)
 KFMI_FOR_NB(KFMI_EXTERN, 2, LAY_MID)
-KFMI_FOR_NB(KFMI_EXTERN, 1, LAY_AC128)
-KFMI_FOR_NB(KFMI_EXTERN, 2, LAY_AC128)
 KFMI_FOR_NB(KFMI_EXTERN, 1, LAY_MIDAC)
 KFMI_FOR_NB(KFMI_EXTERN, 2, LAY_MIDAC)
 KFMI_EXTERN(4, 2, LAY_GRP)
@@ -513,12 +454,8 @@ hipError_t dispatch(Op op, uint32_t K, uint32_t nb, int lay, const SearchLaunch&
   KFMI_FOR_NB(KFMI_CASE, 2, LAY_INTER)
   KFMI_FOR_NB(KFMI_CASE, 1, LAY_AC)
   KFMI_FOR_NB(KFMI_CASE, 2, LAY_AC)
-  KFMI_FOR_NB(KFMI_CASE, 1, LAY_PACKED)
-  KFMI_FOR_NB(KFMI_CASE, 2, LAY_PACKED)
   KFMI_FOR_NB(KFMI_CASE, 1, LAY_MID)
   KFMI_FOR_NB(KFMI_CASE, 2, LAY_MID)
-  KFMI_FOR_NB(KFMI_CASE, 1, LAY_AC128)
-  KFMI_FOR_NB(KFMI_CASE, 2, LAY_AC128)
   KFMI_FOR_NB(KFMI_CASE, 1, LAY_MIDAC)
   KFMI_FOR_NB(KFMI_CASE, 2, LAY_MIDAC)
   KFMI_CASE(4, 2, LAY_GRP)
@@ -545,32 +482,12 @@ static bool geometry_supported(int backend, uint32_t K, uint32_t nb, int lay)
   KFMI_FOR_NB(KFMI_OKC, 2, LAY_INTER)
   KFMI_FOR_NB(KFMI_OKC, 1, LAY_AC)
   KFMI_FOR_NB(KFMI_OKC, 2, LAY_AC)
-  KFMI_FOR_NB(KFMI_OKC, 1, LAY_PACKED)
-  KFMI_FOR_NB(KFMI_OKC, 2, LAY_PACKED)
   KFMI_FOR_NB(KFMI_OKC, 1, LAY_MID)
   KFMI_FOR_NB(KFMI_OKC, 2, LAY_MID)
-  KFMI_FOR_NB(KFMI_OKC, 1, LAY_AC128)
-  KFMI_FOR_NB(KFMI_OKC, 2, LAY_AC128)
   KFMI_FOR_NB(KFMI_OKC, 1, LAY_MIDAC)
   KFMI_FOR_NB(KFMI_OKC, 2, LAY_MIDAC)
 #undef KFMI_OKC
   return false;
-}
-
-static hipError_t dispatch_build_packed(uint32_t K, uint32_t nb, const uint32_t* inter, uint32_t nentries,
-                                        uint32_t* packed, uint32_t* sb, uint32_t* overflow, hipStream_t st)
-{
-  const uint32_t blocks = (nentries + 255) / 256;
-#define KFMI_BP(KK, NBV, LAYV)                                                                  \
-  if (K == KK && nb == NBV) {                                                                   \
-    hipLaunchKernelGGL((build_packed_kernel<KK, NBV>), dim3(blocks), dim3(256), 0, st, inter, nentries, \
-                       packed, sb, overflow);                                                   \
-    return hipGetLastError();                                                                   \
-  }
-  KFMI_FOR_NB(KFMI_BP, 1, 0)
-  KFMI_FOR_NB(KFMI_BP, 2, 0)
-#undef KFMI_BP
-  return hipErrorInvalidValue;
 }
 
 static hipError_t dispatch_build_mid(uint32_t K, uint32_t nb, const uint32_t* inter, uint32_t nentries,
@@ -587,21 +504,6 @@ static hipError_t dispatch_build_mid(uint32_t K, uint32_t nb, const uint32_t* in
   KFMI_FOR_NB(KFMI_BM, 1, 0)
   KFMI_FOR_NB(KFMI_BM, 2, 0)
 #undef KFMI_BM
-  return hipErrorInvalidValue;
-}
-
-static hipError_t dispatch_build_ac128(uint32_t K, uint32_t nb, const uint32_t* ac, uint32_t nent, uint32_t nlines,
-                                       uint32_t* lines, hipStream_t st)
-{
-  const uint32_t blocks = (nlines + 255) / 256;
-#define KFMI_BA(KK, NBV, LAYV)                                                                          \
-  if (K == KK && nb == NBV) {                                                                           \
-    hipLaunchKernelGGL((build_ac128_kernel<KK, NBV>), dim3(blocks), dim3(256), 0, st, ac, nent, nlines, lines); \
-    return hipGetLastError();                                                                           \
-  }
-  KFMI_FOR_NB(KFMI_BA, 1, 0)
-  KFMI_FOR_NB(KFMI_BA, 2, 0)
-#undef KFMI_BA
   return hipErrorInvalidValue;
 }
 
@@ -629,17 +531,14 @@ static int layout_of(int backend)
     case KFMI_BK_TASK_AC: case KFMI_BK_COOP_AC: return LAY_AC;
     case KFMI_BK_TASK_MID: case KFMI_BK_COOP_MID: return LAY_MID;
     case KFMI_BK_TASK_AC_MID: case KFMI_BK_COOP_AC_MID: return LAY_MIDAC;
-    case KFMI_BK_TASK_GRP: case KFMI_BK_COOP_GRP: return LAY_GRP;
-    case KFMI_BK_TASK_AC128: case KFMI_BK_COOP_AC128: return LAY_AC128;
-    default: return LAY_PACKED;
+    default: return LAY_GRP;   /* KFMI_BK_TASK_GRP, KFMI_BK_COOP_GRP */
   }
 }
 
 bool is_coop(int backend)
 {
-  return backend == KFMI_BK_COOP || backend == KFMI_BK_COOP_AC || backend == KFMI_BK_COOP_PACKED ||
-         backend == KFMI_BK_COOP_MID || backend == KFMI_BK_COOP_AC128 || backend == KFMI_BK_COOP_AC_MID ||
-         backend == KFMI_BK_COOP_GRP;
+  return backend == KFMI_BK_COOP || backend == KFMI_BK_COOP_AC || backend == KFMI_BK_COOP_MID ||
+         backend == KFMI_BK_COOP_AC_MID || backend == KFMI_BK_COOP_GRP;
 }
 
 /* ------------------------------------------------------------------------ */
@@ -709,7 +608,7 @@ static bool ac_locate_fix(const kfmi_fmi_t* f, uint32_t* out)
  * distinct row once, as the builder's counters exclude them (a 'ref'-mode index
  * can put two D_s on one row), so the padding entry is the next
  * block the builder would have written and every layout agrees past the end:
- * INTER's line-local step from entry E-1, GRP/PACKED/MID's stored copies and
+ * INTER's line-local step from entry E-1, GRP/MID's stored copies and
  * MID's backward steps (corrected by dollar_dup like every other block).  Used
  * for the padding entry that keeps R/d == nentries in bounds when
  * (n+1) % d == 0 (reference defect B5: it reads past the end there). */
@@ -756,14 +655,14 @@ static bool end_counters(const kfmi_fmi_t* f, uint32_t* out)
 }
 
 /* Host image of the entries for a layout, converting tags as needed.
- * INTER/PACKED/MID/GRP need plain counters (tag 100/101); MIDAC takes those or
+ * INTER/MID/GRP need plain counters (tag 100/101); MIDAC takes those or
  * an AltCounters file (tag 200/201, turned back into its tag-100 file); AC
  * needs tag 201 (a tag-100/101 input goes through the tfmiAC transform first). */
 static int32_t host_entries_for(const kfmi_fmi_t* f, int lay, kfmi_fmi_t** owned, const kfmi_fmi_t** use)
 {
   *owned = nullptr;
   *use = f;
-  if (lay == LAY_INTER || lay == LAY_PACKED || lay == LAY_MID || lay == LAY_MIDAC || lay == LAY_GRP) {
+  if (lay == LAY_INTER || lay == LAY_MID || lay == LAY_MIDAC || lay == LAY_GRP) {
     /* tag 101 as is; tag 100 is interleaved on the device (upload_entries),
      * or on the host with KFMI_HOST_INTERLEAVE=1 (A/B experiment) */
     if (f->tag == 100 && getenv("KFMI_HOST_INTERLEAVE") && atoi(getenv("KFMI_HOST_INTERLEAVE"))) {
@@ -784,7 +683,7 @@ static int32_t host_entries_for(const kfmi_fmi_t* f, int lay, kfmi_fmi_t** owned
     }
     return KFMI_INDEX_VER_INTERLEAVE;   /* an AC file cannot feed a plain-counter backend */
   }
-  /* AC, AC128 */
+  /* AC */
   if (f->tag == 201) return KFMI_SUCCESS;
   kfmi_fmi_t* t100 = nullptr;
   const kfmi_fmi_t* src100 = f;
@@ -834,7 +733,6 @@ void free_dev_index(kfmi_dev_index* di)
   if (!di) return;
   if (di->device >= 0) (void) hipSetDevice(di->device);
   if (di->ent) (void) hipFree(di->ent);
-  if (di->sb) (void) hipFree(di->sb);
   if (di->sa) (void) hipFree(di->sa);
   if (di->ac_tail) (void) hipFree(di->ac_tail);
   for (uint2* t : di->ftab)
@@ -1059,25 +957,7 @@ int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx, kfmi_dev_
     if (tmp) (void) hipFree(tmp);
     (void) hipFree(d_pad);
     if (!ok) return fail(KFMI_E_KERNEL);
-  } else if (lay == LAY_AC128) {
-    /* one line per tag-201 entry (sentinel included) + one padding line, built on
-     * the device from the entries; padding entry b+1 of the sentinel reads 0 */
-    const uint32_t E = src->nentries;                 /* tag-201 entries incl. the sentinel */
-    const uint32_t nl = E + 1;
-    const uint32_t lw = (uint32_t) pow2ceil((int) (2 * f->nbitmaps * f->steps + nc));
-    uint32_t* tmp = nullptr;
-    di->ent_bytes = 4ull * lw * nl;
-    if (hipMalloc((void**) &tmp, body + 16) != hipSuccess) return fail(KFMI_E_DEVICE_ALLOC);
-    if (hipMalloc((void**) &di->ent, di->ent_bytes) != hipSuccess) {
-      (void) hipFree(tmp);
-      return fail(KFMI_E_DEVICE_ALLOC);
-    }
-    bool ok = upload_entries(tmp, src, body, ctx->st) == hipSuccess &&
-              dispatch_build_ac128(f->steps, f->nbitmaps, tmp, E, nl, di->ent, ctx->st) == hipSuccess &&
-              hipStreamSynchronize(ctx->st) == hipSuccess;
-    (void) hipFree(tmp);
-    if (!ok) return fail(KFMI_E_KERNEL);
-  } else if (lay == LAY_MID || lay == LAY_MIDAC) {
+  } else {   /* LAY_MID, LAY_MIDAC */
     /* MID: pairs of blocks per line, built on the device from tag-101 entries;
      * counters of the last line (odd block count) and of one padding line are
      * "rows past n+1 read as A" extensions of the end counters. */
@@ -1111,43 +991,8 @@ int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx, kfmi_dev_
     (void) hipFree(tmp);
     (void) hipFree(d_ext);
     if (!ok) return fail(KFMI_E_KERNEL);
-  } else {
-    /* packed: build on the device from tag-101 entries (+ the padding entry) */
-    const uint32_t ne = src->nentries + 1;
-    uint32_t* tmp = nullptr;
-    uint32_t* d_over = nullptr;
-    const uint32_t pw = (uint32_t) pow2ceil((int) (2 * f->nbitmaps * f->steps + nc / 2));
-    const int S = sb_shift_for((int) f->chunk);
-    const uint64_t nsb = ((uint64_t) ne + (1u << S) - 1) >> S;
-    if (!end_counters(src, pad.data() + 2 * f->nbitmaps * f->steps)) return fail(KFMI_E_KERNEL);
-    di->ent_bytes = 4ull * pw * (ne + 1);
-    di->sb_bytes = 4ull * nc * nsb;
-    if (hipMalloc((void**) &tmp, 4ull * ew * ne) != hipSuccess) return fail(KFMI_E_DEVICE_ALLOC);
-    if (hipMalloc((void**) &di->ent, di->ent_bytes) != hipSuccess ||
-        hipMalloc((void**) &di->sb, di->sb_bytes) != hipSuccess || hipMalloc((void**) &d_over, 4) != hipSuccess) {
-      (void) hipFree(tmp);
-      if (d_over) (void) hipFree(d_over);
-      return fail(KFMI_E_DEVICE_ALLOC);
-    }
-    uint32_t over = 0;
-    bool ok = upload_entries(tmp, src, body, ctx->st) == hipSuccess &&
-              hipMemcpyAsync((uint8_t*) tmp + body, pad.data(), 4ull * ew, hipMemcpyHostToDevice, ctx->st) ==
-                  hipSuccess &&
-              hipMemsetAsync(d_over, 0, 4, ctx->st) == hipSuccess &&
-              hipMemsetAsync(di->ent, 0, di->ent_bytes, ctx->st) == hipSuccess &&
-              dispatch_build_packed(f->steps, f->nbitmaps, tmp, ne, di->ent, di->sb, d_over, ctx->st) ==
-                  hipSuccess &&
-              hipMemcpyAsync(&over, d_over, 4, hipMemcpyDeviceToHost, ctx->st) == hipSuccess &&
-              hipStreamSynchronize(ctx->st) == hipSuccess;
-    (void) hipFree(tmp);
-    (void) hipFree(d_over);
-    if (!ok) return fail(KFMI_E_KERNEL);
-    if (over) {
-      fprintf(stderr, "kstepfmi: packed layout delta overflow (%u) -- corrupt counters\n", over);
-      return fail(KFMI_E_READING_FMI);
-    }
   }
-  if (lay == LAY_AC || lay == LAY_AC128 || lay == LAY_MIDAC) {
+  if (lay == LAY_AC || lay == LAY_MIDAC) {
     /* 4 x NC words: LAY_MIDAC's AltCounters counters of entries E-1, E, E+1
      * (kfmi_ac_tail), and on every AltCounters layout row 3, the locate walk's
      * correction of a backward step from the sentinel (ac_locate_fix) */
@@ -1188,11 +1033,11 @@ int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx, kfmi_dev_
  * in two groups whenever this is 2 or 4; 1 = none.
  *  - tables over 3.5 GB: 4.  Past the translation reach the per-instruction
  *    page cliff costs up to 2.7x (task-grp 96 GB: 17.6 -> 6.8 ms at 100 bp,
- *    25.1 -> 9.1 at 150 bp; task-ac128 6.4 GB: 18.1 -> 10.0, 26.1 -> 15.5);
+ *    25.1 -> 9.1 at 150 bp; the retired AC128 layout's 6.4 GB: 18.1 -> 10.0, 26.1 -> 15.5);
  *  - 2-3.5 GB, one line per LF (MID128 / MIDAC): 2 (task-mid 9.53 -> 9.45 at
  *    100 bp, but 14.41 -> 14.83 ms with the 16-word kernel at 150 bp);
  *  - 2-3.5 GB, other layouts: 4 (task-ac 12.87 -> 11.81 at 100 bp,
- *    18.93 -> 17.94 at 150 bp; task-packed 14.0 -> 13.3).
+ *    18.93 -> 17.94 at 150 bp; the retired packed layout 14.0 -> 13.3).
  * profiles/r02/sweep_split_r2ah.jsonl, sweep_split150_r2aj.jsonl; the asm
  * forms: profiles/r03/sweep_r3n.jsonl, sweep150_r3n.jsonl.  The ftab lookup
  * (one gather per read) is never split: that measured slower.
@@ -1226,7 +1071,6 @@ IdxArgs idx_args(const kfmi_dev_index* di)
 {
   IdxArgs ix;
   ix.ent = di->ent;
-  ix.sb = di->sb;
   ix.bwtsize = di->bwtsize;
   ix.dl = di->dl;
   ix.ftab = nullptr;
@@ -1236,7 +1080,7 @@ IdxArgs idx_args(const kfmi_dev_index* di)
   ix.ac_tail_b0 = di->ac_tail_b0;
   ix.rtab = nullptr;
   ix.rem = 0;
-  ix.split = split_for(di->ent_bytes + di->sb_bytes, di->layout);
+  ix.split = split_for(di->ent_bytes, di->layout);
   return ix;
 }
 
@@ -1250,7 +1094,7 @@ IdxArgs idx_args(const kfmi_dev_index* di)
  * reference defines no result here).  The ftab is not combined with it. */
 bool rem_supported(int layout)
 {
-  return layout == LAY_INTER || layout == LAY_PACKED || layout == LAY_MID || layout == LAY_GRP;
+  return layout == LAY_INTER || layout == LAY_MID || layout == LAY_GRP;
 }
 
 int32_t use_rtab(kfmi_dev_index* di, hipStream_t st, IdxArgs& ix, uint32_t rem)
@@ -1803,11 +1647,11 @@ extern "C" uint64_t kfmi_device_index_bytes(void* index)
   if (f->grp) {   /* all replicas of a device group */
     const GroupIndex* g = (const GroupIndex*) f->grp;
     uint64_t b = 0;
-    for (int i = 0; i < g->n; ++i) b += g->di[i]->ent_bytes + g->di[i]->sb_bytes + g->di[i]->sa_bytes;
+    for (int i = 0; i < g->n; ++i) b += g->di[i]->ent_bytes + g->di[i]->sa_bytes;
     return b;
   }
   if (!f || !f->dev) return 0;
-  return f->dev->ent_bytes + f->dev->sb_bytes + f->dev->sa_bytes;
+  return f->dev->ent_bytes + f->dev->sa_bytes;
 }
 
 }  // namespace kfmi

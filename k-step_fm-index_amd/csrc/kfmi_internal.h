@@ -113,9 +113,8 @@ uint32_t kfmi_plane_index(uint32_t tag, uint32_t steps, uint32_t nb, uint32_t s,
 /* backend registry, fmi_backend.c */
 typedef enum {
   KFMI_BK_TASK = 0, KFMI_BK_COOP, KFMI_BK_TASK_AC, KFMI_BK_COOP_AC,
-  KFMI_BK_TASK_PACKED, KFMI_BK_COOP_PACKED, KFMI_BK_TASK_MID, KFMI_BK_COOP_MID,
-  KFMI_BK_TASK_AC128, KFMI_BK_COOP_AC128, KFMI_BK_TASK_AC_MID, KFMI_BK_COOP_AC_MID,
-  KFMI_BK_TASK_GRP, KFMI_BK_COOP_GRP, KFMI_BK_COUNT
+  KFMI_BK_TASK_MID, KFMI_BK_COOP_MID, KFMI_BK_TASK_AC_MID, KFMI_BK_COOP_AC_MID,
+  KFMI_BK_TASK_GRP, KFMI_BK_COOP_GRP, KFMI_BK_COUNT   /* packed and ac128 retired in round 6 */
 } kfmi_backend_t;
 kfmi_backend_t kfmi_backend(void);
 uint32_t       kfmi_backend_tag(kfmi_backend_t b);   /* 101 or 201 */

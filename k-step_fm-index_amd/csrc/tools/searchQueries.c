@@ -5,8 +5,8 @@
  * searchIndexGPU x iters -> transferGPUtoCPU -> saveResults("<index>.res.gpu").
  * Prints "TIME: <mean seconds per iteration>" like the reference, plus the
  * device-side (HIP event) times of the last iteration.
- * Environment: KFMI_BACKEND (task|coop|task-ac|coop-ac|task-packed|coop-packed|
- * task-mid|coop-mid|task-ac128|coop-ac128), KFMI_DEVICE, KFMI_ITERS (default 5,
+ * Environment: KFMI_BACKEND (task|coop|task-ac|coop-ac|task-mid|coop-mid|
+ * task-ac-mid|coop-ac-mid|task-grp|coop-grp), KFMI_DEVICE, KFMI_ITERS (default 5,
  * the reference's `iter`), KFMI_FTAB.
  * Locate (extension): KFMI_SA_FILE=<samples written by gfmi> also writes
  * "<index>.pos.gpu": per query "<n> <p1> ... <pn>" (text positions, suffix

@@ -20,12 +20,11 @@ PKG_DIR = Path(__file__).resolve().parent.parent          # k-step_fm-index_amd/
 LIB_PATH = PKG_DIR / "lib" / "libkstepfmi.so"
 BIN_DIR = PKG_DIR / "bin"
 
-BACKENDS = ("task", "coop", "task-ac", "coop-ac", "task-packed", "coop-packed", "task-mid", "coop-mid",
-            "task-ac128", "coop-ac128", "task-ac-mid", "coop-ac-mid", "task-grp", "coop-grp")
-BACKEND_TAG = {"task": 101, "coop": 101, "task-ac": 201, "coop-ac": 201,
-               "task-packed": 101, "coop-packed": 101, "task-mid": 101, "coop-mid": 101,
-               "task-ac128": 201, "coop-ac128": 201, "task-ac-mid": 201, "coop-ac-mid": 201,
-               "task-grp": 101, "coop-grp": 101}
+# (the packed and ac128 layouts were retired in round 6)
+BACKENDS = ("task", "coop", "task-ac", "coop-ac", "task-mid", "coop-mid", "task-ac-mid", "coop-ac-mid",
+            "task-grp", "coop-grp")
+BACKEND_TAG = {"task": 101, "coop": 101, "task-ac": 201, "coop-ac": 201, "task-mid": 101, "coop-mid": 101,
+               "task-ac-mid": 201, "coop-ac-mid": 201, "task-grp": 101, "coop-grp": 101}
 
 _lib = None
 

@@ -29,7 +29,7 @@ sys.path.insert(0, str(ROOT / "k-step_fm-index_amd"))
 import kstep_fmi as K  # noqa: E402
 from kstep_fmi import synth  # noqa: E402
 
-K2 = "task-mid,coop-mid,task,coop,task-ac,coop-ac,task-ac128,coop-ac128,task-ac-mid,coop-ac-mid,task-packed,coop-packed"
+K2 = "task-mid,coop-mid,task,coop,task-ac,coop-ac,task-ac-mid,coop-ac-mid"
 
 
 def log(*a):

@@ -3,7 +3,7 @@
 
 Builds the 3 Gbase (or --ref-size) index once on the GPU, then times each
 backend x tuning knob and prints one JSON line per variant to stdout:
-  python scripts/sweep.py --backends task-packed,task,coop --qpt 1,2 --steps 5
+  python scripts/sweep.py --backends task-mid,task,coop --qpt 1,2 --steps 5
 Every variant's results are compared with the first variant's (bit-exact).
 """
 from __future__ import annotations
@@ -35,7 +35,7 @@ def main():
     p.add_argument("--qlen", type=int, default=100)
     p.add_argument("--k", type=int, default=2)
     p.add_argument("--d", type=int, default=64)
-    p.add_argument("--backends", default="task-packed,task,task-ac,coop,coop-ac,coop-packed")
+    p.add_argument("--backends", default="task-mid,task,task-ac,coop,coop-ac,coop-mid")
     p.add_argument("--env", default="", help="semicolon list of VAR=v1,v2 knobs swept for every backend")
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=1, help="untimed searches per variant before its timed steps")

@@ -20,6 +20,7 @@ import json
 import re
 import statistics
 
+# layout ids 2 (packed) and 4 (ac128) name the layouts retired in round 6; kept to read older passes
 LAYOUT = {"task": 0, "coop": 0, "task-ac": 1, "coop-ac": 1, "task-packed": 2, "coop-packed": 2, "task-mid": 3,
           "coop-mid": 3, "task-ac128": 4, "coop-ac128": 4, "task-ac-mid": 5, "coop-ac-mid": 5, "task-grp": 6,
           "coop-grp": 6}

@@ -23,7 +23,7 @@ import pytest
 from util import REPO
 
 REF = REPO / "oracle" / "_ref"
-ALT = ("task-ac", "coop-ac", "task-ac128", "coop-ac128", "task-ac-mid", "coop-ac-mid")
+ALT = ("task-ac", "coop-ac", "task-ac-mid", "coop-ac-mid")
 ACGT = np.frombuffer(b"ACGT", np.uint8)
 
 
@@ -200,7 +200,7 @@ def test_ac_drift_locate(kfmi_mod, k, rate):
     try:
         for m in (2 * k, 64, 80):
             q = np.full((5, m), ord("A"), np.uint8)
-            for b in ("task-ac", "task-ac-mid", "coop-ac-mid", "task-ac128"):
+            for b in ("task-ac", "task-ac-mid", "coop-ac-mid"):
                 res, off, pos = K.locate_array(idx, q, b)
                 assert int(res[1]) > n + 1 or m == 2 * k, (b, m, res[:2])   # the drift reaches past n+1
                 w_pos, w_off = [], [0]
@@ -254,7 +254,7 @@ def test_locate_walks_on_altcounters_layouts(kfmi_mod, name, k):
         st = np.arange(0, n - 4 * k + 1, 7)
         q = np.ascontiguousarray(np.concatenate([t[st[:, None] + np.arange(2 * k)[None, :]],
                                                  np.full((1, 2 * k), ord("T"), np.uint8)]))
-        for b in ("task-ac", "task-ac128", "task-ac-mid", "task-mid"):
+        for b in ("task-ac", "task-ac-mid", "task-mid"):
             res, off, pos = K.locate_array(idx, q, b)
             w_pos = [sa[int(res[2 * j]):min(int(res[2 * j + 1]), n + 1)] for j in range(q.shape[0])]
             assert np.array_equal(pos, np.concatenate(w_pos)), (name, k, b)

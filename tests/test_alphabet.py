@@ -170,8 +170,8 @@ def test_gpu_builder_ref_mode_equals_reference(ref_mode, key, ent):
     assert np.array_equal(plain.image(), K.Index.build(text, k=ent["k"], d=ent["d"], gpu=False).image())
 
 
-PLAIN = ("task", "coop", "task-mid", "coop-mid", "task-packed", "coop-packed")
-AC = ("task-ac", "coop-ac", "task-ac128", "coop-ac128", "task-ac-mid", "coop-ac-mid")
+PLAIN = ("task", "coop", "task-mid", "coop-mid")
+AC = ("task-ac", "coop-ac", "task-ac-mid", "coop-ac-mid")
 
 
 @pytest.mark.gpu

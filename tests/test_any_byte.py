@@ -7,8 +7,8 @@ restatement does (oracle/fmi_oracle.c code_of)."""
 import numpy as np
 import pytest
 
-PLAIN = ("task", "coop", "task-packed", "coop-packed", "task-mid", "coop-mid")
-ALT = ("task-ac", "coop-ac", "task-ac128", "coop-ac128", "task-ac-mid", "coop-ac-mid")
+PLAIN = ("task", "coop", "task-mid", "coop-mid")
+ALT = ("task-ac", "coop-ac", "task-ac-mid", "coop-ac-mid")
 
 
 def _case(k, m):

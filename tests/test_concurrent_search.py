@@ -113,7 +113,7 @@ def test_reupload_while_another_thread_searches(kfmi_mod, oracle_mod, setup):
         K.set_backend("coop-mid" if i % 2 else "task-mid")
         K.transfer_to_gpu(idx_b, None, None)       # unrelated handle
         idx_b.free_gpu()
-        K.set_backend("task" if i % 2 else "task-packed")   # plain semantics: the reader's results stay
+        K.set_backend("task" if i % 2 else "task-mid")   # plain semantics: the reader's results stay
         K.transfer_to_gpu(idx, None, None)         # replaces A's device copy under the reader
     writer_s = time.perf_counter() - t0
     stop.set()

@@ -39,7 +39,7 @@ def _reads(t, n, m, seed):
                                                 rng.choice(np.frombuffer(b"ACGTN", np.uint8), size=(n // 4, m))]))
 
 
-@pytest.mark.parametrize("k,backends", [(2, ("task-mid", "coop-mid", "task", "task-packed", "coop-ac128")),
+@pytest.mark.parametrize("k,backends", [(2, ("task-mid", "coop-mid", "task")),
                                         (4, ("coop-grp", "task-grp"))])
 def test_device_only_build_equals_host_image_build(gpu, tmp_path, k, backends):
     t = _text(2_000_003, k)

@@ -21,7 +21,7 @@ def test_dropin_links_against_engine():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("backend,tag,res_tag", [("task", 101, 100), ("coop", 101, 100), ("task-packed", 100, 100),
+@pytest.mark.parametrize("backend,tag,res_tag", [("task", 101, 100), ("coop", 101, 100), ("task-mid", 100, 100),
                                                  ("task-ac", 201, 200), ("coop-ac", 201, 200),
                                                  # the K = 2 file on the K = 4 layout (derived on upload, DESIGN 5d')
                                                  ("coop-grp", 101, 100), ("task-grp", 100, 100)])

@@ -26,8 +26,8 @@ ACGT = np.frombuffer(b"ACGT", np.uint8)
 WORLDS = 40
 GEOMS = [(1, 64), (2, 64), (1, 192), (2, 192), (3, 64), (4, 64)]
 TAGS = {100: "", 101: ".interleaving", 200: ".ac", 201: ".interleaving.ac"}
-PLAIN = ("task", "coop", "task-packed", "coop-packed", "task-mid", "coop-mid")
-ALT = ("task-ac", "coop-ac", "task-ac128", "coop-ac128", "task-ac-mid", "coop-ac-mid")
+PLAIN = ("task", "coop", "task-mid", "coop-mid")
+ALT = ("task-ac", "coop-ac", "task-ac-mid", "coop-ac-mid")
 
 
 def world(i):
@@ -129,7 +129,7 @@ def test_dropin_world_gpu(tmp_path, i):
         if k > 2:
             pool = ("coop-grp", "task-grp")
         elif tag >= 200:
-            pool = ("task-ac", "task-ac128", "task-ac-mid", "coop-ac-mid") + (("coop-ac", "coop-ac128") if k == 2 else ())
+            pool = ("task-ac", "task-ac-mid", "coop-ac-mid") + (("coop-ac",) if k == 2 else ())
         else:
             pool = PLAIN + (("coop-grp",) if (k, d) == (2, 64) else ())
         for b in rng.choice(pool, size=2, replace=False):

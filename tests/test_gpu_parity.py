@@ -14,8 +14,8 @@ from util import GOLDEN, manifest, read_qry
 
 pytestmark = pytest.mark.gpu
 
-PLAIN = ("task", "coop", "task-packed", "coop-packed", "task-mid", "coop-mid")
-ALT = ("task-ac", "coop-ac", "task-ac128", "coop-ac128", "task-ac-mid", "coop-ac-mid")
+PLAIN = ("task", "coop", "task-mid", "coop-mid")
+ALT = ("task-ac", "coop-ac", "task-ac-mid", "coop-ac-mid")
 ACMID = ("task-ac-mid", "coop-ac-mid")     # AltCounters semantics on MID128 lines: from tag 100/101 (or 200/201, test_ac_inverse.py)
 
 
@@ -25,7 +25,7 @@ def coop_supported(backend, k, d):
         return True
     nb = d // 32
     bmw = 2 * nb * k
-    if backend in ("coop-ac", "coop-ac128"):
+    if backend == "coop-ac":
         return k == 2 and bmw % 4 == 0
     if backend == "coop-ac-mid":
         return bmw % 4 == 0
@@ -126,7 +126,7 @@ def test_block_count_matches_oracle(gpu, oracle_mod, random_index):
     idx = idxs[(2, 64)]
     q = _reads(text, 20000, 100, seed=3)
     _, want = oracle_mod.search(idx.image(), q)
-    gpu.set_backend("task-packed")
+    gpu.set_backend("task-mid")
     qq = gpu.Queries.from_array(q)
     r = gpu.Results.alloc(q.shape[0])
     gpu.transfer_to_gpu(idx, qq, r)
@@ -217,8 +217,8 @@ def test_b5_boundary_against_bruteforce(gpu, n):
 
 
 @pytest.mark.parametrize("bases", [2, 8, 12])
-@pytest.mark.parametrize("backend", ["task-mid", "task", "task-packed", "task-ac", "task-ac128", "coop-mid",
-                                     "coop-ac128", "coop"])
+@pytest.mark.parametrize("backend", ["task-mid", "task", "task-ac", "coop-mid",
+                                     "coop"])
 def test_ftab_jump_start_equals_oracle(gpu, oracle_mod, random_index, backend, bases):
     """The ftab replaces the first bases/K LF steps by a table built with the
     same LF steps: results must not change (reads shorter than the table keep
@@ -298,12 +298,12 @@ def test_ac_tail_blocks(gpu, oracle_mod, n, tail):
                 defined = False
                 want = gpu.search_cpu_array(ac200, q, 2)
                 assert int(want.max()) <= ((n + d) // d + 2) * d - 1
-            for b in ACMID + ("task-ac128", "coop-ac128"):
+            for b in ACMID:
                 if coop_supported(b, k, d):
                     assert np.array_equal(gpu.search_array(idx, q, b), want), (n, tail, k, d, m, b, defined)
 
 
-@pytest.mark.parametrize("backend", ["coop", "coop-packed", "coop-mid", "coop-ac", "coop-ac128", "coop-ac-mid"])
+@pytest.mark.parametrize("backend", ["coop", "coop-mid", "coop-ac", "coop-ac-mid"])
 def test_coop_backends_equal_oracle(gpu, oracle_mod, random_index, backend, monkeypatch):
     """The coop kernel's staging rounds (each round decodes its requests'
     chunk addresses; the pre-addressed form measured neutral and was removed,
@@ -334,7 +334,7 @@ def test_coop_backends_equal_oracle(gpu, oracle_mod, random_index, backend, monk
 
 
 @pytest.mark.parametrize("split", ["1", "2", "4"])
-@pytest.mark.parametrize("backend", ["task-mid", "task", "task-packed", "task-ac", "task-ac128", "task-ac-mid"])
+@pytest.mark.parametrize("backend", ["task-mid", "task", "task-ac", "task-ac-mid"])
 def test_split_gathers_equal_oracle(gpu, oracle_mod, random_index, backend, split, knobs):
     """Every fetch form on small indexes, by forcing the table-size class
     (kfmi_set_split_class = 1: under 2 GB, 2: 2-3.5 GB, 4: larger): the asm
@@ -370,8 +370,8 @@ def test_split_gathers_equal_oracle(gpu, oracle_mod, random_index, backend, spli
 
 
 @pytest.mark.parametrize("backend,k,d,bases", [("task-ac", 1, 64, 12), ("task-ac", 2, 64, 12), ("task", 1, 32, 10),
-                                               ("task", 1, 64, 10), ("task-mid", 2, 64, 10), ("task-ac128", 1, 64, 10),
-                                               ("task-packed", 2, 64, 10), ("coop-ac-mid", 1, 64, 10),
+                                               ("task", 1, 64, 10), ("task-mid", 2, 64, 10), ("task-ac-mid", 1, 64, 10),
+                                               ("coop-mid", 2, 64, 10), ("coop-ac-mid", 1, 64, 10),
                                                ("task", 2, 192, 8)])
 def test_ftab_table_every_entry(gpu, random_index, backend, k, d, bases):
     """Every entry of a freshly built jump-start table, three builds: the

@@ -56,7 +56,7 @@ def run_trio(K, idx, reads):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("backend", ["task-mid", "coop-mid", "task", "coop-ac", "task-ac128", "task-ac-mid"])
+@pytest.mark.parametrize("backend", ["task-mid", "coop-mid", "task", "coop-ac", "task-ac-mid"])
 @pytest.mark.parametrize("group", [[0, 0], [0, 0, 0]])
 @pytest.mark.parametrize("num", [3_333, 130, 64, 1, 0])
 def test_group_equals_single_device(setup, backend, group, num):

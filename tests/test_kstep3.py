@@ -140,7 +140,7 @@ def test_k3_other_backends_refuse(kfmi_mod, k3):
     K = kfmi_mod
     t, i3, _ = k3
     q = _reads(t, 100, 99, 1)
-    for b in ("task-mid", "coop-mid", "task", "coop-ac", "task-packed"):
+    for b in ("task-mid", "coop-mid", "task", "coop-ac"):
         with pytest.raises(K.KfmiError) as e:
             K.search_array(i3, q, b)
         assert e.value.code == 33, b

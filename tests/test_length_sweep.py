@@ -18,12 +18,12 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-PLAIN = ("task", "coop", "task-packed", "coop-packed", "task-mid", "coop-mid")
-ALT = ("task-ac", "coop-ac", "task-ac128", "coop-ac128", "task-ac-mid", "coop-ac-mid")
+PLAIN = ("task", "coop", "task-mid", "coop-mid")
+ALT = ("task-ac", "coop-ac", "task-ac-mid", "coop-ac-mid")
 GRP = ("task-grp", "coop-grp")
 # K = 1: the cooperative AltCounters kernels need 4 counters per half entry
-# (CoopCfg::OK), so coop-ac / coop-ac128 take K = 2 only
-BACKENDS = {1: PLAIN + ("task-ac", "task-ac128", "task-ac-mid", "coop-ac-mid"), 2: PLAIN + ALT, 3: GRP, 4: GRP}
+# (CoopCfg::OK), so coop-ac takes K = 2 only
+BACKENDS = {1: PLAIN + ("task-ac", "task-ac-mid", "coop-ac-mid"), 2: PLAIN + ALT, 3: GRP, 4: GRP}
 
 LENGTHS = sorted({1, 2, 3, 4, 5, 15, 16, 17, 31, 32, 33, 63, 64, 65, 127, 128, 129, 255, 256, 257, 511, 1020,
                   1023, 1024, 1025, 1026, 1040, 1056, 2047, 2048, 2064, 3072, 4095, 4096, 4128}

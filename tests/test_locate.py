@@ -14,8 +14,8 @@ import pytest
 import util
 
 ACGT = np.frombuffer(b"ACGT", dtype=np.uint8)
-PLAIN = ("task", "coop", "task-packed", "coop-packed", "task-mid", "coop-mid")
-ALT = ("task-ac", "coop-ac", "task-ac128", "coop-ac128")
+PLAIN = ("task", "coop", "task-mid", "coop-mid")
+ALT = ("task-ac", "coop-ac")
 
 
 def _text(n, seed):
@@ -123,7 +123,7 @@ def _coop_ok(backend, k, d):
     if not backend.startswith("coop"):
         return True
     bmw = 2 * (d // 32) * k
-    if backend in ("coop-ac", "coop-ac128"):
+    if backend == "coop-ac":
         return k == 2 and bmw % 4 == 0
     if backend == "coop":
         return bmw % 4 == 0 and (bmw + 4 ** k) % 4 == 0

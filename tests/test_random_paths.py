@@ -48,7 +48,7 @@ def test_world_device_resident_and_stream(K, i, monkeypatch):
     rng = np.random.default_rng(500 + i)
     idx = K.Index.build(text, k=k, d=d, gpu=True, host_image=False)
     try:
-        pool = [b for b in ("task-mid", "coop-mid", "task", "task-packed", "task-grp", "coop-grp") if _takes(b, k, d, n)]
+        pool = [b for b in ("task-mid", "coop-mid", "task", "task-grp", "coop-grp") if _takes(b, k, d, n)]
         b = str(rng.choice(pool))
         assert np.array_equal(K.search_array(idx, q, b), want), (i, b)
         monkeypatch.setenv("KFMI_STREAM_HOSTPACK", str(int(rng.integers(0, 3))))

@@ -26,8 +26,8 @@ import pytest
 
 import util
 
-PLAIN = ("task", "coop", "task-packed", "coop-packed", "task-mid", "coop-mid")
-ALT = ("task-ac", "coop-ac", "task-ac128", "coop-ac128", "task-ac-mid", "coop-ac-mid")
+PLAIN = ("task", "coop", "task-mid", "coop-mid")
+ALT = ("task-ac", "coop-ac", "task-ac-mid", "coop-ac-mid")
 GRP = ("task-grp", "coop-grp")
 ACGT = np.frombuffer(b"ACGT", np.uint8)
 WORLDS = 160
@@ -44,7 +44,7 @@ def _takes(backend, k, d, n):
     if not backend.startswith("coop"):
         return True
     bmw = 2 * (d // 32) * k
-    if backend in ("coop-ac", "coop-ac128"):
+    if backend == "coop-ac":
         return k == 2 and bmw % 4 == 0
     return bmw % 4 == 0
 
@@ -218,7 +218,7 @@ def test_random_world_locate_and_ftab(kfmi_mod, i):
         bases = k * int(rng.integers(1, 12 // k + 1))   # a whole number of K-steps, <= 12 bases
         K.set_ftab(bases)
         try:
-            for b in ("task-mid", "coop-mid", "task-packed") if k <= 2 else GRP:
+            for b in ("task-mid", "coop-mid") if k <= 2 else GRP:
                 if _takes(b, k, d, n):
                     got = K.search_array(idx, q, b)
                     bad = np.flatnonzero(got != want)

@@ -18,9 +18,9 @@ import util
 
 pytestmark = pytest.mark.gpu
 
-PLAIN2 = ("task", "coop", "task-packed", "coop-packed", "task-mid", "coop-mid")
+PLAIN2 = ("task", "coop", "task-mid", "coop-mid")
 GRP = ("task-grp", "coop-grp")
-ALT = ("task-ac", "coop-ac", "task-ac128", "coop-ac128", "task-ac-mid", "coop-ac-mid")
+ALT = ("task-ac", "coop-ac", "task-ac-mid", "coop-ac-mid")
 
 
 @pytest.fixture(scope="module")
@@ -56,7 +56,7 @@ def test_rem_matches_k1_oracle(gpu, oracle_mod, texts, fused, knobs):
     text, idx = texts
     img1 = idx[(1, 64)].image()
     cases = [((2, 64), PLAIN2, (1, 3, 5, 17, 99, 101, 151, 255, 257, 301, 1025, 2049, 4001)),
-             ((2, 192), ("task-mid", "coop-mid", "task-packed"), (1, 33, 101)),
+             ((2, 192), ("task-mid", "coop-mid"), (1, 33, 101)),
              ((4, 64), GRP, (1, 2, 3, 5, 6, 7, 98, 99, 101, 150, 151, 254, 258, 1023, 1026, 4097))]
     for kd, backends, ms in cases:
         for m in ms:
@@ -80,7 +80,7 @@ def test_rem_small_texts_against_bruteforce(gpu, n, tail):
         t[n - len(e):] = e
     text = t.tobytes()
     bf = util.BruteForce(text.decode())
-    for k, d, backends in ((2, 64, ("task-mid", "coop-mid", "task", "task-packed")), (2, 32, ("task-mid", "task")),
+    for k, d, backends in ((2, 64, ("task-mid", "coop-mid", "task")), (2, 32, ("task-mid", "task")),
                            (4, 64, GRP)):
         if n + 1 < k:                     # the builders need n + 1 >= K rows
             continue

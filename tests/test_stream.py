@@ -28,7 +28,7 @@ def setup(kfmi_mod):
 
 
 @pytest.mark.parametrize("hostpack", ["1", "0", "2", "3"])
-@pytest.mark.parametrize("backend", ["task-mid", "coop-mid", "task", "coop-ac", "task-ac128"])
+@pytest.mark.parametrize("backend", ["task-mid", "coop-mid", "task", "coop-ac"])
 @pytest.mark.parametrize("chunk", [0, 1_000, 4_099])
 def test_stream_equals_batch_and_oracle(setup, oracle_mod, backend, chunk, hostpack, monkeypatch):
     """hostpack 1: code words packed on the host (qpack.c) and sent over PCIe;

@@ -18,8 +18,8 @@ pytestmark = pytest.mark.gpu
 # the K = 2 backends: a grouped one would derive a K = 4 device copy, and a
 # batch packed for one K meets a copy of the other as a refusal (code 33), by
 # design, not a result
-BACKENDS = ("task", "coop", "task-packed", "coop-packed", "task-mid", "coop-mid", "task-ac", "coop-ac",
-            "task-ac128", "coop-ac128", "task-ac-mid", "coop-ac-mid")
+BACKENDS = ("task", "coop", "task-mid", "coop-mid", "task-ac", "coop-ac",
+            "task-ac-mid", "coop-ac-mid")
 
 
 @pytest.fixture(scope="module")

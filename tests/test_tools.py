@@ -46,7 +46,7 @@ def test_tools_report_reference_errors(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("backend,tag,res_tag", [("task-mid", 100, 100), ("task", 101, 100), ("coop-ac", 201, 200), ("task-ac128", 201, 200)])
+@pytest.mark.parametrize("backend,tag,res_tag", [("task-mid", 100, 100), ("task", 101, 100), ("coop-ac", 201, 200), ("task-ac-mid", 201, 200)])
 def test_search_driver(tmp_path, backend, tag, res_tag):
     c = manifest()["textA"]
     ent = c["indexes"]["k2_d64"]

@@ -10,8 +10,8 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-PLAIN = ("task-mid", "coop-mid", "task", "coop", "task-packed", "coop-packed")
-ALT = ("task-ac", "coop-ac", "task-ac128", "task-ac-mid", "coop-ac-mid")
+PLAIN = ("task-mid", "coop-mid", "task", "coop")
+ALT = ("task-ac", "coop-ac", "task-ac-mid", "coop-ac-mid")
 
 
 @pytest.fixture(scope="module")
