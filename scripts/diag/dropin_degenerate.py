@@ -32,8 +32,8 @@ from oracle import oracle  # noqa: E402
 REF = REPO / "oracle" / "_ref"
 GEOMS = [(1, 64), (2, 64), (1, 192), (2, 192), (3, 64), (4, 64)]
 TAGS = {100: "", 101: ".interleaving", 200: ".ac", 201: ".interleaving.ac"}
-PLAIN = ("task", "coop", "task-packed", "coop-packed", "task-mid", "coop-mid")
-ALT = ("task-ac", "task-ac128", "task-ac-mid", "coop-ac-mid")
+PLAIN = ("task", "coop", "task-mid", "coop-mid")
+ALT = ("task-ac", "task-ac-mid", "coop-ac-mid")
 ACGT = np.frombuffer(b"ACGT", np.uint8)
 
 

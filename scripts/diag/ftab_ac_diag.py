@@ -28,7 +28,7 @@ for trial in range(3):
     # another index object: fresh upload, fresh ftab
     idx.free_gpu()
 K.set_ftab(0)
-for b in ("task-mid", "task", "task-ac128", "coop-ac-mid", "task-ac-mid"):
+for b in ("task-mid", "task", "coop-ac-mid", "task-ac-mid"):
     K.set_ftab(12)
     got = K.search_array(idx, q, b)
     w = want if "ac" in b else oracle.search(idx.image(), q)[0]

@@ -33,11 +33,9 @@ for k, d in ((1, 64), (2, 64), (2, 192)):
             want_ac, _ = oracle.search(a200.image(), q)
             want, _ = oracle.search(idx.image(), q)
             K.set_ftab(bases)
-            for b in ("task-ac", "task-ac128", "task", "task-mid", "task-packed", "coop-ac128", "coop", "coop-mid",
+            for b in ("task-ac", "task", "task-mid", "coop", "coop-mid",
                       "task-ac-mid", "coop-ac-mid"):
                 if b.startswith("coop") and (2 * (d // 32) * k) % 4:
-                    continue
-                if b in ("coop-ac128",) and k == 1:
                     continue
                 try:
                     got = K.search_array(idx, q, b)

@@ -27,7 +27,7 @@ while time.time() - t0 < float(sys.argv[1]) if len(sys.argv) > 1 else 120:
         bases = 12
     m = int(rng.choice([100, 150, 100]))
     q = reads(6000, m, it)
-    b = str(rng.choice(["task-ac", "task-ac", "task", "task-mid", "task-ac128", "coop-ac-mid"]))
+    b = str(rng.choice(["task-ac", "task-ac", "task", "task-mid", "coop-ac-mid"]))
     K.set_ftab(bases)
     want = oracle.search(acimg[kd] if "ac" in b else idx.image(), q)[0]
     got = K.search_array(idx, q, b)

@@ -13,13 +13,12 @@ geoms = [(1, 64), (2, 64), (1, 128), (2, 128), (1, 192), (2, 192), (2, 448), (2,
 idxs = {g: K.Index.build(text, k=g[0], d=g[1]) for g in geoms}
 img = {g: i.image() for g, i in idxs.items()}
 ac = {g: i.alt_counters()[0].image() for g, i in idxs.items()}
-BACK = ["task", "coop", "task-packed", "coop-packed", "task-mid", "coop-mid", "task-ac", "coop-ac", "task-ac128",
-        "coop-ac128", "task-ac-mid", "coop-ac-mid"]
+BACK = ["task", "coop", "task-mid", "coop-mid", "task-ac", "coop-ac", "task-ac-mid", "coop-ac-mid"]
 def coop_ok(b, k, d):
     if not b.startswith("coop"):
         return True
     bmw = 2 * (d // 32) * k
-    if b in ("coop-ac", "coop-ac128"):
+    if b == "coop-ac":
         return k == 2 and bmw % 4 == 0
     if b == "coop":
         return bmw % 4 == 0 and (bmw + 4 ** k) % 4 == 0

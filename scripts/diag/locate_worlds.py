@@ -17,7 +17,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parent))
 import dropin_degenerate as D  # noqa: E402
 
 K = D.K
-BACKENDS = ("task", "task-mid", "task-packed", "coop-mid", "task-ac", "task-ac128", "task-ac-mid")
+BACKENDS = ("task", "task-mid", "coop-mid", "task-ac", "task-ac-mid")
 
 
 def main():
