@@ -37,6 +37,21 @@ static int stream_slots(void)
   return v < 2 ? 2 : v > NSLOT_MAX ? NSLOT_MAX : v;
 }
 
+/* Pageable callers' buffers taken by the DMA engines directly instead of
+ * through pinned staging copies on the host pool (KFMI_STREAM_DIRECT, read
+ * once: bit 0 = the reads, bit 1 = the results; default 0).  On this ROCm a
+ * pageable hipMemcpyAsync runs at the pinned rate (DESIGN.md 6a'), so a
+ * direct ASCII chunk costs the host nothing -- what matters when 8 ranks share
+ * a 16-CPU quota and each has ~2 host threads to pack or stage with. */
+static int stream_direct(void)
+{
+  static const int v = [] {
+    const char* e = getenv("KFMI_STREAM_DIRECT");
+    return e ? (atoi(e) & 3) : 0;
+  }();
+  return v;
+}
+
 struct StreamSlot {
   hipStream_t st = nullptr;
   hipEvent_t done = nullptr;
@@ -362,7 +377,9 @@ static int32_t stream_on(kfmi_dev_index* di, int member, const char* ascii, uint
   const uint32_t rem = size % K;
   const uint32_t steps = (size - rem) / K, spw = 32 / (2 * K), nwords = (steps + spw - 1) / spw;
   const uint32_t rows = nwords + (rem ? 1u : 0u);   /* code-word rows per read */
-  const bool pin_in = host_pinned(ascii), pin_out = host_pinned(results);
+  const int direct = stream_direct();
+  /* pinned, or taken directly from pageable memory: no staging either way */
+  const bool pin_in = host_pinned(ascii) || (direct & 1), pin_out = host_pinned(results) || (direct & 2);
 
   std::lock_guard<std::mutex> lk(g_pool_mu[di->device][member]);
   StreamPool& pool = g_pool[di->device][member];
