@@ -250,8 +250,10 @@ int32_t kfmi_build_index_gpu(const char *text, uint64_t n, uint32_t k, uint32_t 
  * 2, tag 100 or 101; k_out = 2K), without the text: row i's 2K-mer is its
  * K-mer plus the K-mer of row LF_K(i) (DESIGN.md 5d').  The result is the
  * tag-100 index the builders write for that text at k_out, byte for byte
- * (ACGT texts; 'ref'-mode walks that are not a permutation return
- * KFMI_E_BUILDING_FMI); its entries stay in HBM unless want_host_image.  The
+ * (ACGT texts; an index whose LF_K is not a permutation -- 'ref'-mode
+ * indexes of texts with other bytes -- returns KFMI_E_BUILDING_FMI, checked
+ * row by row during the derivation); its entries stay in HBM unless
+ * want_host_image.  The
  * reference's K = 2 files thus search on the K = 4 layout (coop-grp). */
 int32_t kfmi_derive_index_gpu(void *index, uint32_t k_out, int32_t want_host_image, void **out);
 /* Alphabet of the builders (process-wide; NULL = KFMI_ALPHABET, else "acgt"):
@@ -374,10 +376,13 @@ int32_t kfmi_load_sa(const char *fn, void *index);
  * searchIndexGPU / kfmi_search) and an index with samples on the device.
  * Query q's positions are positions[offsets[q] .. offsets[q+1]), in row order
  * (positions[offsets[q] + j] = SA[L_q + j]).  Rows from n+1 on hold no
- * suffix and are not reported (an AltCounters interval can end past n+1); a
- * walk that cannot reach a suffix (a 'ref'-mode index whose BWT is not a
- * permutation) reports 0xFFFFFFFF.  kfmi_last_timing: total, scan, locate
- * kernel (ms).  Errors: 34 before transfer/search, 33 without samples. */
+ * suffix and are not reported (an AltCounters interval can end past n+1).
+ * Before the first walk on a device copy, one LF_K per row checks that LF_K
+ * is a permutation of the non-'$' rows (about one search of n/K reads); an
+ * index that fails it ('ref'-mode indexes of texts with bytes other than
+ * A/C/G/T, whose walks need not end) returns KFMI_E_BUILDING_FMI (9) instead
+ * of walking.  kfmi_last_timing: total, scan, locate kernel (ms).  Errors: 34
+ * before transfer/search, 33 without samples, 9 as above. */
 int32_t         kfmi_locate(void *index, void *results, uint32_t max_occ, void **locations);
 uint64_t        kfmi_locations_total(void *locations);
 const uint64_t *kfmi_locations_offsets(void *locations);    /* num + 1 */

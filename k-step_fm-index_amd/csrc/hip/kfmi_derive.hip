@@ -54,6 +54,16 @@ int32_t derive_index(kfmi_fmi_t* f, uint32_t k_out, int dev, bool host_image, kf
     codes = nullptr;
     isa = nullptr;
   };
+  /* the derivation composes LF_K with itself: only an index whose walks are
+   * the text's (every row reaches a '$' row) has a 2K-step index to derive --
+   * a 'ref'-mode index of a text with bytes other than A/C/G/T does not
+   * (check_lf_walks) */
+  err = check_lf_walks(di, ctx->st);
+  if (!err && di->lf_perm.load() == 0) err = KFMI_E_BUILDING_FMI;
+  if (err) {
+    cleanup();
+    return err;
+  }
   if (hipMalloc((void**) &codes, rows) != hipSuccess || hipMalloc((void**) &isa, 16) != hipSuccess) {
     cleanup();
     return KFMI_E_DEVICE_ALLOC;

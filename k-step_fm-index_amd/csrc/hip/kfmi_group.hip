@@ -118,6 +118,7 @@ static int32_t replicate_index(const kfmi_dev_index* src, int dev, hipStream_t s
   di->sa_bytes = src->sa_bytes;
   di->sa_log2 = src->sa_log2;
   di->sa_gen = src->sa_gen;
+  di->lf_perm.store(src->lf_perm.load());
   di->ac_tail_b0 = src->ac_tail_b0;
   struct Buf { uint32_t* const* from; uint32_t** to; uint64_t bytes; };
   const Buf bufs[3] = {{&src->ent, &di->ent, src->ent_bytes},

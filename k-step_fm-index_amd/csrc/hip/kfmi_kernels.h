@@ -389,6 +389,30 @@ __global__ __launch_bounds__(256) void count_blocks_kernel(IdxArgs ix, const uin
  * written by the host from the text's tail (row 0's code, see the caller);
  * a row whose LF lands on D_s is the row of suffix K + s, the new D_{K+s}
  * (isa[s]). */
+/* The LF_K successor of every row for the walk check (check_lf_walks,
+ * kfmi_search.hip): next[X] = LF_K(X) as a locate walk takes it (lf_row), a
+ * '$' row D_s its own successor; an image past the last row sets *bad. */
+template <class G>
+__global__ __launch_bounds__(256) void lf_next_kernel(IdxArgs ix, uint64_t rows, uint32_t* __restrict__ next,
+                                                      uint32_t* __restrict__ bad)
+{
+  for (uint64_t i = (uint64_t) blockIdx.x * 256 + threadIdx.x; i < rows; i += (uint64_t) gridDim.x * 256) {
+    const uint32_t X = (uint32_t) i;
+    bool dollar = false;
+#pragma unroll
+    for (int s = 0; s < G::K; ++s) dollar = dollar || ix.dl.dpos[s] == X;
+    uint32_t j = X;
+    if (!dollar) {
+      j = lf_row<G>(ix, X);
+      if ((uint64_t) j >= rows) {
+        atomicOr(bad, 1u);
+        j = X;
+      }
+    }
+    next[i] = j;
+  }
+}
+
 template <class G>
 __global__ __launch_bounds__(256) void derive_codes_kernel(IdxArgs ix, uint64_t rows, uint8_t* __restrict__ codes,
                                                            uint32_t* __restrict__ isa)
@@ -535,6 +559,9 @@ struct SearchLaunch {
   /* index derivation: 2K-mer code per row (num rows), the rows of suffixes K..2K-1 */
   uint8_t* derive_codes;
   uint32_t* derive_isa;
+  /* walk check (Op::PermCheck): every row's LF_K successor, and the flag of an image past the rows */
+  uint32_t* perm_next;
+  uint32_t* perm_bad;
 };
 
 template <class G, int SPLIT>
@@ -666,7 +693,15 @@ static hipError_t launch_derive(const SearchLaunch& a)
   return hipErrorInvalidValue;
 }
 
-enum class Op { Task, Coop, Count, Locate, Ftab, RemTab, CountLines, Derive };
+template <class G>
+static hipError_t launch_perm(const SearchLaunch& a)
+{
+  hipLaunchKernelGGL((lf_next_kernel<G>), dim3(grid_blocks((a.num + 255) / 256, 65536)), dim3(256), 0, a.st, a.ix,
+                     a.num, a.perm_next, a.perm_bad);
+  return hipGetLastError();
+}
+
+enum class Op { Task, Coop, Count, Locate, Ftab, RemTab, CountLines, Derive, PermCheck };
 
 /* Defined here, instantiated once per (K, NB, LAY) in kfmi_inst_*.hip. */
 template <int K, int NB, int LAY>
@@ -681,6 +716,7 @@ hipError_t dispatch_one(Op op, const SearchLaunch& a, unsigned long long* d_tota
     case Op::RemTab: return launch_rem_tab<G>(a);
     case Op::CountLines: return launch_count_lines<G>(a, d_total);
     case Op::Derive: return launch_derive<G>(a);
+    case Op::PermCheck: return launch_perm<G>(a);
     default: return launch_count<G>(a, d_total);
   }
 }

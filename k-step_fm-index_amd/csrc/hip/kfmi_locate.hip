@@ -109,6 +109,13 @@ static int32_t locate_on(kfmi_fmi_t* f, kfmi_dev_index* di, uint32_t* d_res, uin
     err = upload_sa(f, di, ctx);
     if (err) return err;
   }
+  if (di->lf_perm.load() < 0) {   /* once per device copy */
+    err = check_lf_walks(di, ctx->st);
+    if (err) return err;
+  }
+  /* an LF_K cycle that misses every '$' row would keep a slot walking for up
+   * to n/K dependent loads before walk_lost gives up */
+  if (di->lf_perm.load() == 0) return KFMI_E_BUILDING_FMI;
   kfmi_locations* L = new (std::nothrow) kfmi_locations();
   if (!L) return KFMI_E_ALLOCATING_RESULTS;
   L->num = num;

@@ -8,6 +8,7 @@
 #define KFMI_RUNTIME_H_
 
 #include <hip/hip_runtime.h>
+#include <atomic>
 #include <stdint.h>
 #include <stdio.h>
 #include <mutex>
@@ -41,6 +42,9 @@ struct kfmi_dev_index {
   uint32_t* ent = nullptr;     /* device entries */
   uint64_t ent_bytes = 0;
   uint32_t* sa = nullptr;      /* locate: row-sampled suffix array */
+  /* every LF_K walk ends at a '$' row (check_lf_walks), checked once before
+   * the first locate walk or derivation: -1 not yet, 0 no (refused), 1 yes */
+  std::atomic<int> lf_perm{-1};
   uint64_t sa_bytes = 0;
   uint32_t sa_log2 = 0, sa_gen = 0;
   /* jump-start tables, one per base count (built on first use, then immutable
@@ -124,6 +128,7 @@ uint32_t ftab_bases(void);
 bool is_coop(int backend);
 int backend_for(uint32_t K);   /* the selected backend, or coop-grp for K = 4 under the implicit default */
 int fused_maxw(int backend, uint32_t bases);   /* bases = K * steps of the batch */
+int32_t check_lf_walks(kfmi_dev_index* di, hipStream_t st);   /* sets di->lf_perm (kfmi_search.hip) */
 hipError_t dispatch(Op op, uint32_t K, uint32_t nb, int lay, const SearchLaunch& a,
                     unsigned long long* d_total = nullptr);
 IdxArgs idx_args(const kfmi_dev_index* di);

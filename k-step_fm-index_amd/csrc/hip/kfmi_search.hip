@@ -853,7 +853,12 @@ int32_t upload_index(kfmi_fmi_t* f, int backend, int dev, DevCtx* ctx, kfmi_dev_
   if (f->steps == 2 && layout_of(backend) == LAY_GRP) {
     /* a K = 2 file (the reference's GPU index) on the grouped-counter layout:
      * its K = 4 index derived on the device, laid out, and dropped again
-     * (DESIGN.md 5d'); the handle keeps the K = 4 device copy */
+     * (DESIGN.md 5d'); the handle keeps the K = 4 device copy.  The K = 4
+     * geometry and row limits are checked first, so a file the layout cannot
+     * take fails before the derivation's buffers are allocated. */
+    if (!geometry_supported(backend, 4, f->nbitmaps, LAY_GRP) ||
+        ((uint64_t) f->nentries + 3u) * f->chunk > 0xFFFFFFFFull)
+      return KFMI_E_BAD_ARGUMENT;
     kfmi_fmi_t* g = nullptr;
     int32_t e = derive_index(f, 4, dev, false, &g);
     if (e) return e;
@@ -1082,6 +1087,71 @@ IdxArgs idx_args(const kfmi_dev_index* di)
   ix.rem = 0;
   ix.split = split_for(di->ent_bytes, di->layout);
   return ix;
+}
+
+/* Pointer jumping over the successor array: out[X] = next[next[X]]. */
+__global__ __launch_bounds__(256) void jump_kernel(const uint32_t* __restrict__ next, uint64_t rows,
+                                                   uint32_t* __restrict__ out)
+{
+  for (uint64_t i = (uint64_t) blockIdx.x * 256 + threadIdx.x; i < rows; i += (uint64_t) gridDim.x * 256)
+    out[i] = next[next[i]];
+}
+
+/* After the jumps every row's successor must be a '$' row D_s. */
+__global__ __launch_bounds__(256) void walk_end_kernel(const uint32_t* __restrict__ next, uint64_t rows, DollarArgs dl,
+                                                       uint32_t K, uint32_t* __restrict__ bad)
+{
+  for (uint64_t i = (uint64_t) blockIdx.x * 256 + threadIdx.x; i < rows; i += (uint64_t) gridDim.x * 256) {
+    const uint32_t e = next[i];
+    bool d = false;
+    for (uint32_t s = 0; s < K; ++s) d = d || dl.dpos[s] == e;
+    if (!d) atomicOr(bad, 2u);
+  }
+}
+
+/* Whether every LF_K walk of di ends at a '$' row -- true of every index of a
+ * text (LF_K takes the row of suffix p to the row of p - K) -- kept in
+ * di->lf_perm.  A 'ref'-mode index of a text with bytes other than A/C/G/T
+ * (the reference builder counts the raw bytes in one order and the codes in
+ * another, genFMindex.c:283-309, :402-424) has LF_K cycles that never reach a
+ * '$' row: locate walks on it need not end and a derivation would compose a
+ * map that is not the text's.  The successor of every row (lf_next_kernel,
+ * '$' rows fixed), then ceil(log2 rows) rounds of pointer jumping, then every
+ * row's successor must be a '$' row.  8 bytes per row of scratch (24 GB at 3
+ * Gbase); one LF per row plus ~32 random-gather passes. */
+int32_t check_lf_walks(kfmi_dev_index* di, hipStream_t st)
+{
+  const uint64_t rows = di->bwtsize;
+  uint32_t *next = nullptr, *tmp = nullptr, *bad = nullptr;
+  auto done = [&](int32_t code) {
+    if (next) (void) hipFree(next);
+    if (tmp) (void) hipFree(tmp);
+    if (bad) (void) hipFree(bad);
+    return code;
+  };
+  if (hipMalloc((void**) &next, 4 * rows) != hipSuccess || hipMalloc((void**) &tmp, 4 * rows) != hipSuccess ||
+      hipMalloc((void**) &bad, 4) != hipSuccess)
+    return done(KFMI_E_DEVICE_ALLOC);
+  SearchLaunch a{};
+  a.st = st;
+  a.ix = idx_args(di);
+  a.num = rows;
+  a.perm_next = next;
+  a.perm_bad = bad;
+  if (hipMemsetAsync(bad, 0, 4, st) != hipSuccess || dispatch(Op::PermCheck, di->K, di->nb, di->layout, a) != hipSuccess)
+    return done(KFMI_E_KERNEL);
+  const dim3 grid(grid_blocks((rows + 255) / 256, 65536));
+  for (uint64_t span = 1; span < rows; span <<= 1) {   /* after round r every row looks 2^r steps ahead */
+    hipLaunchKernelGGL(jump_kernel, grid, dim3(256), 0, st, next, rows, tmp);
+    std::swap(next, tmp);
+  }
+  hipLaunchKernelGGL(walk_end_kernel, grid, dim3(256), 0, st, next, rows, di->dl, di->K, bad);
+  uint32_t h_bad = 0;
+  if (hipGetLastError() != hipSuccess || hipMemcpyAsync(&h_bad, bad, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return done(KFMI_E_KERNEL);
+  di->lf_perm.store(h_bad ? 0 : 1);
+  return done(KFMI_SUCCESS);
 }
 
 /* Reads with m % K = rem != 0 (the reference reads P[-1] there, defect B6):
@@ -1361,6 +1431,7 @@ extern "C" int32_t transferCPUtoGPU(void* index, void* queries, void* results)
   int32_t err = ctx_for(dev, &ctx);
   if (err) return err;
   const int backend = f ? backend_for(f->steps) : kfmi_backend();
+  uint32_t qk = f ? f->steps : 0;   /* K of the device copy, read under the handle's lock */
   if (f) {
     /* the index's device copy is replaced only under the handle's exclusive
      * lock (searches on other threads hold it shared); when it already fits,
@@ -1370,6 +1441,7 @@ extern "C" int32_t transferCPUtoGPU(void* index, void* queries, void* results)
     {
       std::shared_lock<RwLock> sl(index_lock(f));
       ok = fits();
+      if (ok) qk = device_steps(f);
     }
     if (!ok) {
       std::unique_lock<RwLock> ul(index_lock(f));
@@ -1378,6 +1450,7 @@ extern "C" int32_t transferCPUtoGPU(void* index, void* queries, void* results)
         err = upload_index(f, backend, dev, ctx);
         if (err) return err;
       }
+      qk = device_steps(f);
     }
   }
   if (q) {
@@ -1385,7 +1458,7 @@ extern "C" int32_t transferCPUtoGPU(void* index, void* queries, void* results)
     if (!q->h_queries && q->num) {   /* parsed on the device (kfmi_load_queries_gpu): already there */
       if (!q->dev) return KFMI_E_NOT_ON_DEVICE;
       if (q->dev->device != dev) return KFMI_E_BAD_ARGUMENT;
-      query_geometry(q->dev, device_steps(f));
+      query_geometry(q->dev, qk);
       kfmi_dev_queries* dq = q->dev;
       if (dq->nwords + 1 > dq->packed_rows) {   /* K = 3 packs 15 bases per word: a few more rows */
         (void) hipFree(dq->packed);
@@ -1396,7 +1469,7 @@ extern "C" int32_t transferCPUtoGPU(void* index, void* queries, void* results)
         dq->packed_rows = dq->nwords + 1;
       }
     } else {
-      err = upload_queries(q, device_steps(f), dev, ctx);
+      err = upload_queries(q, qk, dev, ctx);
       if (err) return err;
     }
   }

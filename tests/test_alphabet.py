@@ -198,6 +198,16 @@ def test_gpu_search_on_reference_indexes(ref_mode, key, ent):
                 continue                                   # geometry the cooperative kernel rejects (code 33)
             got = K.search_array(idx, reads, be)
             assert np.array_equal(got, want), (key, rk, be)
+        if tag == 100 and ent["k"] == 2 and ent["d"] == 64:
+            # the grouped-counter backends take a K = 2 file through the device
+            # derivation (DESIGN.md 5d'), which needs an LF_K that is a
+            # permutation: this text's N runs make the reference walk's BWT_1
+            # not one, so the derivation refuses (KFMI_E_BUILDING_FMI) instead
+            # of searching a wrong K = 4 index
+            for be in ("coop-grp", "task-grp"):
+                with pytest.raises(K.KfmiError) as e:
+                    K.search_array(idx, reads, be)
+                assert e.value.code == 9, (key, rk, be, e.value.code)
     idx.close()
 
 

@@ -129,3 +129,43 @@ def test_grouped_backends_derive_on_upload(K):
     q.close()
     r.close()
     i2.close()
+
+
+def test_ref_alphabet_derivation_and_locate(K):
+    """'ref'-mode indexes (the reference builder's byte semantics, DESIGN.md
+    4a).  A text of A/C/G/T only is an ordinary index: it derives to the K = 4
+    index built from the text and its searches on coop-grp equal the K = 2
+    ones, and locate works.  A text with N runs and lowercase letters makes
+    the reference walk's LF_K not a permutation (genFMindex.c:347-391): the
+    derivation and locate refuse it (KFMI_E_BUILDING_FMI = 9, the
+    check_lf_walks cycle check) instead of returning a wrong index or walking n/K
+    steps per slot."""
+    rng = np.random.default_rng(11)
+    pure = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=40_001)
+    mixed = pure.copy()
+    mixed[1000:1300] = ord("N")
+    mixed[5000:5050] = np.frombuffer(b"acgt", np.uint8)[rng.integers(0, 4, 50)]
+    reads = pure[rng.integers(0, pure.size - 100, size=2000)[:, None] + np.arange(100)]
+    try:
+        K.set_alphabet("ref")
+        src = K.Index.build(pure.tobytes(), k=2, d=64, sa_rate=8)
+        want4 = K.Index.build(pure.tobytes(), k=4, d=64)
+        got4 = src.derive(4, host_image=True)
+        assert np.array_equal(np.asarray(got4.image()), np.asarray(want4.image()))
+        k2 = K.search_array(src, reads, "task-mid")
+        assert np.array_equal(K.search_array(src, reads, "coop-grp"), k2)
+        res, off, pos = K.locate_array(src, reads[:200], "task-mid")
+        assert off[-1] == int(np.sum(res[1::2].astype(np.int64) - res[0::2]))
+        for x in (src, want4, got4):
+            x.close()
+        bad = K.Index.build(mixed.tobytes(), k=2, d=64, sa_rate=8)
+        with pytest.raises(K.KfmiError) as e:
+            bad.derive(4)
+        assert e.value.code == 9
+        with pytest.raises(K.KfmiError) as e:
+            K.locate_array(bad, reads[:50], "task-mid")
+        assert e.value.code == 9
+        assert K.search_array(bad, reads, "task-mid").shape == (4000,)   # the K = 2 search itself runs
+        bad.close()
+    finally:
+        K.set_alphabet(None)
