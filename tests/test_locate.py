@@ -230,3 +230,42 @@ def test_locate_errors(gpu):
         idx.load_sa(os.path.join(d, "s.sa"))
     loc = gpu.locate(idx, r)
     assert loc.total() == 1 and int(loc.positions()[0]) == 0
+
+
+@pytest.mark.gpu
+def test_locate_refuses_cyclic_walks_fast(kfmi_mod):
+    """A 'ref'-mode index of a text with N runs and lowercase letters (the
+    reference builder's byte semantics) has LF_K cycles that
+    miss every '$' row: a walk there would take up to n/K dependent loads
+    before walk_lost stops it.  Locate checks the walks once per
+    device copy (check_lf_walks: one LF per row and log2(rows) pointer-jumping
+    passes) and refuses with KFMI_E_BUILDING_FMI -- quickly, on a 4 Mbase
+    index -- while the same text's ACGT-only twin locates."""
+    import time
+    K = kfmi_mod
+    if K.device_count() < 1:
+        pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
+    K.set_device(0)
+    rng = np.random.default_rng(21)
+    pure = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=4_000_001)
+    mixed = pure.copy()
+    for s in rng.integers(0, pure.size - 500, size=40):
+        mixed[s:s + int(rng.integers(1, 400))] = ord("N")
+    mixed[100:160] = np.frombuffer(b"acgt", np.uint8)[rng.integers(0, 4, 60)]
+    reads = pure[rng.integers(0, pure.size - 100, size=5000)[:, None] + np.arange(100)]
+    try:
+        K.set_alphabet("ref")
+        for text, ok in ((pure, True), (mixed, False)):
+            idx = K.Index.build(text.tobytes(), k=2, d=64, gpu=True, sa_rate=32)
+            t0 = time.perf_counter()
+            if ok:
+                res, off, pos = K.locate_array(idx, reads, "task-mid")
+                assert off[-1] == int(np.sum(res[1::2].astype(np.int64) - res[0::2]))
+            else:
+                with pytest.raises(K.KfmiError) as e:
+                    K.locate_array(idx, reads, "task-mid")
+                assert e.value.code == 9
+            assert time.perf_counter() - t0 < 30
+            idx.close()
+    finally:
+        K.set_alphabet(None)
