@@ -233,7 +233,7 @@ def test_locate_errors(gpu):
 
 
 @pytest.mark.gpu
-def test_locate_refuses_cyclic_walks_fast(kfmi_mod):
+def test_locate_refuses_cyclic_walks_fast(gpu):
     """A 'ref'-mode index of a text with N runs and lowercase letters (the
     reference builder's byte semantics) has LF_K cycles that
     miss every '$' row: a walk there would take up to n/K dependent loads
@@ -242,10 +242,7 @@ def test_locate_refuses_cyclic_walks_fast(kfmi_mod):
     passes) and refuses with KFMI_E_BUILDING_FMI -- quickly, on a 4 Mbase
     index -- while the same text's ACGT-only twin locates."""
     import time
-    K = kfmi_mod
-    if K.device_count() < 1:
-        pytest.fail("no HIP device visible: GPU tests must run on the MI355X box")
-    K.set_device(0)
+    K = gpu
     rng = np.random.default_rng(21)
     pure = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=4_000_001)
     mixed = pure.copy()
