@@ -15,7 +15,7 @@ run() {  # name, extra args
   timeout -s KILL 400 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_REQ_sum --kernel-include-regex "task_kernel|coop_kernel" -d $OUT/pmc_${T}_$N -o p --output-format csv -- python3 $R/scripts/pmc_variants.py --order $OUT/pmc_${T}_${N}_order.json "$@" > $OUT/pmc_${T}_$N.log 2>&1 || { tail -20 $OUT/pmc_${T}_$N.log; return 33; }
   local CSV=$(find $OUT/pmc_${T}_$N -name "*counter_collection.csv" | head -1)
   cp $CSV $OUT/pmc_${T}_${N}.csv
-  python3 $R/scripts/traffic_variants.py $CSV $OUT/pmc_${T}_${N}_order.json --source "profiles/r05/pmc_${T}_${N}.csv (rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_REQ_sum over scripts/pmc_variants.py $*)" > $OUT/traffic_variants_${T}_$N.json || return 34
+  python3 $R/scripts/traffic_variants.py $CSV $OUT/pmc_${T}_${N}_order.json --source "profiles/${PROF_DIR:-r06}/pmc_${T}_${N}.csv (rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_REQ_sum over scripts/pmc_variants.py $*)" > $OUT/traffic_variants_${T}_$N.json || return 34
   grep -o '"line_requests_per_query": [0-9.]*' $OUT/traffic_variants_${T}_$N.json | head -20
 }
 if [ "$W" = fetch ]; then
