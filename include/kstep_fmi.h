@@ -188,6 +188,16 @@ int32_t     kfmi_set_ftab(uint32_t bases);
  * separate pack launch.  Results are identical either way. */
 int32_t     kfmi_set_split_class(uint32_t cls);
 int32_t     kfmi_set_fused(int32_t on);
+/* Walk check of locate and the K = 2 -> 4 derivation (every LF_K walk must end
+ * at a '$' row; indexes that fail are refused with KFMI_E_BUILDING_FMI), run
+ * once per device copy: 0 = by size (default: full pointer jumping below 2^22
+ * rows, the sampled check above), 1 = always full pointer jumping, 2 = always
+ * the sampled check (which falls back to full jumping when it cannot decide);
+ * other values KFMI_E_BAD_ARGUMENT.  Test knob, process-wide, no environment
+ * variable.  kfmi_walk_check_last: how the last check decided -- 0 none yet,
+ * 1 full, 2 sampled, 3 sampled then full. */
+int32_t     kfmi_set_walk_check(uint32_t mode);
+int32_t     kfmi_walk_check_last(void);
 /* Every entry point leaves the caller's current HIP device as it found it
  * (hipGetDevice before == after), whichever devices it used inside. */
 /* Device groups (runtime multi-GPU behind the same handles; the reference

@@ -1109,6 +1109,176 @@ __global__ __launch_bounds__(256) void walk_end_kernel(const uint32_t* __restric
   }
 }
 
+/* ---- the sampled walk check (large indexes) --------------------------------
+ * Rows whose hashed index has its low 8 bits zero are "samples" (1 in 256,
+ * independent of the LF order); a sample's walk runs over the successor array
+ * to the next sample or '$' row, marking the rows it passes (next[] := WSENT)
+ * and leaving the sample's skeleton successor in next[sample].  Every row
+ * then lies on a sample's path, or is an "orphan" (the few rows before the
+ * first sample of each chain, or a cycle with no sample), and each orphan
+ * walks forward to a stop.  Pointer jumping over the skeleton decides the
+ * rest.  Walks past kWalkLimit steps, a walk running into a marked row (LF not
+ * injective) or list overflow fall back to full pointer jumping. */
+constexpr uint32_t WSENT = 0xFFFFFFFFu;
+constexpr uint32_t kWalkLimit = 1u << 16;
+constexpr uint32_t kOrphanCap = 1u << 16;
+enum : uint32_t { WALK_BAD_IMAGE = 1u, WALK_CYCLE = 2u, WALK_FALLBACK = 4u };
+
+__device__ __forceinline__ bool walk_sample(uint32_t x)
+{
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return (x & 255u) == 0;
+}
+
+__device__ __forceinline__ bool walk_dollar(uint32_t x, const DollarArgs& dl, uint32_t K)
+{
+  bool d = false;
+  for (uint32_t s = 0; s < K; ++s) d = d || dl.dpos[s] == x;
+  return d;
+}
+
+/* Appends row i to list (wave-aggregated) when want; overflow sets the fallback flag. */
+__device__ __forceinline__ void walk_append(bool want, uint32_t i, uint32_t* __restrict__ list, uint32_t cap,
+                                            uint32_t* __restrict__ count, uint32_t* __restrict__ flags)
+{
+  const uint64_t m = __ballot(want);
+  if (!m) return;
+  const uint32_t lane = threadIdx.x & 63u;
+  const int leader = __ffsll((unsigned long long) m) - 1;
+  uint32_t base = 0;
+  if ((int) lane == leader) base = atomicAdd(count, (uint32_t) __popcll(m));
+  base = __shfl(base, leader);
+  if (want) {
+    const uint32_t slot = base + __builtin_amdgcn_mbcnt_hi((uint32_t) (m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) m, 0u));
+    if (slot < cap) list[slot] = i;
+    else atomicOr(flags, WALK_FALLBACK);
+  }
+}
+
+/* The sample list: every non-'$' row with walk_sample(row).  One block per
+ * kSampleChunk rows gathers its ~256 samples in LDS and claims their slots
+ * with one global atomic (one counter shared by 12 M per-wave atomics was
+ * 118 ms at 3 Gbase, all of it contention). */
+constexpr uint32_t kSampleChunk = 1u << 16;
+constexpr uint32_t kSampleBuf = 1024;   /* Binomial(65536, 1/256): mean 256, sd 16 */
+
+__global__ __launch_bounds__(256) void walk_samples_kernel(uint64_t rows, DollarArgs dl, uint32_t K,
+                                                           uint32_t* __restrict__ list, uint32_t cap,
+                                                           uint32_t* __restrict__ count, uint32_t* __restrict__ flags)
+{
+  __shared__ uint32_t buf[kSampleBuf];
+  __shared__ uint32_t n, base;
+  for (uint64_t c0 = (uint64_t) blockIdx.x * kSampleChunk; c0 < rows; c0 += (uint64_t) gridDim.x * kSampleChunk) {
+    if (threadIdx.x == 0) n = 0;
+    __syncthreads();
+    const uint64_t c1 = min(rows, c0 + kSampleChunk);
+    for (uint64_t i = c0 + threadIdx.x; i < c1; i += 256)
+      if (walk_sample((uint32_t) i) && !walk_dollar((uint32_t) i, dl, K)) {
+        const uint32_t s = atomicAdd(&n, 1u);
+        if (s < kSampleBuf) buf[s] = (uint32_t) i;
+      }
+    __syncthreads();
+    const uint32_t m = min(n, kSampleBuf);
+    if (threadIdx.x == 0) {
+      if (n > kSampleBuf) atomicOr(flags, WALK_FALLBACK);
+      base = atomicAdd(count, m);
+    }
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < m; t += 256) {
+      if (base + t < cap) list[base + t] = buf[t];
+      else atomicOr(flags, WALK_FALLBACK);
+    }
+    __syncthreads();
+  }
+}
+
+/* Each sample's walk to the next stop, marking the rows passed. */
+__global__ __launch_bounds__(256) void walk_paths_kernel(uint32_t* __restrict__ next, const uint32_t* __restrict__ list,
+                                                         const uint32_t* __restrict__ count, uint32_t cap, DollarArgs dl,
+                                                         uint32_t K, uint32_t* __restrict__ flags)
+{
+  const uint32_t n = min(*count, cap);
+  for (uint32_t t = blockIdx.x * 256 + threadIdx.x; t < n; t += gridDim.x * 256) {
+    const uint32_t s = list[t];
+    uint32_t j = next[s], steps = 0;
+    while (!walk_dollar(j, dl, K) && !walk_sample(j)) {
+      const uint32_t nj = next[j];
+      if (nj == WSENT || ++steps > kWalkLimit) {   /* two walks meet (LF not injective) or a long gap */
+        atomicOr(flags, WALK_FALLBACK);
+        break;
+      }
+      next[j] = WSENT;
+      j = nj;
+    }
+    next[s] = j;
+  }
+}
+
+/* Rows on no sample's path: neither marked, a sample nor a '$' row. */
+__global__ __launch_bounds__(256) void walk_orphans_kernel(const uint32_t* __restrict__ next, uint64_t rows, DollarArgs dl,
+                                                           uint32_t K, uint32_t* __restrict__ list,
+                                                           uint32_t* __restrict__ count, uint32_t* __restrict__ flags)
+{
+  for (uint64_t base = (uint64_t) blockIdx.x * 256 + (threadIdx.x & ~63u); base < rows; base += (uint64_t) gridDim.x * 256) {
+    const uint64_t i = base + (threadIdx.x & 63u);
+    bool want = false;
+    if (i < rows) {
+      const uint32_t x = (uint32_t) i;
+      want = next[i] != WSENT && !walk_sample(x) && !walk_dollar(x, dl, K);
+    }
+    walk_append(want, (uint32_t) i, list, kOrphanCap, count, flags);
+  }
+}
+
+/* Each orphan walks over unmarked rows to a stop; coming back to itself is a
+ * cycle with no sample and no '$' row. */
+__global__ __launch_bounds__(256) void walk_orphan_paths_kernel(const uint32_t* __restrict__ next,
+                                                                const uint32_t* __restrict__ list,
+                                                                const uint32_t* __restrict__ count, DollarArgs dl,
+                                                                uint32_t K, uint32_t* __restrict__ flags)
+{
+  const uint32_t n = min(*count, kOrphanCap);
+  for (uint32_t t = blockIdx.x * 256 + threadIdx.x; t < n; t += gridDim.x * 256) {
+    const uint32_t o = list[t];
+    uint32_t j = o;
+    for (uint32_t steps = 0;; ++steps) {
+      const uint32_t nj = next[j];
+      if (nj == o) {
+        atomicOr(flags, WALK_CYCLE);
+        break;
+      }
+      if (walk_dollar(nj, dl, K) || walk_sample(nj) || next[nj] == WSENT) break;   /* a stop, or a sample's path */
+      if (steps >= kWalkLimit) {
+        atomicOr(flags, WALK_FALLBACK);
+        break;
+      }
+      j = nj;
+    }
+  }
+}
+
+/* One round of pointer jumping over the samples' skeleton successors (in
+ * place: a pointer read mid-round is at least as far along as the round's
+ * start value, so each round still at least doubles every distance). */
+__global__ __launch_bounds__(256) void walk_skeleton_kernel(uint32_t* __restrict__ next, const uint32_t* __restrict__ list,
+                                                            const uint32_t* __restrict__ count, uint32_t cap,
+                                                            DollarArgs dl, uint32_t K, uint32_t* __restrict__ flags,
+                                                            bool last)
+{
+  const uint32_t n = min(*count, cap);
+  for (uint32_t t = blockIdx.x * 256 + threadIdx.x; t < n; t += gridDim.x * 256) {
+    const uint32_t s = list[t];
+    const uint32_t j = next[s];
+    if (walk_dollar(j, dl, K)) continue;
+    if (last) atomicOr(flags, WALK_CYCLE);
+    else next[s] = next[j];
+  }
+}
+
 /* Whether every LF_K walk of di ends at a '$' row -- true of every index of a
  * text (LF_K takes the row of suffix p to the row of p - K) -- kept in
  * di->lf_perm.  A 'ref'-mode index of a text with bytes other than A/C/G/T
@@ -1116,12 +1286,29 @@ __global__ __launch_bounds__(256) void walk_end_kernel(const uint32_t* __restric
  * another, genFMindex.c:283-309, :402-424) has LF_K cycles that never reach a
  * '$' row: locate walks on it need not end and a derivation would compose a
  * map that is not the text's.  The successor of every row (lf_next_kernel,
- * '$' rows fixed), then ceil(log2 rows) rounds of pointer jumping, then every
- * row's successor must be a '$' row.  8 bytes per row of scratch (24 GB at 3
- * Gbase); one LF per row plus ~32 random-gather passes. */
+ * '$' rows fixed), then, below 2^22 rows or when the sampled check falls
+ * back, ceil(log2 rows) rounds of full pointer jumping (8 bytes per row of
+ * scratch, ~32 random-gather passes at 3 Gbase: 2.0 s); otherwise the sampled
+ * check above (4 bytes per row, about one random gather and one random store
+ * per row). */
+static std::atomic<int> g_walk_mode{0};   /* 0 = by size, 1 = full pointer jumping, 2 = sampled */
+static std::atomic<int> g_walk_last{0};   /* 1 = full, 2 = sampled, 3 = sampled then full */
+
+extern "C" int32_t kfmi_set_walk_check(uint32_t mode)
+{
+  if (mode > 2) return KFMI_E_BAD_ARGUMENT;
+  g_walk_mode.store((int) mode, std::memory_order_relaxed);
+  return KFMI_SUCCESS;
+}
+
+extern "C" int32_t kfmi_walk_check_last(void) { return g_walk_last.load(std::memory_order_relaxed); }
+
 int32_t check_lf_walks(kfmi_dev_index* di, hipStream_t st)
 {
   const uint64_t rows = di->bwtsize;
+  const int mode = g_walk_mode.load(std::memory_order_relaxed);
+  const bool sampled = mode == 2 || (mode == 0 && rows >= (1ull << 22));
+  const uint32_t cap = (uint32_t) std::min<uint64_t>(rows / 128 + 4096, rows);
   uint32_t *next = nullptr, *tmp = nullptr, *bad = nullptr;
   auto done = [&](int32_t code) {
     if (next) (void) hipFree(next);
@@ -1129,8 +1316,9 @@ int32_t check_lf_walks(kfmi_dev_index* di, hipStream_t st)
     if (bad) (void) hipFree(bad);
     return code;
   };
-  if (hipMalloc((void**) &next, 4 * rows) != hipSuccess || hipMalloc((void**) &tmp, 4 * rows) != hipSuccess ||
-      hipMalloc((void**) &bad, 4) != hipSuccess)
+  /* bad[0] flags, bad[1] sample count, bad[2] orphan count, then the lists */
+  const uint64_t tmp_words = sampled ? 3 + (uint64_t) cap + kOrphanCap : 4;
+  if (hipMalloc((void**) &next, 4 * rows) != hipSuccess || hipMalloc((void**) &bad, 4 * tmp_words) != hipSuccess)
     return done(KFMI_E_DEVICE_ALLOC);
   SearchLaunch a{};
   a.st = st;
@@ -1138,18 +1326,44 @@ int32_t check_lf_walks(kfmi_dev_index* di, hipStream_t st)
   a.num = rows;
   a.perm_next = next;
   a.perm_bad = bad;
-  if (hipMemsetAsync(bad, 0, 4, st) != hipSuccess || dispatch(Op::PermCheck, di->K, di->nb, di->layout, a) != hipSuccess)
+  auto fetch_flags = [&](uint32_t& h) {
+    return hipGetLastError() == hipSuccess && hipMemcpyAsync(&h, bad, 4, hipMemcpyDeviceToHost, st) == hipSuccess &&
+           hipStreamSynchronize(st) == hipSuccess;
+  };
+  if (hipMemsetAsync(bad, 0, 12, st) != hipSuccess || dispatch(Op::PermCheck, di->K, di->nb, di->layout, a) != hipSuccess)
     return done(KFMI_E_KERNEL);
   const dim3 grid(grid_blocks((rows + 255) / 256, 65536));
+  uint32_t h_bad = 0;
+  if (sampled) {
+    uint32_t* list = bad + 3;
+    uint32_t* orphans = list + cap;
+    const dim3 wgrid(grid_blocks((cap + 255) / 256, 8192));
+    hipLaunchKernelGGL(walk_samples_kernel, dim3(grid_blocks((rows + kSampleChunk - 1) / kSampleChunk, 65536)), dim3(256), 0,
+                       st, rows, di->dl, di->K, list, cap, bad + 1, bad);
+    hipLaunchKernelGGL(walk_paths_kernel, wgrid, dim3(256), 0, st, next, list, bad + 1, cap, di->dl, di->K, bad);
+    hipLaunchKernelGGL(walk_orphans_kernel, grid, dim3(256), 0, st, next, rows, di->dl, di->K, orphans, bad + 2, bad);
+    hipLaunchKernelGGL(walk_orphan_paths_kernel, dim3(256), dim3(256), 0, st, next, orphans, bad + 2, di->dl, di->K, bad);
+    for (uint64_t span = 1; span <= cap; span <<= 1)   /* skeleton paths are at most cap long */
+      hipLaunchKernelGGL(walk_skeleton_kernel, wgrid, dim3(256), 0, st, next, list, bad + 1, cap, di->dl, di->K, bad, false);
+    hipLaunchKernelGGL(walk_skeleton_kernel, wgrid, dim3(256), 0, st, next, list, bad + 1, cap, di->dl, di->K, bad, true);
+    if (!fetch_flags(h_bad)) return done(KFMI_E_KERNEL);
+    if ((h_bad & (WALK_BAD_IMAGE | WALK_CYCLE)) || !(h_bad & WALK_FALLBACK)) {
+      g_walk_last.store(2, std::memory_order_relaxed);
+      di->lf_perm.store((h_bad & (WALK_BAD_IMAGE | WALK_CYCLE)) ? 0 : 1);
+      return done(KFMI_SUCCESS);
+    }
+    /* undecided: the successors again, then full pointer jumping */
+    if (hipMemsetAsync(bad, 0, 4, st) != hipSuccess || dispatch(Op::PermCheck, di->K, di->nb, di->layout, a) != hipSuccess)
+      return done(KFMI_E_KERNEL);
+  }
+  if (hipMalloc((void**) &tmp, 4 * rows) != hipSuccess) return done(KFMI_E_DEVICE_ALLOC);
   for (uint64_t span = 1; span < rows; span <<= 1) {   /* after round r every row looks 2^r steps ahead */
     hipLaunchKernelGGL(jump_kernel, grid, dim3(256), 0, st, next, rows, tmp);
     std::swap(next, tmp);
   }
   hipLaunchKernelGGL(walk_end_kernel, grid, dim3(256), 0, st, next, rows, di->dl, di->K, bad);
-  uint32_t h_bad = 0;
-  if (hipGetLastError() != hipSuccess || hipMemcpyAsync(&h_bad, bad, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
-      hipStreamSynchronize(st) != hipSuccess)
-    return done(KFMI_E_KERNEL);
+  if (!fetch_flags(h_bad)) return done(KFMI_E_KERNEL);
+  g_walk_last.store(sampled ? 3 : 1, std::memory_order_relaxed);
   di->lf_perm.store(h_bad ? 0 : 1);
   return done(KFMI_SUCCESS);
 }

@@ -120,6 +120,8 @@ def load() -> ctypes.CDLL:
         "kfmi_set_ftab": (i32, [u32]),
         "kfmi_set_split_class": (i32, [u32]),
         "kfmi_set_fused": (i32, [i32]),
+        "kfmi_set_walk_check": (i32, [u32]),
+        "kfmi_walk_check_last": (i32, []),
         "kfmi_set_alphabet": (i32, [ctypes.c_char_p]),
         "kfmi_index_sa": (i32, [vp, pvp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint32)]),
         "kfmi_save_sa": (i32, [ctypes.c_char_p, vp]),
@@ -172,6 +174,17 @@ def set_fused(on: bool) -> None:
     """In-kernel query packing where it fits (True, default) or always the
     separate pack launch (False); process-wide test knob (KFMI_FUSED)."""
     _check(load().kfmi_set_fused(1 if on else 0), f"set_fused({on})")
+
+
+def set_walk_check(mode: int) -> None:
+    """Walk check of locate / derivation: 0 = by size (default), 1 = full
+    pointer jumping, 2 = the sampled check; process-wide test knob."""
+    _check(load().kfmi_set_walk_check(int(mode)), f"set_walk_check({mode})")
+
+
+def walk_check_last() -> int:
+    """How the last walk check decided: 0 none yet, 1 full, 2 sampled, 3 sampled then full."""
+    return int(load().kfmi_walk_check_last())
 
 
 def set_alphabet(mode: str | None) -> None:

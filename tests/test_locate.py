@@ -238,13 +238,13 @@ def test_locate_refuses_cyclic_walks_fast(gpu):
     reference builder's byte semantics) has LF_K cycles that
     miss every '$' row: a walk there would take up to n/K dependent loads
     before walk_lost stops it.  Locate checks the walks once per
-    device copy (check_lf_walks: one LF per row and log2(rows) pointer-jumping
-    passes) and refuses with KFMI_E_BUILDING_FMI -- quickly, on a 4 Mbase
-    index -- while the same text's ACGT-only twin locates."""
+    device copy (check_lf_walks; at 4.5 Mbase, above 2^22 rows, the sampled
+    check) and refuses with KFMI_E_BUILDING_FMI -- quickly -- while the same
+    text's ACGT-only twin locates."""
     import time
     K = gpu
     rng = np.random.default_rng(21)
-    pure = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=4_000_001)
+    pure = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=4_500_001)
     mixed = pure.copy()
     for s in rng.integers(0, pure.size - 500, size=40):
         mixed[s:s + int(rng.integers(1, 400))] = ord("N")
@@ -258,11 +258,72 @@ def test_locate_refuses_cyclic_walks_fast(gpu):
             if ok:
                 res, off, pos = K.locate_array(idx, reads, "task-mid")
                 assert off[-1] == int(np.sum(res[1::2].astype(np.int64) - res[0::2]))
+                assert K.walk_check_last() == 2          # decided by the sampled check alone
             else:
                 with pytest.raises(K.KfmiError) as e:
                     K.locate_array(idx, reads, "task-mid")
                 assert e.value.code == 9
+                assert K.walk_check_last() in (2, 3)
             assert time.perf_counter() - t0 < 30
             idx.close()
     finally:
         K.set_alphabet(None)
+
+
+def _walk_texts(rng):
+    """Texts whose LF_K orders are far from random: runs, periods, repeats."""
+    acgt = np.frombuffer(b"ACGT", np.uint8)
+    rnd = rng.choice(acgt, size=300_001)
+    rep = rnd.copy()
+    rep[150_000:290_000] = np.tile(rnd[:14_000], 10)
+    return {"random": rnd, "all-A": np.full(200_001, ord("A"), np.uint8),
+            "ACGT-period": np.tile(acgt, 60_000), "AC-period": np.tile(acgt[:2], 90_001),
+            "period-7": np.tile(rng.choice(acgt, 7), 40_000), "repeats": rep}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [1, 2])
+def test_walk_check_full_and_sampled_agree(gpu, k):
+    """The sampled walk check (1-in-256 hashed sample rows, their paths marked,
+    orphans walked, pointer jumping over the samples' skeleton) against full
+    pointer jumping over every row, forced through kfmi_set_walk_check on
+    indexes below the size switch: both accept every text of a valid index
+    (random, a single letter, short periods, long repeats) and locate equals
+    the brute-force suffix array; both refuse the 'ref'-mode N-rich text."""
+    K = gpu
+    rng = np.random.default_rng(5 + k)
+    try:
+        for name, t in _walk_texts(rng).items():
+            text = t.tobytes()
+            sa = np.array(util.suffix_array(text + b"$"), dtype=np.int64)
+            q = t[rng.integers(0, t.size - 40, size=300)[:, None] + np.arange(40)]
+            for mode in (1, 2):
+                K.set_walk_check(mode)
+                idx = K.Index.build(text, k=k, d=64, gpu=True, sa_rate=8)
+                res, off, pos = K.locate_array(idx, q, "task-mid", max_occ=64)
+                assert K.walk_check_last() == (1 if mode == 1 else 2), (name, mode)
+                assert np.array_equal(pos, _expected(sa, res, 64)[1]), (name, mode)
+                idx.close()
+        mixed = _walk_texts(rng)["random"].copy()
+        mixed[1000:1300] = ord("N")
+        mixed[5000:5050] = np.frombuffer(b"acgt", np.uint8)[rng.integers(0, 4, 50)]
+        K.set_alphabet("ref")
+        for mode in (1, 2):
+            K.set_walk_check(mode)
+            bad = K.Index.build(mixed.tobytes(), k=2, d=64, gpu=True, sa_rate=8)
+            with pytest.raises(K.KfmiError) as e:
+                K.locate_array(bad, q, "task-mid")
+            assert e.value.code == 9, mode
+            bad.close()
+    finally:
+        K.set_alphabet(None)
+        K.set_walk_check(0)
+
+
+def test_walk_check_mode_argument(kfmi_mod):
+    """kfmi_set_walk_check takes 0, 1 or 2 (no device needed)."""
+    K = kfmi_mod
+    with pytest.raises(K.KfmiError):
+        K.set_walk_check(3)
+    K.set_walk_check(1)
+    K.set_walk_check(0)
