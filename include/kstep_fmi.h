@@ -260,10 +260,10 @@ int32_t kfmi_build_index_gpu(const char *text, uint64_t n, uint32_t k, uint32_t 
  * 2, tag 100 or 101; k_out = 2K), without the text: row i's 2K-mer is its
  * K-mer plus the K-mer of row LF_K(i) (DESIGN.md 5d').  The result is the
  * tag-100 index the builders write for that text at k_out, byte for byte
- * (ACGT texts; an index whose LF_K is not a permutation -- 'ref'-mode
- * indexes of texts with other bytes -- returns KFMI_E_BUILDING_FMI, checked
- * row by row during the derivation); its entries stay in HBM unless
- * want_host_image.  The
+ * (ACGT texts; an index with an LF_K walk that never reaches a '$' row --
+ * 'ref'-mode indexes of texts with other bytes -- returns
+ * KFMI_E_BUILDING_FMI, from the walk check run before deriving, see
+ * kfmi_set_walk_check); its entries stay in HBM unless want_host_image.  The
  * reference's K = 2 files thus search on the K = 4 layout (coop-grp). */
 int32_t kfmi_derive_index_gpu(void *index, uint32_t k_out, int32_t want_host_image, void **out);
 /* Alphabet of the builders (process-wide; NULL = KFMI_ALPHABET, else "acgt"):
@@ -272,8 +272,9 @@ int32_t kfmi_derive_index_gpu(void *index, uint32_t k_out, int32_t want_host_ima
  *          consistent index of that text (true suffix-array intervals);
  *   "ref"  byte-compatible with the reference builder (genFMindex.c) on any
  *          text: raw-byte suffix order (divbwt64), base2index codes, and for
- *          K >= 2 its LF walk, whose unwritten rows hold KFMI_REF_FILL (the
- *          reference: uninitialised malloc memory).  loadRef also copies the
+ *          K >= 2 its LF walk; rows the walk never writes hold code 0 (A)
+ *          where the reference leaves uninitialised malloc memory (the
+ *          tests emulate its bytes, tests/ref_fill.py).  loadRef also copies the
  *          file the reference's way (readRef, common.c:42-76: later header
  *          lines kept, 255-byte fgets pieces each losing their last byte).
  * All three agree on ACGT-only text. */
@@ -387,11 +388,12 @@ int32_t kfmi_load_sa(const char *fn, void *index);
  * Query q's positions are positions[offsets[q] .. offsets[q+1]), in row order
  * (positions[offsets[q] + j] = SA[L_q + j]).  Rows from n+1 on hold no
  * suffix and are not reported (an AltCounters interval can end past n+1).
- * Before the first walk on a device copy, one LF_K per row checks that LF_K
- * is a permutation of the non-'$' rows (about one search of n/K reads); an
- * index that fails it ('ref'-mode indexes of texts with bytes other than
- * A/C/G/T, whose walks need not end) returns KFMI_E_BUILDING_FMI (9) instead
- * of walking.  kfmi_last_timing: total, scan, locate kernel (ms).  Errors: 34
+ * Before the first walk on a device copy, the walk check (kfmi_set_walk_check:
+ * one LF_K per row, then the sampled check or pointer jumping; 0.16 s at 3
+ * Gbase) verifies that every LF_K walk ends at a '$' row; an index that fails
+ * it ('ref'-mode indexes of texts with bytes other than A/C/G/T, whose walks
+ * can cycle and would never end) returns KFMI_E_BUILDING_FMI (9) instead of
+ * walking, so no slot ever runs the walk_lost cap of n/K steps.  kfmi_last_timing: total, scan, locate kernel (ms).  Errors: 34
  * before transfer/search, 33 without samples, 9 as above. */
 int32_t         kfmi_locate(void *index, void *results, uint32_t max_occ, void **locations);
 uint64_t        kfmi_locations_total(void *locations);
