@@ -1236,7 +1236,7 @@ __global__ __launch_bounds__(256) void walk_orphans_kernel(const uint32_t* __res
 
 /* Each orphan walks over unmarked rows to a stop; coming back to itself is a
  * cycle with no sample and no '$' row. */
-__global__ __launch_bounds__(256) void walk_orphan_paths_kernel(const uint32_t* __restrict__ next,
+__global__ __launch_bounds__(256) void walk_orphan_paths_kernel(const uint32_t* __restrict__ next, uint64_t rows,
                                                                 const uint32_t* __restrict__ list,
                                                                 const uint32_t* __restrict__ count, DollarArgs dl,
                                                                 uint32_t K, uint32_t* __restrict__ flags)
@@ -1247,6 +1247,10 @@ __global__ __launch_bounds__(256) void walk_orphan_paths_kernel(const uint32_t* 
     uint32_t j = o;
     for (uint32_t steps = 0;; ++steps) {
       const uint32_t nj = next[j];
+      if ((uint64_t) nj >= rows) {   /* never: j is unmarked and lf_next_kernel keeps images in range */
+        atomicOr(flags, WALK_FALLBACK);
+        break;
+      }
       if (nj == o) {
         atomicOr(flags, WALK_CYCLE);
         break;
@@ -1264,7 +1268,8 @@ __global__ __launch_bounds__(256) void walk_orphan_paths_kernel(const uint32_t* 
 /* One round of pointer jumping over the samples' skeleton successors (in
  * place: a pointer read mid-round is at least as far along as the round's
  * start value, so each round still at least doubles every distance). */
-__global__ __launch_bounds__(256) void walk_skeleton_kernel(uint32_t* __restrict__ next, const uint32_t* __restrict__ list,
+__global__ __launch_bounds__(256) void walk_skeleton_kernel(uint32_t* __restrict__ next, uint64_t rows,
+                                                            const uint32_t* __restrict__ list,
                                                             const uint32_t* __restrict__ count, uint32_t cap,
                                                             DollarArgs dl, uint32_t K, uint32_t* __restrict__ flags,
                                                             bool last)
@@ -1274,6 +1279,10 @@ __global__ __launch_bounds__(256) void walk_skeleton_kernel(uint32_t* __restrict
     const uint32_t s = list[t];
     const uint32_t j = next[s];
     if (walk_dollar(j, dl, K)) continue;
+    if ((uint64_t) j >= rows) {   /* a mark, not a row: only after a walk broke off (the host skips us then) */
+      atomicOr(flags, WALK_FALLBACK);
+      continue;
+    }
     if (last) atomicOr(flags, WALK_CYCLE);
     else next[s] = next[j];
   }
@@ -1342,11 +1351,17 @@ int32_t check_lf_walks(kfmi_dev_index* di, hipStream_t st)
                        st, rows, di->dl, di->K, list, cap, bad + 1, bad);
     hipLaunchKernelGGL(walk_paths_kernel, wgrid, dim3(256), 0, st, next, list, bad + 1, cap, di->dl, di->K, bad);
     hipLaunchKernelGGL(walk_orphans_kernel, grid, dim3(256), 0, st, next, rows, di->dl, di->K, orphans, bad + 2, bad);
-    hipLaunchKernelGGL(walk_orphan_paths_kernel, dim3(256), dim3(256), 0, st, next, orphans, bad + 2, di->dl, di->K, bad);
-    for (uint64_t span = 1; span <= cap; span <<= 1)   /* skeleton paths are at most cap long */
-      hipLaunchKernelGGL(walk_skeleton_kernel, wgrid, dim3(256), 0, st, next, list, bad + 1, cap, di->dl, di->K, bad, false);
-    hipLaunchKernelGGL(walk_skeleton_kernel, wgrid, dim3(256), 0, st, next, list, bad + 1, cap, di->dl, di->K, bad, true);
+    hipLaunchKernelGGL(walk_orphan_paths_kernel, dim3(256), dim3(256), 0, st, next, rows, orphans, bad + 2, di->dl, di->K,
+                       bad);
     if (!fetch_flags(h_bad)) return done(KFMI_E_KERNEL);
+    if (!h_bad) {   /* every walk reached a stop: the skeleton decides (after a broken walk it may hold marks) */
+      for (uint64_t span = 1; span <= cap; span <<= 1)   /* skeleton paths are at most cap long */
+        hipLaunchKernelGGL(walk_skeleton_kernel, wgrid, dim3(256), 0, st, next, rows, list, bad + 1, cap, di->dl, di->K,
+                           bad, false);
+      hipLaunchKernelGGL(walk_skeleton_kernel, wgrid, dim3(256), 0, st, next, rows, list, bad + 1, cap, di->dl, di->K, bad,
+                         true);
+      if (!fetch_flags(h_bad)) return done(KFMI_E_KERNEL);
+    }
     if ((h_bad & (WALK_BAD_IMAGE | WALK_CYCLE)) || !(h_bad & WALK_FALLBACK)) {
       g_walk_last.store(2, std::memory_order_relaxed);
       di->lf_perm.store((h_bad & (WALK_BAD_IMAGE | WALK_CYCLE)) ? 0 : 1);

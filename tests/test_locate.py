@@ -327,3 +327,53 @@ def test_walk_check_mode_argument(kfmi_mod):
         K.set_walk_check(3)
     K.set_walk_check(1)
     K.set_walk_check(0)
+
+
+@pytest.mark.gpu
+def test_walk_check_modes_agree_on_corrupted_counters(gpu, tmp_path):
+    """Indexes whose LF_K is not a text's: one counter of a valid image moved
+    by a few rows, so that LF_K merges rows, skips rows, leaves the table or
+    closes cycles.  Full pointer jumping and the sampled check (which falls
+    back to full jumping when two walks meet) must give the same verdict on
+    each: refuse with KFMI_E_BUILDING_FMI, or accept and locate."""
+    from oracle import oracle
+    K = gpu
+    rng = np.random.default_rng(44)
+    t = rng.choice(ACGT, size=60_001)
+    src = K.Index.build(t.tobytes(), k=2, d=64, gpu=True, sa_rate=8)
+    src.save_sa(str(tmp_path / "x.sa"))
+    img = np.array(src.image(), dtype=np.uint8, copy=True)
+    src.close()
+    h = oracle.header(img)
+    k, d, ne = h["steps"], h["chunk"], h["nentries"]
+    nb = d // 32
+    ew = 2 * nb * k + 4 ** k
+    q = t[rng.integers(0, t.size - 40, size=200)[:, None] + np.arange(40)]
+    verdicts = {}
+    try:
+        for trial in range(24):
+            bad = img.copy()
+            ent = bad[bad.size - 4 * ew * ne:].view(np.uint32).reshape(ne, ew)
+            b, c = int(rng.integers(1, ne)), int(rng.integers(0, 4 ** k))
+            delta = int(rng.choice([-3, -1, 1, 3, 64, -64]))
+            if int(ent[b, 2 * nb * k + c]) + delta < 0:
+                continue
+            ent[b, 2 * nb * k + c] = np.uint32(int(ent[b, 2 * nb * k + c]) + delta)
+            got = []
+            for mode in (1, 2):
+                K.set_walk_check(mode)
+                idx = K.Index.from_image(bad)
+                idx.load_sa(str(tmp_path / "x.sa"))
+                try:
+                    K.locate_array(idx, q, "task-mid", max_occ=16)
+                    got.append("accepted")
+                except K.KfmiError as e:
+                    assert e.code == 9, (trial, mode, e.code)
+                    got.append("refused")
+                assert K.walk_check_last() in ((1,) if mode == 1 else (2, 3))
+                idx.close()
+            assert got[0] == got[1], (trial, b, c, delta, got)
+            verdicts[got[0]] = verdicts.get(got[0], 0) + 1
+    finally:
+        K.set_walk_check(0)
+    assert verdicts.get("refused", 0) > 0, verdicts
