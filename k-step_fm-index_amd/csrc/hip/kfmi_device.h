@@ -117,6 +117,12 @@ struct IdxArgs {
   // beyond the translation reach (~3.5 GB) stalls on translation; 16-32 pages
   // per instruction do not (profiles/r02/gather_mask_r2ag.jsonl)
   uint32_t split;
+  // largest row an LF step may return (idx_args): the last row of the last
+  // block every layout holds.  No result of a valid index comes near it (plain
+  // results stay <= n+1 + d, AltCounters ones <= ac_clamp's cap); it keeps the
+  // next step's loads inside the table when the counters or '$' rows of a
+  // loaded file are corrupt (a wrapped or oversized counter).
+  uint32_t lf_cap;
 };
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
@@ -489,10 +495,10 @@ __device__ __forceinline__ uint32_t finish(const IdxArgs& ix, uint32_t cnt, uint
       const bool want = G::LAY == LAY_MIDAC && ac_rule_e<G>(b, c);
       v = v - (e ? dup : 0u) + (want ? dup : 0u);
     }
-    return v;
+    return min(v, ix.lf_cap);
   }
-  if constexpr (G::TWO_SIDED) return e ? cnt - bc : cnt + bc;
-  return cnt + bc;
+  if constexpr (G::TWO_SIDED) return min(e ? cnt - bc : cnt + bc, ix.lf_cap);
+  return min(cnt + bc, ix.lf_cap);
 }
 
 // line_local_prev's step: cnt = cnt_{b-1}[c], pop = rows of code c in block b-1
@@ -515,7 +521,7 @@ __device__ __forceinline__ uint32_t finish_prev(const IdxArgs& ix, uint32_t cnt,
     if (G::K > 1 && ac_rule_e<G>(b, c)) v += dollar_dup<G::K>(ix.dl, b, c);
     return ac_clamp<G>(ix, v);
   }
-  return v;
+  return min(v, ix.lf_cap);
 }
 
 // LAY_MIDAC, block b >= E-1: the AltCounters searcher's step

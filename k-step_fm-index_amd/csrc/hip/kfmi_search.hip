@@ -1086,6 +1086,14 @@ IdxArgs idx_args(const kfmi_dev_index* di)
   ix.rtab = nullptr;
   ix.rem = 0;
   ix.split = split_for(di->ent_bytes, di->layout);
+  /* the last row of block nentries, which every layout holds (INTER / AC: 2
+   * padding entries, MID: the padding line, GRP: the padding entry); on the
+   * AltCounters layouts ac_clamp's bound, block ceil(n+1 / d) + 1 */
+  const uint64_t d = di->d;
+  const uint64_t cap = (di->layout == LAY_AC || di->layout == LAY_MIDAC)
+                           ? ((di->bwtsize + d - 1) / d + 2) * d - 1
+                           : ((uint64_t) di->nentries + 1) * d - 1;
+  ix.lf_cap = (uint32_t) std::min<uint64_t>(cap, 0xFFFFFFFFull);
   return ix;
 }
 

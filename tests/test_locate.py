@@ -377,3 +377,45 @@ def test_walk_check_modes_agree_on_corrupted_counters(gpu, tmp_path):
     finally:
         K.set_walk_check(0)
     assert verdicts.get("refused", 0) > 0, verdicts
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("backend", ["task", "coop", "task-mid", "coop-mid", "task-ac", "task-ac-mid"])
+def test_corrupt_counters_stay_in_table(gpu, backend):
+    """A loaded file with wrapped or oversized counters (every counter of some
+    entries set to 0xFFFFFFFF, 2^31 or a random u32): the LF steps' results
+    are capped at the last row of the last block the layout holds
+    (IdxArgs::lf_cap; ac_clamp on the AltCounters layouts), so every search
+    stays inside the table -- it returns, with some intervals, and the same
+    batch on the intact file still equals the oracle."""
+    from oracle import oracle
+    K = gpu
+    rng = np.random.default_rng(91)
+    t = rng.choice(ACGT, size=40_001)
+    src = K.Index.build(t.tobytes(), k=2, d=64, gpu=False)
+    img = np.array(src.image(), dtype=np.uint8, copy=True)
+    src.close()
+    h = oracle.header(img)
+    k, d, ne = h["steps"], h["chunk"], h["nentries"]
+    nb = d // 32
+    ew = 2 * nb * k + 4 ** k
+    q = np.concatenate([t[rng.integers(0, t.size - 60, size=1500)[:, None] + np.arange(60)],
+                        rng.choice(ACGT, size=(500, 60))])
+    good = K.Index.from_image(img)
+    want_img = good.alt_counters()[0].image() if "ac" in backend else img
+    assert np.array_equal(K.search_array(good, q, backend), oracle.search(want_img, q)[0])
+    good.close()
+    for how in ("ones", "high", "random"):
+        bad = img.copy()
+        ent = bad[bad.size - 4 * ew * ne:].view(np.uint32).reshape(ne, ew)
+        rows = rng.choice(ne, size=max(1, ne // 8), replace=False)
+        if how == "ones":
+            ent[rows, 2 * nb * k:] = 0xFFFFFFFF
+        elif how == "high":
+            ent[rows, 2 * nb * k:] = 0x80000000
+        else:
+            ent[rows, 2 * nb * k:] = rng.integers(0, 1 << 32, size=(rows.size, 4 ** k), dtype=np.uint64).astype(np.uint32)
+        idx = K.Index.from_image(bad)
+        got = K.search_array(idx, q, backend)
+        assert got.shape == (2 * q.shape[0],)
+        idx.close()
