@@ -302,6 +302,66 @@ int main(int argc, char **argv)
     freeQueries(&qs);
   }
 
+  /* 9b. damaged bodies: every tag's image with 1-16 entry words (counters or
+   *     bit planes) replaced by 0, 0xFFFFFFFF, 2^31 or a random word -- every
+   *     such file loads, and the host search and the transforms stay inside
+   *     their buffers whatever the counters say (cs_lf's padding entry) */
+  {
+    void *qs = NULL;
+    uint32_t lcg = 4242u + k * 13u + d;
+    snprintf(q, sizeof q, "%s/%s/q%u.qry", g, cs, m);
+    CHECK(loadQueries(q, m, num < 64 ? num : 64, &qs) == 0, "body fuzz queries");
+    for (tag = 100; tag <= 201; tag += (tag == 101 ? 99 : 1)) {
+      size_t len = 0;
+      unsigned char *img;
+      uint32_t trial, loaded = 0;
+      snprintf(p, sizeof p, "%s/%s/k%u_d%u.%u.fmi", g, cs, k, d, tag);
+      img = slurp(p, &len);
+      CHECK(img != NULL, "body fuzz image %u", tag);
+      if (!img) continue;
+      for (trial = 0; trial < 300; trial++) {
+        const uint32_t steps = ((uint32_t *) img)[1];
+        const uint64_t hw = 6 + 2 * steps, words = len / 4;
+        unsigned char *b = (unsigned char *) malloc(len);
+        uint32_t *w = (uint32_t *) b, nw, j;
+        void *x = NULL, *y = NULL, *z = NULL, *rs = NULL;
+        memcpy(b, img, len);
+        lcg = lcg * 1664525u + 1013904223u;
+        nw = 1 + (lcg >> 12) % 16u;
+        for (j = 0; j < nw && words > hw; j++) {
+          uint32_t val;
+          lcg = lcg * 1664525u + 1013904223u;
+          switch ((lcg >> 4) % 4) {
+            case 0: val = 0; break;
+            case 1: val = 0xFFFFFFFFu; break;
+            case 2: val = 0x80000000u; break;
+            default: val = lcg * 2654435761u; break;
+          }
+          lcg = lcg * 1664525u + 1013904223u;
+          w[hw + (lcg >> 3) % (words - hw)] = val;
+        }
+        if (kfmi_index_from_image(b, len, &x) == 0) {
+          loaded++;
+          if (initResults(num < 64 ? num : 64, &rs) == 0) {
+            (void) kfmi_search_cpu(x, qs, rs, 2);
+            freeResults(&rs);
+          }
+          if (tag == 100) {
+            if (kfmi_transform_interleave(x, &y) == 0) freeIndex(&y);
+            if (kfmi_transform_ac(x, &y, &z) == 0) { freeIndex(&y); freeIndex(&z); }
+          } else if (tag >= 200 && kfmi_transform_plain(x, &y) == 0) {
+            freeIndex(&y);
+          }
+          freeIndex(&x);
+        }
+        free(b);
+      }
+      CHECK(loaded == 300, "body fuzz: every damaged %u body loads (%u)", tag, loaded);
+      free(img);
+    }
+    freeQueries(&qs);
+  }
+
   /* 10. damaged text files: random bytes drawn mostly from ">\n\rACGTN" (and
    *     any byte now and then), 0-5000 of them, through loadQueries, loadRef
    *     and loadResults with random sizes -- each either fails or returns a

@@ -216,3 +216,37 @@ def test_large_image_on_2mb_pages(kfmi_mod, oracle_mod, monkeypatch, tmp_path):
         del img
         I.close()
     assert np.array_equal(res["1"], res["0"])
+
+
+@pytest.mark.parametrize("form", ["plain", "ac"])
+def test_cpu_search_on_corrupt_counters_stays_in_image(kfmi_mod, oracle_mod, form):
+    """searchIndexCPU (the product's host search) on a file whose counters are
+    wrapped or oversized (0xFFFFFFFF, 2^31, random u32 on an eighth of the
+    entries): a step landing past the last entry reads the padding entry's
+    end counters (cs_lf), so the search returns instead of reading past the
+    image -- the host side of the GPU kernels' LF cap."""
+    K = kfmi_mod
+    rng = np.random.default_rng(92)
+    t = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=20_001)
+    src = K.Index.build(t.tobytes(), k=2, d=64)
+    img = np.array(src.image(), dtype=np.uint8, copy=True)
+    src.close()
+    h = oracle_mod.header(img)
+    k, d, ne = h["steps"], h["chunk"], h["nentries"]
+    nb = d // 32
+    ew = 2 * nb * k + 4 ** k
+    q = np.concatenate([t[rng.integers(0, t.size - 40, size=300)[:, None] + np.arange(40)],
+                        rng.choice(np.frombuffer(b"ACGT", np.uint8), size=(100, 40))])
+    for how in ("ones", "high", "random"):
+        bad = img.copy()
+        ent = bad[bad.size - 4 * ew * ne:].view(np.uint32).reshape(ne, ew)
+        rows = rng.choice(ne, size=max(1, ne // 8), replace=False)
+        vals = {"ones": 0xFFFFFFFF, "high": 0x80000000}.get(how)
+        ent[rows, 2 * nb * k:] = (vals if vals is not None else
+                                  rng.integers(0, 1 << 32, size=(rows.size, 4 ** k), dtype=np.uint64).astype(np.uint32))
+        idx = K.Index.from_image(bad)
+        if form == "ac":
+            idx = idx.alt_counters()[0]
+        got = K.search_cpu_array(idx, q, nthreads=2)
+        assert got.shape == (2 * q.shape[0],)
+        idx.close()
